@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s + frames/s of raytrace_tris on the dragon-class config.
+
+Workload (BASELINE.json configs[3], the metric's config): 871,414-triangle
+synthetic mesh (dragon class), 1920x1080, sampleRate 16 (256 spp, one launch,
+progression 0), maxDepth 6, plymain.cpp lights and camera, BVH traversal.
+One step = one full frame: every rank renders its interleaved row stripes (rt_tile) and,
+for N > 1, the frame is gathered to rank 0 over RCCL (torch.distributed "nccl").
+A ray = one closest-hit or one any-hit (shadow) query, counted on the device.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a `roofline` object for
+the triangle kernel (algorithmic bytes from the device traversal counters / HIP-event kernel
+time) and a `cpu_baseline` object (the CPU oracle, bit-identical restatement of the reference
+kernel, on a bounded pixel sample, rank 0 at N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+NODE_BYTES = 64  # one BVH node (both child boxes + links), csrc/rt_internal.h
+TRI_BYTES = 48   # one triangle record (v0+orig, e1, e2 as float4), csrc/rt_internal.h
+PIXEL_BYTES = 16 + 8 + 8  # RGBA32F store + seed read + seed write per pixel
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="dragon", choices=["dragon", "bunny", "lucy", "spheres"])
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--sample-rate", type=int, default=None)
+    ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = local_rank if world > 1 else 0
+    torch.cuda.set_device(device)
+
+    import ptload
+
+    pt = ptload.load()
+    sc = pt.scenes
+    ptdist = ptload.submodule("dist")
+
+    cfg = args.config
+    if cfg == "spheres":
+        W, H, sr, kernel = 1024, 1024, 1, pt.RayTracer.KERNEL_SPHERES
+        n_tris = 0
+    else:
+        W, H = (1920, 1080) if cfg == "dragon" else ((1024, 1024) if cfg == "bunny" else (4096, 4096))
+        sr = 16 if cfg == "dragon" else (1 if cfg == "bunny" else 4)
+        n_tris = sc.MESH_CONFIGS[cfg]
+        kernel = pt.RayTracer.KERNEL_TRIS
+    W = args.width or W
+    H = args.height or H
+    sr = args.sample_rate or sr
+
+    rt = pt.RayTracer(device)
+    S = sc.ply_scene() if kernel == pt.RayTracer.KERNEL_TRIS else sc.main_scene()
+    rt.setSpheres(S)
+    cam_setup = sc.PLY_CAMERA if kernel == pt.RayTracer.KERNEL_TRIS else sc.MAIN_CAMERA
+    rt.setCameraSpherical(cam_setup["target"], cam_setup["elevation"], cam_setup["azimuth"], cam_setup["distance"])
+    rt.setFoVAngle(sc.DEFAULT_FOV)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setTraversal(args.linear)
+    mesh_info = {}
+    if n_tris:
+        t0 = time.time()
+        verts, idx = sc.make_mesh(n_tris)
+        t1 = time.time()
+        rt.setMesh(verts, idx)
+        mesh_info = rt.meshInfo()
+        mesh_info["gen_seconds"] = round(t1 - t0, 3)
+
+    n_ranks = world
+    tile = (args.stripe, n_ranks, rank) if n_ranks > 1 else None
+    rows = ptdist.max_tile_rows(H, args.stripe, n_ranks) if n_ranks > 1 else H
+    out = torch.zeros(rows * W * 4, dtype=torch.float32, device=f"cuda:{device}")
+
+    def step():
+        rt.rayTrace(out, W, H, 0, kernel=kernel, tile=tile)
+        c = rt.counters()
+        if n_ranks > 1:
+            ptdist.gather_frame(out, H, W, args.stripe)
+        return c["rays_closest"] + c["rays_shadow"]
+
+    # first render creates the seed layout; snapshot it so the counting launch and the
+    # first timed frame see the same seeds
+    step()
+    Wp, Hp = sc.padded_dims(W, H)
+    seeds0 = rt.getSeeds()
+    # counting launch (untimed): traversal node / triangle-test counts for the roofline
+    rt.setCounting(True)
+    rt.setSeeds(Wp, Hp, seeds0)
+    rt.rayTrace(out, W, H, 0, kernel=kernel, tile=tile)
+    cnt = rt.counters()
+    rt.setCounting(False)
+    rt.setSeeds(Wp, Hp, seeds0)
+
+    for _ in range(args.warmup):
+        step()
+
+    kernel_ms = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rays = 0
+    for _ in range(args.steps):
+        rays += step()
+        kernel_ms.append(rt.lastKernelMs())
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays = int(r.item())
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    steps = args.steps
+    mrays = rays / elapsed / 1e6
+    ms_step = elapsed / steps * 1e3
+    # roofline of the dominant kernel, per launch (rank 0's launches)
+    k_ms = float(np.mean(kernel_ms))
+    rays_cnt = cnt["rays_closest"] + cnt["rays_shadow"]
+    pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0)) if n_ranks > 1 else H)
+    if kernel == pt.RayTracer.KERNEL_TRIS:
+        alg_bytes = cnt["nodes_visited"] * NODE_BYTES + cnt["tris_tested"] * TRI_BYTES + pix * PIXEL_BYTES
+    else:
+        alg_bytes = pix * PIXEL_BYTES
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_tris<BVH>" if kernel == 2 and not args.linear else ("k_tris<LINEAR>" if kernel == 2 else "k_spheres"),
+                "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
+                "nodes_per_ray": round(cnt["nodes_visited"] / max(rays_cnt, 1), 2),
+                "tris_per_ray": round(cnt["tris_tested"] / max(rays_cnt, 1), 2)}
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds0, Wp, Hp, kernel, args.cpu_seconds,
+                           verts if n_tris else None, idx if n_tris else None)
+
+    line = {
+        "metric": METRIC,
+        "value": round(mrays, 2),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "frames_per_sec": round(steps / elapsed, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"raytrace_tris {cfg}-class synthetic mesh {n_tris} tris, {W}x{H}, "
+                               f"sampleRate {sr} ({sr * sr} spp, one launch), maxDepth 6, "
+                               f"{'linear' if args.linear else 'BVH'} traversal" if n_tris else
+                               f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}",
+                   "W": W, "H": H, "spp": sr * sr, "n_tris": n_tris,
+                   "parallelism": f"row-stripes({args.stripe})x{world}" + (" + rccl gather" if world > 1 else ""),
+                   "rays_per_frame": int(rays / steps), "mesh": mesh_info},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, verts, idx):
+    """The CPU oracle (bit-identical restatement of the reference kernel, oracle/pt_oracle.c)
+    on a bounded sample of the same frame: one full pixel (all sr*sr samples) per thread,
+    pixels strided over the frame; rays counted by the oracle."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    from oracle import Oracle
+
+    orc = Oracle()
+    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+    cam = sc.camera_spherical(W, **(sc.PLY_CAMERA if kernel == 2 else sc.MAIN_CAMERA))
+    out = np.zeros(W * H * 4, np.float32)
+    sd = seeds.copy()
+    if kernel == 2:
+        n_px = threads
+        pix = (np.arange(n_px, dtype=np.uint64) * (W * H // n_px) + (W * H // (2 * n_px))).astype(np.uint32)
+        t0 = time.perf_counter()
+        closest, shadow = orc.render_tris(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix,
+                                          nthreads=threads)
+        dt = time.perf_counter() - t0
+        sample = f"{n_px} pixels x {sr * sr} samples (strided over the frame), linear traversal (reference algorithm)"
+    else:
+        t0 = time.perf_counter()
+        closest, shadow = orc.render_spheres(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, nthreads=threads)
+        dt = time.perf_counter() - t0
+        sample = f"full {W}x{H} frame"
+    rays = closest + shadow
+    return {"value": round(rays / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": sample, "seconds": round(dt, 2), "rays": int(rays)}
+
+
+if __name__ == "__main__":
+    main()

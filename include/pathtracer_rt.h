@@ -1,0 +1,156 @@
+/*
+ * pathtracer_rt.h — C-ABI drop-in boundary of the MI355X path tracer
+ * (librtmi.so, built from pathtracer.cl_amd/csrc).
+ *
+ * It replaces the OpenCL host RayTracerCL (clrt/RayTracerCL.{h,cpp}) and the
+ * device-agnostic RayTracer API (clrt/RayTracer.{h,cpp}) for the per-pixel
+ * path-tracing kernels of clrt/ocl/raytracer.cl.  Plain pointers and sizes,
+ * int status codes, no exceptions and no HIP/torch types in any signature.
+ * One context per GPU; a context is not thread-safe (the reference is driven
+ * from one GLUT thread, clrt/GlutCLWindow.cpp:136-227).
+ *
+ * Each entry point names the reference interface it replaces.
+ */
+#ifndef PATHTRACER_RT_H
+#define PATHTRACER_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rt_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rt_ctx rt_ctx;
+
+/* Status codes (the reference throws cl::Error, RayTracerCL.cpp:102-107, :297-303). */
+enum {
+    RT_OK = 0,
+    RT_ERR_ARG = -1,      /* bad argument (null pointer, zero size, out of range) */
+    RT_ERR_HIP = -2,      /* a HIP runtime call failed; see rt_last_error() */
+    RT_ERR_NO_SCENE = -3, /* render requested with no spheres set */
+    RT_ERR_NO_MESH = -4,  /* triangle kernel requested with no mesh set */
+    RT_ERR_ALLOC = -5,    /* host or device allocation failed */
+    RT_ERR_STATE = -6,    /* inconsistent state (e.g. seed layout smaller than the frame) */
+    RT_ERR_LIMIT = -7     /* input exceeds a device limit (e.g. BVH deeper than the traversal stack) */
+};
+
+/* Kernels of clrt/ocl/raytracer.cl. */
+enum {
+    RT_KERNEL_SPHERES = 0,    /* raytrace      raytracer.cl:46-104  (row-shifted seeds, sampleRate^2 samples) */
+    RT_KERNEL_SPHERES_SS = 1, /* raytrace_ss   raytracer.cl:120-166 (one sample, unshifted seeds) */
+    RT_KERNEL_TRIS = 2        /* raytrace_tris raytracer.cl:184-243 (mesh lit by the emissive spheres) */
+};
+
+/* Triangle traversal: the reference's linear loop (rtcommon.h:39-68) or the BVH
+   (identical results: closest hit = minimum t, ties to the highest index). */
+enum { RT_TRAVERSAL_BVH = 0, RT_TRAVERSAL_LINEAR = 1 };
+
+/* rt_render flags */
+enum {
+    RT_OUT_DEVICE = 1 /* `out` is a device pointer on the context's GPU (else host memory) */
+};
+
+/* Row-stripe tile of the frame owned by one rank (multi-GPU sharding).
+   Rows y with (y / stripe_rows) % n_ranks == rank are rendered, compacted in
+   increasing y into `out` (rt_tile_rows() rows of W pixels).  Seeds are always
+   indexed in the global padded frame (raytracer.cl:207-209).  NULL = full frame. */
+typedef struct rt_tile {
+    uint32_t stripe_rows;
+    uint32_t n_ranks;
+    uint32_t rank;
+} rt_tile;
+
+/* Ray accounting: one closest-hit query or one any-hit (shadow) query = 1 ray. */
+typedef struct rt_counters {
+    uint64_t rays_closest;
+    uint64_t rays_shadow;
+    uint64_t nodes_visited; /* BVH inner nodes fetched (counting launches only) */
+    uint64_t tris_tested;   /* ray/triangle tests (counting launches only) */
+} rt_counters;
+
+/* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */
+int rt_create(int device, rt_ctx **out);
+int rt_destroy(rt_ctx *ctx);
+const char *rt_last_error(const rt_ctx *ctx);
+const char *rt_status_string(int status);
+
+/* ---- scene: RayTracer::addSphere / clearSpheres (RayTracer.cpp:50-63) and the
+   scene upload of RayTracerCL::rayTrace (RayTracerCL.cpp:251-264) ---- */
+int rt_set_spheres(rt_ctx *ctx, const rt_sphere *spheres, uint32_t n);
+
+/* ---- mesh: the tri_verts / tri_vert_idx / n_tris kernel arguments of
+   raytrace_tris (raytracer.cl:184-188); the context builds the BVH. ---- */
+int rt_set_mesh(rt_ctx *ctx, const float *verts_xyz, uint32_t n_verts, const int32_t *idx, uint32_t n_tris);
+/* BVH statistics of the current mesh: nodes, leaves, depth, build seconds. */
+int rt_mesh_info(const rt_ctx *ctx, uint32_t *n_nodes, uint32_t *depth, double *build_seconds);
+
+/* ---- camera: RayTracer::setCameraMatrix / setCameraSpherical / setFoVAngle
+   (RayTracer.h:56-60, RayTracer.cpp:24-47); the Camera struct is derived per
+   frame width exactly as RayTracerCL::updateCLCamera (RayTracerCL.cpp:178-215). ---- */
+int rt_set_view_matrix(rt_ctx *ctx, const float m_colmajor[16]);
+int rt_set_camera_spherical(rt_ctx *ctx, float tx, float ty, float tz, float elevation_deg, float azimuth_deg,
+                            float distance);
+int rt_set_fov(rt_ctx *ctx, float fov_deg);
+/* Explicit Camera override (fixtures); cleared by the three calls above. */
+int rt_set_camera(rt_ctx *ctx, const rt_camera *cam);
+/* Host helper: the Camera the reference would upload for this setup and width. */
+int rt_camera_spherical(float tx, float ty, float tz, float elevation_deg, float azimuth_deg, float distance,
+                        float fov_deg, uint32_t width, rt_camera *out);
+
+/* ---- settings: RayTracer::setSampleRate / setMaxPathDepth (RayTracer.h:62-66) ---- */
+int rt_set_params(rt_ctx *ctx, uint32_t sample_rate, uint32_t max_depth);
+int rt_set_traversal(rt_ctx *ctx, int traversal);
+
+/* ---- RNG seeds: RayTracerCL::updateSeedBuffer (RayTracerCL.cpp:147-171).
+   Work-group height ndY fixes the padded height (RayTracerCL.cpp:114-116,
+   :229-232; 8 = a 256-item work-group on AMD GPUs, the default). ---- */
+int rt_set_ndrange(rt_ctx *ctx, uint32_t nd_y);
+/* Allocate a Wpad x Hpad layout filled from the context's glibc-rand() stream
+   (glibc TYPE_3 random(), default seed 1 — no srand in the reference). */
+int rt_set_seed_layout(rt_ctx *ctx, uint32_t wpad, uint32_t hpad);
+/* Replace the seeds: count == 2 * Wpad * Hpad (x plane then y plane). */
+int rt_set_seeds(rt_ctx *ctx, const uint32_t *seeds, size_t count);
+int rt_get_seeds(const rt_ctx *ctx, uint32_t *out, size_t count);
+int rt_seed_layout(const rt_ctx *ctx, uint32_t *wpad, uint32_t *hpad);
+/* glibc rand() stream restated (tests compare it with libc's own rand()). */
+int rt_glibc_rand_fill(uint32_t seed, uint32_t *out, size_t count, uint32_t skip);
+
+/* ---- render: RayTracerCL::rayTrace(cl_mem*, W, H, progression) (RayTracerCL.cpp:217-307).
+   progression 0 overwrites; p > 0 mixes with weight 1/p (GlutCLWindow.cpp:144-158).
+   Pads the frame, (re)creates seeds on a size change and refreshes the camera
+   exactly as the reference does, then launches and waits (finish()). ---- */
+int rt_render(rt_ctx *ctx, float *out_rgba, uint32_t width, uint32_t height, uint32_t progression, int kernel,
+              const rt_tile *tile, int flags);
+/* Same, enqueued on `hip_stream` (a hipStream_t, or NULL = the context stream), no wait. */
+int rt_render_async(rt_ctx *ctx, float *out_rgba, uint32_t width, uint32_t height, uint32_t progression,
+                    int kernel, const rt_tile *tile, int flags, void *hip_stream);
+int rt_synchronize(rt_ctx *ctx);
+/* Rows of `height` owned by `tile` (NULL: height). */
+uint32_t rt_tile_rows(uint32_t height, const rt_tile *tile);
+
+/* ---- instrumentation ---- */
+int rt_get_counters(const rt_ctx *ctx, rt_counters *out); /* of the last completed render */
+int rt_set_counting(rt_ctx *ctx, int enable);             /* count nodes/tris in the next renders */
+/* Device time of the last render's kernel (HIP events on the launch stream), ms. */
+int rt_last_kernel_ms(const rt_ctx *ctx, float *ms);
+
+/* ---- ray queries for hit-index parity (rtcommon.h:39-52 / :59-68 semantics).
+   Host arrays; any_hit=0: out_idx = closest triangle (-1 none), out_t = its t;
+   any_hit=1: out_idx = 1 if occluded in (tmin, tmax). ---- */
+int rt_trace_rays(rt_ctx *ctx, const rt_ray *rays, uint32_t n, int any_hit, int32_t *out_idx, float *out_t);
+
+/* ---- synthetic meshes (deterministic, host-independent: rt_math.h only) ----
+   A displaced lat-long sphere truncated to exactly n_tris triangles, centred at
+   (cx, cy, cz) with base radius r.  verts must hold rt_mesh_vertex_count(n_tris)
+   xyz triples, idx 3*n_tris ints. */
+uint32_t rt_mesh_vertex_count(uint32_t n_tris);
+int rt_make_mesh(uint32_t n_tris, float cx, float cy, float cz, float r, float *verts_xyz, int32_t *idx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PATHTRACER_RT_H */

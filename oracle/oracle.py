@@ -1,0 +1,157 @@
+"""ctypes binding of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+- `Oracle`     — oracle/liboracle.so, the C restatement of the reference kernel
+                 (oracle/pt_oracle.c).  Used by tests/, __graft_entry__.smoke() and the
+                 cpu_baseline leg of bench.py — never by the product path.
+- `Reference`  — oracle/_ref/libptref.so, the reference's own clrt/ocl/raytracer.cl compiled
+                 for x86-64 (oracle/Makefile `ref`; needs /root/reference, container only).
+
+Both take the same numpy records as librtmi (pathtracer.cl_amd/_abi.py dtypes).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIBORACLE = ORACLE_DIR / "liboracle.so"
+LIBREF = ORACLE_DIR / "_ref" / "libptref.so"
+REFERENCE_ROOT = Path("/root/reference")
+
+KERNEL_SPHERES, KERNEL_SPHERES_SS, KERNEL_TRIS = 0, 1, 2
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [("closest", ctypes.c_uint64), ("shadow", ctypes.c_uint64)]
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def build(ref: bool = False) -> None:
+    """Compile liboracle.so (and, if /root/reference exists and ref=True, oracle/_ref)."""
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+    if ref and REFERENCE_ROOT.exists():
+        subprocess.run(["make", "-s", "-C", str(ORACLE_DIR), "ref"], check=True)
+
+
+class Oracle:
+    def __init__(self, path: os.PathLike | None = None):
+        p = Path(path) if path else LIBORACLE
+        if not p.exists():
+            build()
+        self.lib = ctypes.CDLL(str(p))
+        L = self.lib
+        vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+        L.or_render_spheres.argtypes = [vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32, vp, i32, i32, vp]
+        L.or_render_spheres.restype = i32
+        L.or_render_tris.argtypes = [vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32, vp, vp, vp, u32, vp, u32,
+                                     u32, i32, vp]
+        L.or_render_tris.restype = i32
+        L.or_closest_hits.argtypes = [vp, u32, vp, vp, u32, vp, vp]
+        L.or_any_hits.argtypes = [vp, u32, vp, vp, u32, vp]
+        for f in ("sin", "cos", "exp", "log"):
+            fn = getattr(L, f"or_math_{f}")
+            fn.argtypes = [ctypes.c_float]
+            fn.restype = ctypes.c_float
+        L.or_math_pow.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.or_math_pow.restype = ctypes.c_float
+
+    def render_spheres(self, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds,
+                       single_sample=False, nthreads=None):
+        c = Counters()
+        nthreads = nthreads or min(os.cpu_count() or 1, 16)
+        st = self.lib.or_render_spheres(_p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad, sample_rate,
+                                        max_depth, progressive, _p(seeds), int(single_sample), nthreads,
+                                        ctypes.byref(c))
+        assert st == 0
+        return c.closest, c.shadow
+
+    def render_tris(self, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds, verts,
+                    idx, pixels=None, max_samples=0, nthreads=None):
+        c = Counters()
+        nthreads = nthreads or min(os.cpu_count() or 1, 16)
+        n_tris = idx.size // 3
+        npx = 0 if pixels is None else len(pixels)
+        st = self.lib.or_render_tris(_p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad, sample_rate,
+                                     max_depth, progressive, _p(seeds), _p(verts), _p(idx), n_tris, _p(pixels), npx,
+                                     max_samples, nthreads, ctypes.byref(c))
+        assert st == 0
+        return c.closest, c.shadow
+
+    def closest_hits(self, rays, verts, idx):
+        n = len(rays)
+        oi = np.empty(n, np.int32)
+        ot = np.empty(n, np.float32)
+        self.lib.or_closest_hits(_p(rays), n, _p(verts), _p(idx), idx.size // 3, _p(oi), _p(ot))
+        return oi, ot
+
+    def any_hits(self, rays, verts, idx):
+        n = len(rays)
+        oi = np.empty(n, np.int32)
+        self.lib.or_any_hits(_p(rays), n, _p(verts), _p(idx), idx.size // 3, _p(oi))
+        return oi
+
+
+class Reference:
+    """The reference kernel itself (clrt/ocl/raytracer.cl compiled for x86-64) + KAT wrappers."""
+
+    def __init__(self):
+        if not LIBREF.exists():
+            build(ref=True)
+        if not LIBREF.exists():
+            raise FileNotFoundError(f"{LIBREF} (needs /root/reference to build)")
+        self.lib = ctypes.CDLL(str(LIBREF))
+        L = self.lib
+        vp, u32, i32, f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
+        L.ref_launch_kernel.argtypes = [i32, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32, vp, vp, vp, u32, i32]
+        L.ref_launch_kernel.restype = i32
+        L.ref_camera_spherical.argtypes = [f32, f32, f32, f32, f32, f32, f32, u32, vp]
+        L.ref_frand_seq.argtypes = [vp, vp, u32]
+        L.ref_strat_seq.argtypes = [vp, vp, u32, i32]
+        L.ref_intersect_sphere.argtypes = [vp, vp, f32]
+        L.ref_intersect_sphere.restype = f32
+        L.ref_intersects_box.argtypes = [vp, f32, f32, f32]
+        L.ref_intersects_box.restype = f32
+        L.ref_box_normal.argtypes = [vp, vp, f32, f32, f32]
+        L.ref_intersects_triangle.argtypes = [vp, vp, vp, vp]
+        L.ref_intersects_triangle.restype = i32
+        L.ref_intersects_triangle_p.argtypes = [vp, vp]
+        L.ref_intersects_triangle_p.restype = i32
+        L.ref_sphere_emissive.argtypes = [vp, vp, f32, f32, f32]
+        L.ref_sample_material.argtypes = [vp, vp, vp, vp]
+        L.ref_sample_material.restype = i32
+        L.ref_closest_hits.argtypes = [vp, u32, vp, vp, u32, vp, vp]
+        L.ref_any_hits.argtypes = [vp, u32, vp, vp, u32, vp]
+
+    def launch(self, kernel, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds,
+               verts=None, idx=None, nthreads=8):
+        n_tris = 0 if idx is None else idx.size // 3
+        st = self.lib.ref_launch_kernel(kernel, _p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad,
+                                        sample_rate, max_depth, progressive, _p(seeds), _p(verts), _p(idx), n_tris,
+                                        nthreads)
+        assert st == 0
+
+    def camera_spherical(self, width, target, elevation, azimuth, distance, fov=53.0):
+        cam = np.zeros(16, np.float32)
+        self.lib.ref_camera_spherical(*[float(t) for t in target], float(elevation), float(azimuth), float(distance),
+                                      float(fov), int(width), _p(cam))
+        return cam
+
+    def closest_hits(self, rays, verts, idx):
+        n = len(rays)
+        oi = np.empty(n, np.int32)
+        ot = np.empty(n, np.float32)
+        self.lib.ref_closest_hits(_p(rays), n, _p(verts), _p(idx), idx.size // 3, _p(oi), _p(ot))
+        return oi, ot
+
+    def any_hits(self, rays, verts, idx):
+        n = len(rays)
+        oi = np.empty(n, np.int32)
+        self.lib.ref_any_hits(_p(rays), n, _p(verts), _p(idx), idx.size // 3, _p(oi))
+        return oi

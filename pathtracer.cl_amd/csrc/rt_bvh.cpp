@@ -1,0 +1,357 @@
+/*
+ * rt_bvh.cpp — host BVH builder for the triangle kernel.
+ *
+ * The reference has no acceleration structure: every ray scans all triangles
+ * (clrt/ocl/rtcommon.h:39-68).  This binary BVH changes only which triangles a
+ * ray tests, never how: leaves hold the reference's triangle_t (v0, e1, e2;
+ * rtcommon.h:20-37) with the edges precomputed by the same float subtraction,
+ * and the kernel's accept rule reproduces the linear loop's result exactly
+ * (minimum t, ties to the highest original index).  Culling must therefore be
+ * conservative: every triangle box is padded beyond the rounding slack of the
+ * Moller-Trumbore test (see DESIGN.md "BVH contract").
+ *
+ * Binned SAH (16 bins over centroid bounds) with a depth budget: when the
+ * remaining levels would only just fit a balanced tree under
+ * RT_BVH_MAX_DEPTH, the split falls back to an object median, so inner depth
+ * never exceeds RT_STACK_DEPTH (the LDS traversal stack).
+ */
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace {
+
+struct Box {
+    float lo[3], hi[3];
+    void reset()
+    {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = INFINITY;
+            hi[k] = -INFINITY;
+        }
+    }
+    void grow(const Box &b)
+    {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    void grow(const float *p)
+    {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    float area() const
+    {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (!(dx >= 0.0f) || !(dy >= 0.0f) || !(dz >= 0.0f)) return 0.0f;
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct TmpNode {
+    Box box;
+    int left = -1, right = -1; /* TmpNode indices, or -1 for a leaf */
+    uint32_t first = 0, count = 0;
+};
+
+struct Builder {
+    const float *verts;
+    const int32_t *idx;
+    std::vector<Box> tbox;     /* padded triangle boxes */
+    std::vector<float> cent;   /* centroids, 3 per triangle */
+    std::vector<uint32_t> perm;
+    std::vector<TmpNode> nodes;
+    uint32_t max_depth_seen = 0;
+
+    static int ceil_log2(uint32_t v)
+    {
+        int l = 0;
+        while ((1u << l) < v && l < 31) ++l;
+        return l;
+    }
+
+    /* Levels a balanced (median) tree over n triangles needs below this node. */
+    static int balanced_levels(uint32_t n)
+    {
+        uint32_t leaves = (n + RT_LEAF_MAX - 1) / RT_LEAF_MAX;
+        return ceil_log2(leaves);
+    }
+
+    Box bounds(uint32_t first, uint32_t count) const
+    {
+        Box b;
+        b.reset();
+        for (uint32_t i = first; i < first + count; ++i) b.grow(tbox[perm[i]]);
+        return b;
+    }
+
+    /* Splits [first, first+count) and returns the number in the left part, or
+       0 to make a leaf. */
+    uint32_t split(uint32_t first, uint32_t count, const Box &nb, uint32_t depth)
+    {
+        if (count <= 1) return 0;
+        Box cb;
+        cb.reset();
+        for (uint32_t i = first; i < first + count; ++i) cb.grow(&cent[3 * perm[i]]);
+        int axis = 0;
+        float ext[3];
+        for (int k = 0; k < 3; ++k) ext[k] = cb.hi[k] - cb.lo[k];
+        if (ext[1] > ext[axis]) axis = 1;
+        if (ext[2] > ext[axis]) axis = 2;
+
+        const bool must_median =
+            (int)depth + balanced_levels(count) >= RT_BVH_MAX_DEPTH - 1 || ext[axis] <= 0.0f;
+        if (!must_median) {
+            constexpr int B = 16;
+            float best_cost = INFINITY;
+            int best_axis = -1, best_bin = -1;
+            for (int k = 0; k < 3; ++k) {
+                if (!(ext[k] > 0.0f)) continue;
+                Box bb[B];
+                uint32_t bn[B];
+                for (int b = 0; b < B; ++b) {
+                    bb[b].reset();
+                    bn[b] = 0;
+                }
+                const float scale = (float)B / ext[k];
+                for (uint32_t i = first; i < first + count; ++i) {
+                    const uint32_t t = perm[i];
+                    int b = (int)((cent[3 * t + k] - cb.lo[k]) * scale);
+                    b = std::min(std::max(b, 0), B - 1);
+                    bb[b].grow(tbox[t]);
+                    bn[b]++;
+                }
+                float left_area[B];
+                uint32_t left_n[B];
+                Box acc;
+                acc.reset();
+                uint32_t n = 0;
+                for (int b = 0; b < B - 1; ++b) {
+                    acc.grow(bb[b]);
+                    n += bn[b];
+                    left_area[b] = acc.area();
+                    left_n[b] = n;
+                }
+                acc.reset();
+                n = 0;
+                for (int b = B - 1; b > 0; --b) {
+                    acc.grow(bb[b]);
+                    n += bn[b];
+                    const uint32_t ln = left_n[b - 1];
+                    if (ln == 0 || n == 0) continue;
+                    const float cost = left_area[b - 1] * (float)ln + acc.area() * (float)n;
+                    if (cost < best_cost) {
+                        best_cost = cost;
+                        best_axis = k;
+                        best_bin = b;
+                    }
+                }
+            }
+            const float parent_area = nb.area();
+            /* SAH: traversal cost 1, triangle cost 1 (relative to the parent) */
+            const float leaf_cost = (float)count;
+            const float split_cost = 1.0f + (parent_area > 0.0f ? best_cost / parent_area : INFINITY);
+            if (count <= RT_LEAF_MAX && !(split_cost < leaf_cost)) return 0;
+            if (best_axis >= 0) {
+                const float scale = (float)B / ext[best_axis];
+                uint32_t *lo = perm.data() + first;
+                uint32_t *hi = lo + count;
+                uint32_t *mid = std::partition(lo, hi, [&](uint32_t t) {
+                    int b = (int)((cent[3 * t + best_axis] - cb.lo[best_axis]) * scale);
+                    b = std::min(std::max(b, 0), B - 1);
+                    return b < best_bin;
+                });
+                const uint32_t nl = (uint32_t)(mid - lo);
+                if (nl > 0 && nl < count) return nl;
+            }
+        }
+        if (count <= RT_LEAF_MAX) return 0;
+        /* object median along the widest centroid axis (ties broken by index) */
+        const uint32_t half = count / 2;
+        uint32_t *lo = perm.data() + first;
+        std::nth_element(lo, lo + half, lo + count, [&](uint32_t a, uint32_t b) {
+            const float ca = cent[3 * a + axis], cb2 = cent[3 * b + axis];
+            return ca < cb2 || (ca == cb2 && a < b);
+        });
+        return half;
+    }
+
+    /* Recursive build; returns the TmpNode index. */
+    int build(uint32_t first, uint32_t count, uint32_t depth)
+    {
+        const int id = (int)nodes.size();
+        nodes.emplace_back();
+        nodes[id].box = bounds(first, count);
+        nodes[id].first = first;
+        nodes[id].count = count;
+        if (depth > max_depth_seen) max_depth_seen = depth;
+        const uint32_t nl = split(first, count, nodes[id].box, depth);
+        if (nl == 0) return id; /* leaf */
+        const int l = build(first, nl, depth + 1);
+        const int r = build(first + nl, count - nl, depth + 1);
+        nodes[id].left = l;
+        nodes[id].right = r;
+        return id;
+    }
+};
+
+int32_t leaf_code(uint32_t first, uint32_t count) { return ~(int32_t)((first << 3) | (count - 1)); }
+
+} // namespace
+
+bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtBvh &out,
+                  std::string &err)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!verts || !idx || n_tris == 0 || n_verts == 0) {
+        err = "empty mesh";
+        return false;
+    }
+    if (n_tris >= (1u << 28)) {
+        err = "too many triangles (leaf encoding holds 2^28)";
+        return false;
+    }
+    for (uint64_t i = 0; i < 3ull * n_verts; ++i) {
+        if (!std::isfinite(verts[i]) || std::fabs(verts[i]) > 1e15f) {
+            err = "non-finite or out-of-range vertex coordinate";
+            return false;
+        }
+    }
+    for (uint64_t i = 0; i < 3ull * n_tris; ++i) {
+        if (idx[i] < 0 || (uint32_t)idx[i] >= n_verts) {
+            err = "vertex index out of range";
+            return false;
+        }
+    }
+
+    Builder b;
+    b.verts = verts;
+    b.idx = idx;
+    b.tbox.resize(n_tris);
+    b.cent.resize(3ull * n_tris);
+    b.perm.resize(n_tris);
+    for (uint32_t t = 0; t < n_tris; ++t) {
+        Box bx;
+        bx.reset();
+        float maxabs = 0.0f;
+        for (int k = 0; k < 3; ++k) {
+            const float *p = verts + 3ull * (uint32_t)idx[3ull * t + k];
+            bx.grow(p);
+            for (int c = 0; c < 3; ++c) maxabs = std::max(maxabs, std::fabs(p[c]));
+        }
+        float ext = 0.0f;
+        for (int c = 0; c < 3; ++c) ext = std::max(ext, bx.hi[c] - bx.lo[c]);
+        /* culling pad: beyond the Moller-Trumbore rounding slack */
+        const float pad = ext * (1.0f / 512.0f) + 1e-6f * (1.0f + maxabs);
+        for (int c = 0; c < 3; ++c) {
+            b.cent[3ull * t + c] = 0.5f * (bx.lo[c] + bx.hi[c]);
+            bx.lo[c] -= pad;
+            bx.hi[c] += pad;
+        }
+        b.tbox[t] = bx;
+        b.perm[t] = t;
+    }
+    b.nodes.reserve(2ull * n_tris / RT_LEAF_MAX + 16);
+    const int root = b.build(0, n_tris, 1);
+
+    /* Flatten: inner nodes in DFS preorder, each storing both children's boxes. */
+    std::vector<int> order; /* TmpNode index per output inner node */
+    std::vector<int> out_index(b.nodes.size(), -1);
+    uint32_t n_leaves = 0;
+    if (b.nodes[root].left < 0) {
+        /* a single leaf: give it an inner root whose two children are that leaf */
+        out.n_nodes = 1;
+        out.nodes.assign(16, 0.0f);
+        const Box &bx = b.nodes[root].box;
+        float *n = out.nodes.data();
+        n[0] = bx.lo[0]; n[1] = bx.hi[0]; n[2] = bx.lo[1]; n[3] = bx.hi[1];
+        n[4] = bx.lo[0]; n[5] = bx.hi[0]; n[6] = bx.lo[1]; n[7] = bx.hi[1];
+        n[8] = bx.lo[2]; n[9] = bx.hi[2]; n[10] = bx.lo[2]; n[11] = bx.hi[2];
+        const int32_t code = leaf_code(0, n_tris);
+        std::memcpy(&n[12], &code, 4);
+        std::memcpy(&n[13], &code, 4);
+        n_leaves = 1;
+        out.depth = 1;
+    } else {
+        std::vector<int> stack;
+        stack.push_back(root);
+        while (!stack.empty()) {
+            const int id = stack.back();
+            stack.pop_back();
+            out_index[id] = (int)order.size();
+            order.push_back(id);
+            const TmpNode &nd = b.nodes[id];
+            /* push right first so the left child follows its parent */
+            if (b.nodes[nd.right].left >= 0) stack.push_back(nd.right);
+            if (b.nodes[nd.left].left >= 0) stack.push_back(nd.left);
+        }
+        out.n_nodes = (uint32_t)order.size();
+        out.nodes.assign(16ull * out.n_nodes, 0.0f);
+        for (uint32_t i = 0; i < out.n_nodes; ++i) {
+            const TmpNode &nd = b.nodes[order[i]];
+            const TmpNode &l = b.nodes[nd.left];
+            const TmpNode &r = b.nodes[nd.right];
+            float *n = out.nodes.data() + 16ull * i;
+            n[0] = l.box.lo[0]; n[1] = l.box.hi[0]; n[2] = l.box.lo[1]; n[3] = l.box.hi[1];
+            n[4] = r.box.lo[0]; n[5] = r.box.hi[0]; n[6] = r.box.lo[1]; n[7] = r.box.hi[1];
+            n[8] = l.box.lo[2]; n[9] = l.box.hi[2]; n[10] = r.box.lo[2]; n[11] = r.box.hi[2];
+            int32_t c0, c1;
+            if (l.left >= 0) c0 = out_index[nd.left];
+            else { c0 = leaf_code(l.first, l.count); ++n_leaves; }
+            if (r.left >= 0) c1 = out_index[nd.right];
+            else { c1 = leaf_code(r.first, r.count); ++n_leaves; }
+            std::memcpy(&n[12], &c0, 4);
+            std::memcpy(&n[13], &c1, 4);
+        }
+        /* inner depth = depth of the deepest inner node (root = 1) */
+        out.depth = 0;
+        std::vector<std::pair<int, uint32_t>> st;
+        st.push_back({root, 1u});
+        while (!st.empty()) {
+            auto [id, d] = st.back();
+            st.pop_back();
+            const TmpNode &nd = b.nodes[id];
+            if (nd.left < 0) continue;
+            out.depth = std::max(out.depth, d);
+            st.push_back({nd.left, d + 1});
+            st.push_back({nd.right, d + 1});
+        }
+    }
+    out.n_leaves = n_leaves;
+
+    /* Triangles in leaf order: (v0, orig), (e1 = v1 - v0), (e2 = v2 - v0). */
+    out.tris.assign(12ull * n_tris, 0.0f);
+    for (uint32_t s = 0; s < n_tris; ++s) {
+        const uint32_t t = b.perm[s];
+        const float *a = verts + 3ull * (uint32_t)idx[3ull * t];
+        const float *p1 = verts + 3ull * (uint32_t)idx[3ull * t + 1];
+        const float *p2 = verts + 3ull * (uint32_t)idx[3ull * t + 2];
+        float *o = out.tris.data() + 12ull * s;
+        o[0] = a[0];
+        o[1] = a[1];
+        o[2] = a[2];
+        const int32_t orig = (int32_t)t;
+        std::memcpy(&o[3], &orig, 4);
+        o[4] = p1[0] - a[0];
+        o[5] = p1[1] - a[1];
+        o[6] = p1[2] - a[2];
+        o[8] = p2[0] - a[0];
+        o[9] = p2[1] - a[1];
+        o[10] = p2[2] - a[2];
+    }
+    out.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (out.depth > RT_STACK_DEPTH) {
+        err = "BVH deeper than the traversal stack";
+        return false;
+    }
+    return true;
+}

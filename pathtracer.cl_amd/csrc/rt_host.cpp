@@ -1,0 +1,784 @@
+/*
+ * rt_host.cpp — the C-ABI host runtime (librtmi.so), MI355X replacement of
+ * the reference's OpenCL host RayTracerCL (clrt/RayTracerCL.cpp) and of the
+ * device-agnostic RayTracer settings (clrt/RayTracer.cpp).
+ *
+ * Owns per context: the HIP stream and events, the scene (spheres, the
+ * emissive subset for the triangle kernel), the mesh BVH, the seed planes, the
+ * camera derivation and the launch of the kernels in rt_kernels.hip.  There is
+ * no CPU fallback: every render runs the HIP kernels or returns an error.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "pathtracer_rt.h"
+#include "rt_internal.h"
+#include "rt_math.h"
+
+namespace {
+
+/* glibc random() TYPE_3 (the generator behind rand(), seeded with 1 when the
+   program never calls srand — the reference never does).  Published algorithm:
+   r[0] = seed; r[i] = 16807 r[i-1] mod (2^31-1) for i < 31; r[i] = r[i-31]
+   for 31 <= i < 34; then r[i] = r[i-31] + r[i-3] (mod 2^32) and the outputs
+   are r[i] >> 1 from i = 344 on. */
+struct GlibcRand {
+    uint32_t r[34];
+    int k = 0;
+    void seed(uint32_t s)
+    {
+        int32_t w[344 + 34];
+        if (s == 0) s = 1;
+        w[0] = (int32_t)s;
+        for (int i = 1; i < 31; ++i) {
+            const int64_t v = (16807LL * w[i - 1]) % 2147483647LL;
+            w[i] = (int32_t)(v < 0 ? v + 2147483647LL : v);
+        }
+        for (int i = 31; i < 34; ++i) w[i] = w[i - 31];
+        uint32_t u[344];
+        for (int i = 0; i < 34; ++i) u[i] = (uint32_t)w[i];
+        for (int i = 34; i < 344; ++i) u[i] = u[i - 31] + u[i - 3];
+        for (int i = 0; i < 34; ++i) r[i] = u[310 + i]; /* last 34 values, oldest first */
+        k = 0;
+    }
+    uint32_t next()
+    {
+        /* r holds the last 34 values in a ring starting at k (oldest) */
+        const uint32_t v = r[(k + 34 - 31) % 34] + r[(k + 34 - 3) % 34];
+        r[k] = v;
+        k = (k + 1) % 34;
+        return v >> 1;
+    }
+};
+
+const char *hip_str(hipError_t e) { return hipGetErrorString(e); }
+
+constexpr double kPi = 3.14159265358979323846; /* M_PI */
+
+} // namespace
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+
+    /* scene */
+    std::vector<rt_sphere> spheres;
+    std::vector<rt_sphere> lights;
+    rt_sphere *d_spheres = nullptr;
+    rt_sphere *d_lights = nullptr;
+
+    /* mesh */
+    RtBvh bvh;
+    float *d_nodes = nullptr;
+    float *d_tris = nullptr;
+    uint32_t n_tris = 0;
+
+    /* camera state (RayTracer.h:21-29) */
+    float view[4][4]; /* viewMatrix, row-major; identity by default (gmtl) */
+    float fov = 53.0f; /* RayTracer() default, RayTracer.cpp:18 */
+    bool cam_override = false;
+    rt_camera cam_explicit;
+    bool cam_dirty = true;
+    rt_camera cam;
+    uint32_t width = 0, height = 0;
+
+    /* settings: RayTracer() defaults (RayTracer.cpp:16-22) */
+    uint32_t sample_rate = 8, max_depth = 4;
+    int traversal = RT_TRAVERSAL_BVH;
+    uint32_t nd_y = 8;
+    bool counting = false;
+
+    /* seeds */
+    GlibcRand rng;
+    uint32_t wpad = 0, hpad = 0;
+    bool user_seeds = false;
+    uint32_t *d_seeds = nullptr;
+
+    /* scratch */
+    uint32_t *d_work = nullptr;
+    unsigned long long *d_counters = nullptr;
+    float *d_stage = nullptr;
+    size_t stage_bytes = 0;
+    rt_counters last = {0, 0, 0, 0};
+    bool have_timing = false;
+    int grid_cache[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+int fail(rt_ctx *c, int code, const std::string &msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+int hip_fail(rt_ctx *c, hipError_t e, const char *what)
+{
+    return fail(c, RT_ERR_HIP, std::string(what) + ": " + hip_str(e));
+}
+
+#define HIPCHK(ctx, call)                                                                                              \
+    do {                                                                                                               \
+        hipError_t e_ = (call);                                                                                        \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #call);                                                       \
+    } while (0)
+
+void free_dev(void *p)
+{
+    if (p) (void)hipFree(p);
+}
+
+/* RayTracer::setCameraSpherical (RayTracer.cpp:33-47): gmtl EulerAngle<ZYX>
+   (0, yaw, pitch) -> quaternion qz*qy*qx (Generate.h:214-260), normalised
+   (QuatOps.h:337-351), position = q (0,0,d) q* (Xforms.h:40-60) + target, and
+   the rotation matrix of q (Generate.h:1143-1176).  float arithmetic in gmtl's
+   order; the two angle conversions are binary64 as in the D2R macro. */
+void spherical_view(float tx, float ty, float tz, float el, float az, float dist, float m[4][4])
+{
+    const float yaw = (float)(-(az * kPi / 180.0f) + kPi);
+    const float pitch = (float)(-(el * kPi / 180.0f));
+    const float xr = pitch, yr = yaw, zr = 0.0f;
+    const float x2 = xr * 0.5f, y2 = yr * 0.5f, z2 = zr * 0.5f;
+    /* quaternions as (x, y, z, w) */
+    const float qx[4] = {std::sin(x2), 0.0f, 0.0f, std::cos(x2)};
+    const float qy[4] = {0.0f, std::sin(y2), 0.0f, std::cos(y2)};
+    const float qz[4] = {0.0f, 0.0f, std::sin(z2), std::cos(z2)};
+    auto qmul = [](const float *a, const float *b, float *r) {
+        r[0] = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+        r[1] = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+        r[2] = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+        r[3] = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    };
+    float t[4], q[4];
+    qmul(qz, qy, t);
+    qmul(t, qx, q);
+    const float len = std::sqrt((((q[0] * q[0]) + (q[1] * q[1])) + (q[2] * q[2])) + (q[3] * q[3]));
+    if (!(len < 0.0001f)) {
+        const float li = 1.0f / len;
+        for (int i = 0; i < 4; ++i) q[i] *= li;
+    }
+    /* position = q * (0,0,dist) * conj(q) */
+    const float rc[4] = {-q[0], -q[1], -q[2], q[3]};
+    const float pure[4] = {0.0f, 0.0f, dist, 0.0f};
+    float tmp[4];
+    tmp[0] = pure[3] * rc[0] + pure[0] * rc[3] + pure[1] * rc[2] - pure[2] * rc[1];
+    tmp[1] = pure[3] * rc[1] + pure[1] * rc[3] + pure[2] * rc[0] - pure[0] * rc[2];
+    tmp[2] = pure[3] * rc[2] + pure[2] * rc[3] + pure[0] * rc[1] - pure[1] * rc[0];
+    tmp[3] = pure[3] * rc[3] - pure[0] * rc[0] - pure[1] * rc[1] - pure[2] * rc[2];
+    const float px = q[3] * tmp[0] + q[0] * tmp[3] + q[1] * tmp[2] - q[2] * tmp[1];
+    const float py = q[3] * tmp[1] + q[1] * tmp[3] + q[2] * tmp[0] - q[0] * tmp[2];
+    const float pz = q[3] * tmp[2] + q[2] * tmp[3] + q[0] * tmp[1] - q[1] * tmp[0];
+    /* rotation part (Watt & Watt) */
+    const float xs = q[0] + q[0], ys = q[1] + q[1], zs = q[2] + q[2];
+    const float xx = q[0] * xs, xy = q[0] * ys, xz = q[0] * zs;
+    const float yy = q[1] * ys, yz = q[1] * zs, zz = q[2] * zs;
+    const float wx = q[3] * xs, wy = q[3] * ys, wz = q[3] * zs;
+    m[0][0] = 1.0f - (yy + zz);
+    m[1][0] = xy + wz;
+    m[2][0] = xz - wy;
+    m[0][1] = xy - wz;
+    m[1][1] = 1.0f - (xx + zz);
+    m[2][1] = yz + wx;
+    m[0][2] = xz + wy;
+    m[1][2] = yz - wx;
+    m[2][2] = 1.0f - (xx + yy);
+    m[3][0] = m[3][1] = m[3][2] = 0.0f;
+    m[3][3] = 1.0f;
+    m[0][3] = px + tx;
+    m[1][3] = py + ty;
+    m[2][3] = pz + tz;
+}
+
+/* RayTracerCL::updateCLCamera (RayTracerCL.cpp:178-215). */
+void camera_from_view(const float m[4][4], float fov_deg, uint32_t width, rt_camera *c)
+{
+    auto xform = [&](float v0, float v1, float v2, float *r) { /* gmtl Matrix44 * Vec3 (w = 0), Xforms.h:113-190 */
+        float res[4];
+        for (int i = 0; i < 4; ++i) {
+            res[i] = 0.0f;
+            res[i] += m[i][0] * v0;
+            res[i] += m[i][1] * v1;
+            res[i] += m[i][2] * v2;
+            res[i] += m[i][3] * 0.0f;
+        }
+        if (!(std::fabs(res[3] - 0.0f) <= 0.0001f)) {
+            const float wi = 1.0f / res[3];
+            for (int i = 0; i < 3; ++i) r[i] = res[i] * wi;
+        } else {
+            for (int i = 0; i < 3; ++i) r[i] = res[i];
+        }
+    };
+    float view[3], up[3], right[3];
+    xform(0.0f, 0.0f, -1.0f, view);
+    xform(0.0f, 1.0f, 0.0f, up);
+    right[0] = (view[1] * up[2]) - (view[2] * up[1]);
+    right[1] = (view[2] * up[0]) - (view[0] * up[2]);
+    right[2] = (view[0] * up[1]) - (view[1] * up[0]);
+    const float s = (float)((width / 2.0) / std::tan((fov_deg * kPi / 180.0f) / 2.0));
+    for (int i = 0; i < 3; ++i) view[i] *= s;
+    c->view = {view[0], view[1], view[2], 0.0f};
+    c->up = {up[0], up[1], up[2], 0.0f};
+    c->right = {right[0], right[1], right[2], 0.0f};
+    c->position = {m[0][3], m[1][3], m[2][3], 0.0f};
+}
+
+int ensure_seeds(rt_ctx *c, uint32_t wpad, uint32_t hpad, const uint32_t *src)
+{
+    const size_t count = 2ull * wpad * hpad;
+    if (wpad != c->wpad || hpad != c->hpad) {
+        free_dev(c->d_seeds);
+        c->d_seeds = nullptr;
+        c->wpad = c->hpad = 0;
+        if (count) HIPCHK(c, hipMalloc(&c->d_seeds, count * sizeof(uint32_t)));
+        c->wpad = wpad;
+        c->hpad = hpad;
+    }
+    std::vector<uint32_t> host;
+    if (!src) { /* RayTracerCL::updateSeedBuffer: rand(), values < 2 raised to 2 */
+        host.resize(count);
+        for (size_t i = 0; i < count; ++i) {
+            uint32_t v = c->rng.next();
+            host[i] = v < 2 ? 2 : v;
+        }
+        src = host.data();
+    }
+    if (count) HIPCHK(c, hipMemcpy(c->d_seeds, src, count * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+int grid_blocks(rt_ctx *c, bool linear, bool count, int *out)
+{
+    const int key = (linear ? 2 : 0) + (count ? 1 : 0);
+    if (!c->grid_cache[key]) {
+        int b = 0;
+        const int e = rt_tris_grid_blocks(c->device, linear, count, &b);
+        if (e) return hip_fail(c, (hipError_t)e, "occupancy query");
+        c->grid_cache[key] = b;
+    }
+    *out = c->grid_cache[key];
+    return RT_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+const char *rt_status_string(int s)
+{
+    switch (s) {
+    case RT_OK: return "ok";
+    case RT_ERR_ARG: return "invalid argument";
+    case RT_ERR_HIP: return "HIP runtime error";
+    case RT_ERR_NO_SCENE: return "no spheres set";
+    case RT_ERR_NO_MESH: return "no mesh set";
+    case RT_ERR_ALLOC: return "allocation failed";
+    case RT_ERR_STATE: return "invalid state";
+    case RT_ERR_LIMIT: return "device limit exceeded";
+    default: return "unknown status";
+    }
+}
+
+int rt_create(int device, rt_ctx **out)
+{
+    if (!out) return RT_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return RT_ERR_HIP;
+    if (device < 0 || device >= n) return RT_ERR_ARG;
+    rt_ctx *c = new (std::nothrow) rt_ctx();
+    if (!c) return RT_ERR_ALLOC;
+    c->device = device;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) c->view[i][j] = (i == j) ? 1.0f : 0.0f;
+    c->rng.seed(1);
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        rt_destroy(c);
+        return RT_ERR_HIP;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+int rt_destroy(rt_ctx *c)
+{
+    if (!c) return RT_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_dev(c->d_spheres);
+    free_dev(c->d_lights);
+    free_dev(c->d_nodes);
+    free_dev(c->d_tris);
+    free_dev(c->d_seeds);
+    free_dev(c->d_work);
+    free_dev(c->d_counters);
+    free_dev(c->d_stage);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RT_OK;
+}
+
+const char *rt_last_error(const rt_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int rt_set_spheres(rt_ctx *c, const rt_sphere *s, uint32_t n)
+{
+    if (!c || (n && !s)) return RT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    c->spheres.assign(s, s + n);
+    c->lights.clear();
+    for (uint32_t i = 0; i < n; ++i)
+        if (s[i].mat.emission_power != 0) c->lights.push_back(s[i]); /* rtcommon.h:90 */
+    free_dev(c->d_spheres);
+    free_dev(c->d_lights);
+    c->d_spheres = c->d_lights = nullptr;
+    if (n) {
+        HIPCHK(c, hipMalloc(&c->d_spheres, n * sizeof(rt_sphere)));
+        HIPCHK(c, hipMemcpy(c->d_spheres, s, n * sizeof(rt_sphere), hipMemcpyHostToDevice));
+    }
+    if (!c->lights.empty()) {
+        HIPCHK(c, hipMalloc(&c->d_lights, c->lights.size() * sizeof(rt_sphere)));
+        HIPCHK(c, hipMemcpy(c->d_lights, c->lights.data(), c->lights.size() * sizeof(rt_sphere),
+                            hipMemcpyHostToDevice));
+    }
+    return RT_OK;
+}
+
+int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris)
+{
+    if (!c || !verts || !idx || !n_verts || !n_tris) return fail(c, RT_ERR_ARG, "empty mesh");
+    HIPCHK(c, hipSetDevice(c->device));
+    RtBvh b;
+    std::string err;
+    if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
+        return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
+    free_dev(c->d_nodes);
+    free_dev(c->d_tris);
+    c->d_nodes = c->d_tris = nullptr;
+    c->n_tris = 0;
+    HIPCHK(c, hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
+    HIPCHK(c, hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_tris, b.tris.data(), b.tris.size() * sizeof(float), hipMemcpyHostToDevice));
+    c->n_tris = n_tris;
+    c->bvh.n_nodes = b.n_nodes;
+    c->bvh.n_leaves = b.n_leaves;
+    c->bvh.depth = b.depth;
+    c->bvh.build_seconds = b.build_seconds;
+    return RT_OK;
+}
+
+int rt_mesh_info(const rt_ctx *c, uint32_t *n_nodes, uint32_t *depth, double *build_seconds)
+{
+    if (!c) return RT_ERR_ARG;
+    if (!c->n_tris) return RT_ERR_NO_MESH;
+    if (n_nodes) *n_nodes = c->bvh.n_nodes;
+    if (depth) *depth = c->bvh.depth;
+    if (build_seconds) *build_seconds = c->bvh.build_seconds;
+    return RT_OK;
+}
+
+int rt_set_view_matrix(rt_ctx *c, const float m[16])
+{
+    if (!c || !m) return RT_ERR_ARG;
+    for (int col = 0; col < 4; ++col)
+        for (int row = 0; row < 4; ++row) c->view[row][col] = m[col * 4 + row];
+    c->cam_override = false;
+    c->cam_dirty = true;
+    return RT_OK;
+}
+
+int rt_set_camera_spherical(rt_ctx *c, float tx, float ty, float tz, float el, float az, float dist)
+{
+    if (!c) return RT_ERR_ARG;
+    spherical_view(tx, ty, tz, el, az, dist, c->view);
+    c->cam_override = false;
+    c->cam_dirty = true;
+    return RT_OK;
+}
+
+int rt_set_fov(rt_ctx *c, float fov)
+{
+    if (!c) return RT_ERR_ARG;
+    c->fov = fov;
+    c->cam_override = false;
+    c->cam_dirty = true;
+    return RT_OK;
+}
+
+int rt_set_camera(rt_ctx *c, const rt_camera *cam)
+{
+    if (!c || !cam) return RT_ERR_ARG;
+    c->cam_explicit = *cam;
+    c->cam_override = true;
+    c->cam_dirty = true;
+    return RT_OK;
+}
+
+int rt_camera_spherical(float tx, float ty, float tz, float el, float az, float dist, float fov, uint32_t width,
+                        rt_camera *out)
+{
+    if (!out) return RT_ERR_ARG;
+    float m[4][4];
+    spherical_view(tx, ty, tz, el, az, dist, m);
+    camera_from_view(m, fov, width, out);
+    return RT_OK;
+}
+
+int rt_set_params(rt_ctx *c, uint32_t sample_rate, uint32_t max_depth)
+{
+    if (!c) return RT_ERR_ARG;
+    if (sample_rate > 4096) return fail(c, RT_ERR_ARG, "sample rate too large");
+    c->sample_rate = sample_rate;
+    c->max_depth = max_depth;
+    return RT_OK;
+}
+
+int rt_set_traversal(rt_ctx *c, int t)
+{
+    if (!c || (t != RT_TRAVERSAL_BVH && t != RT_TRAVERSAL_LINEAR)) return RT_ERR_ARG;
+    c->traversal = t;
+    return RT_OK;
+}
+
+int rt_set_ndrange(rt_ctx *c, uint32_t nd_y)
+{
+    if (!c || nd_y == 0 || nd_y > 1024) return RT_ERR_ARG;
+    c->nd_y = nd_y;
+    return RT_OK;
+}
+
+int rt_set_seed_layout(rt_ctx *c, uint32_t wpad, uint32_t hpad)
+{
+    if (!c || !wpad || !hpad) return RT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int r = ensure_seeds(c, wpad, hpad, nullptr);
+    if (r == RT_OK) c->user_seeds = true;
+    return r;
+}
+
+int rt_set_seeds(rt_ctx *c, const uint32_t *seeds, size_t count)
+{
+    if (!c || !seeds) return RT_ERR_ARG;
+    if (!c->wpad || count != 2ull * c->wpad * c->hpad) return fail(c, RT_ERR_STATE, "seed count != 2*Wpad*Hpad");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int r = ensure_seeds(c, c->wpad, c->hpad, seeds);
+    if (r == RT_OK) c->user_seeds = true;
+    return r;
+}
+
+int rt_get_seeds(const rt_ctx *c, uint32_t *out, size_t count)
+{
+    if (!c || !out) return RT_ERR_ARG;
+    if (!c->wpad || count != 2ull * c->wpad * c->hpad) return RT_ERR_STATE;
+    if (hipSetDevice(c->device) != hipSuccess) return RT_ERR_HIP;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return RT_ERR_HIP;
+    if (hipMemcpy(out, c->d_seeds, count * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
+    return RT_OK;
+}
+
+int rt_seed_layout(const rt_ctx *c, uint32_t *wpad, uint32_t *hpad)
+{
+    if (!c) return RT_ERR_ARG;
+    if (wpad) *wpad = c->wpad;
+    if (hpad) *hpad = c->hpad;
+    return RT_OK;
+}
+
+int rt_glibc_rand_fill(uint32_t seed, uint32_t *out, size_t count, uint32_t skip)
+{
+    if (!out && count) return RT_ERR_ARG;
+    GlibcRand g;
+    g.seed(seed);
+    for (uint32_t i = 0; i < skip; ++i) (void)g.next();
+    for (size_t i = 0; i < count; ++i) out[i] = g.next();
+    return RT_OK;
+}
+
+uint32_t rt_tile_rows(uint32_t height, const rt_tile *t)
+{
+    if (!t || t->n_ranks <= 1) return height;
+    if (t->stripe_rows == 0 || t->rank >= t->n_ranks) return 0;
+    const uint32_t period = t->stripe_rows * t->n_ranks;
+    const uint32_t full = height / period;
+    uint32_t rows = full * t->stripe_rows;
+    const uint32_t rem = height - full * period;
+    const uint32_t start = t->rank * t->stripe_rows;
+    if (rem > start) rows += std::min(rem - start, t->stripe_rows);
+    return rows;
+}
+
+int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int kernel, const rt_tile *tile,
+                    int flags, void *stream)
+{
+    if (!c) return RT_ERR_ARG;
+    if (W == 0 || H == 0) return RT_OK; /* RayTracerCL.cpp:219-220 */
+    if (!out) return fail(c, RT_ERR_ARG, "null output buffer");
+    if (kernel < RT_KERNEL_SPHERES || kernel > RT_KERNEL_TRIS) return fail(c, RT_ERR_ARG, "unknown kernel");
+    if (tile && tile->n_ranks > 1 && (tile->stripe_rows == 0 || tile->rank >= tile->n_ranks))
+        return fail(c, RT_ERR_ARG, "bad tile");
+    if (tile && tile->n_ranks > 1 && kernel == RT_KERNEL_SPHERES && prog > 0)
+        return fail(c, RT_ERR_ARG,
+                    "row-shifted seeds (raytracer.cl:20-30) cross stripe boundaries: progressive sphere frames need "
+                    "the full frame on one device");
+    if (kernel == RT_KERNEL_TRIS && c->n_tris == 0) return fail(c, RT_ERR_NO_MESH, "no mesh set");
+    if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
+    if (kernel == RT_KERNEL_TRIS && c->bvh.depth > RT_STACK_DEPTH) return fail(c, RT_ERR_LIMIT, "BVH too deep");
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+
+    /* RayTracerCL.cpp:229-249: NDRange padding, camera/seed refresh */
+    const uint32_t wpad = ((W & 0x1F) == 0) ? W : ((W & 0xFFFFFFE0u) + 0x20u);
+    const uint32_t hpad = (uint32_t)std::ceil(H / (float)c->nd_y) * c->nd_y;
+    if (W != c->width || H != c->height) {
+        c->cam_dirty = false;
+        c->width = W;
+        c->height = H;
+        if (c->cam_override) c->cam = c->cam_explicit;
+        else camera_from_view(c->view, c->fov, W, &c->cam);
+        if (c->user_seeds && c->wpad == wpad && c->hpad == hpad) {
+            c->user_seeds = false; /* caller-provided seeds for this layout */
+        } else {
+            const int r = ensure_seeds(c, wpad, hpad, nullptr);
+            if (r != RT_OK) return r;
+            c->user_seeds = false;
+        }
+    } else if (c->cam_dirty) {
+        c->cam_dirty = false;
+        if (c->cam_override) c->cam = c->cam_explicit;
+        else camera_from_view(c->view, c->fov, W, &c->cam);
+    }
+    if (c->wpad < W || c->hpad < H) return fail(c, RT_ERR_STATE, "seed layout smaller than the frame");
+
+    const uint32_t hl = rt_tile_rows(H, tile);
+    if (hl == 0) return RT_OK;
+    const size_t out_bytes = (size_t)W * hl * 4 * sizeof(float);
+    float *dout = out;
+    if (!(flags & RT_OUT_DEVICE)) {
+        if (c->stage_bytes < out_bytes) {
+            free_dev(c->d_stage);
+            c->d_stage = nullptr;
+            c->stage_bytes = 0;
+            HIPCHK(c, hipMalloc(&c->d_stage, out_bytes));
+            c->stage_bytes = out_bytes;
+        }
+        dout = c->d_stage;
+        if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), st));
+    const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
+                   rk = tile ? tile->rank : 0u;
+    int e = 0;
+    if (kernel == RT_KERNEL_TRIS) {
+        RtTriLaunch a;
+        a.out = dout;
+        a.seeds = c->d_seeds;
+        a.nodes = c->d_nodes;
+        a.tris = c->d_tris;
+        a.n_tris = c->n_tris;
+        a.lights = c->d_lights;
+        a.n_lights = (uint32_t)c->lights.size();
+        if (a.n_lights > 16) return fail(c, RT_ERR_LIMIT, "more than 16 emissive spheres");
+        a.cam = c->cam;
+        a.W = W;
+        a.H = H;
+        a.Wpad = c->wpad;
+        a.Hpad = c->hpad;
+        a.Hl = hl;
+        a.sample_rate = c->sample_rate;
+        a.max_depth = c->max_depth;
+        a.progressive = prog;
+        a.stripe = stripe;
+        a.n_ranks = nr;
+        a.rank = rk;
+        a.work_counter = c->d_work;
+        a.counters = c->d_counters;
+        const bool linear = c->traversal == RT_TRAVERSAL_LINEAR;
+        int blocks = 0;
+        const int r = grid_blocks(c, linear, c->counting, &blocks);
+        if (r != RT_OK) return r;
+        const uint64_t items = (uint64_t)((W + 7) / 8) * ((hl + 7) / 8) * 64;
+        blocks = (int)std::min<uint64_t>((uint64_t)blocks, (items + RT_BLOCK - 1) / RT_BLOCK);
+        if (blocks < 1) blocks = 1;
+        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
+        HIPCHK(c, hipEventRecord(c->ev0, st));
+        e = rt_launch_tris(a, linear, c->counting, blocks, st);
+        HIPCHK(c, hipEventRecord(c->ev1, st));
+    } else {
+        RtSphLaunch a;
+        a.out = dout;
+        a.seeds = c->d_seeds;
+        a.spheres = c->d_spheres;
+        a.n_spheres = (uint32_t)c->spheres.size();
+        a.cam = c->cam;
+        a.W = W;
+        a.H = H;
+        a.Wpad = c->wpad;
+        a.Hpad = c->hpad;
+        a.Hl = hl;
+        a.sample_rate = c->sample_rate;
+        a.max_depth = c->max_depth;
+        a.progressive = prog;
+        a.stripe = stripe;
+        a.n_ranks = nr;
+        a.rank = rk;
+        a.counters = c->d_counters;
+        HIPCHK(c, hipEventRecord(c->ev0, st));
+        e = rt_launch_spheres(a, kernel == RT_KERNEL_SPHERES_SS, st);
+        HIPCHK(c, hipEventRecord(c->ev1, st));
+    }
+    if (e) return hip_fail(c, (hipError_t)e, "kernel launch");
+    c->have_timing = true;
+    if (!(flags & RT_OUT_DEVICE)) HIPCHK(c, hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, st));
+    return RT_OK;
+}
+
+int rt_synchronize(rt_ctx *c)
+{
+    if (!c) return RT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    unsigned long long h[4];
+    HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+    c->last.rays_closest = h[0];
+    c->last.rays_shadow = h[1];
+    c->last.nodes_visited = h[2];
+    c->last.tris_tested = h[3];
+    return RT_OK;
+}
+
+int rt_render(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int kernel, const rt_tile *tile,
+              int flags)
+{
+    const int r = rt_render_async(c, out, W, H, prog, kernel, tile, flags, nullptr);
+    if (r != RT_OK) return r;
+    return rt_synchronize(c); /* cmdQueue.finish(), RayTracerCL.cpp:292 */
+}
+
+int rt_get_counters(const rt_ctx *c, rt_counters *out)
+{
+    if (!c || !out) return RT_ERR_ARG;
+    *out = c->last;
+    return RT_OK;
+}
+
+int rt_set_counting(rt_ctx *c, int enable)
+{
+    if (!c) return RT_ERR_ARG;
+    c->counting = enable != 0;
+    return RT_OK;
+}
+
+int rt_last_kernel_ms(const rt_ctx *c, float *ms)
+{
+    if (!c || !ms) return RT_ERR_ARG;
+    if (!c->have_timing) return RT_ERR_STATE;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return RT_ERR_HIP;
+    return hipEventElapsedTime(ms, c->ev0, c->ev1) == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
+int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_t *out_idx, float *out_t)
+{
+    if (!c || !rays || !out_idx) return RT_ERR_ARG;
+    if (!c->n_tris) return fail(c, RT_ERR_NO_MESH, "no mesh set");
+    if (n == 0) return RT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    rt_ray *d_rays = nullptr;
+    int32_t *d_idx = nullptr;
+    float *d_t = nullptr;
+    auto cleanup = [&]() {
+        free_dev(d_rays);
+        free_dev(d_idx);
+        free_dev(d_t);
+    };
+    hipError_t e = hipMalloc(&d_rays, n * sizeof(rt_ray));
+    if (e == hipSuccess) e = hipMalloc(&d_idx, n * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&d_t, n * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, n * sizeof(rt_ray), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        const int le = rt_launch_trace_rays(c->d_nodes, c->d_tris, c->n_tris, d_rays, n, any_hit,
+                                            c->traversal == RT_TRAVERSAL_LINEAR, d_idx, d_t, c->stream);
+        e = (hipError_t)le;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out_idx, d_idx, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_t) e = hipMemcpy(out_t, d_t, n * sizeof(float), hipMemcpyDeviceToHost);
+    cleanup();
+    if (e != hipSuccess) return hip_fail(c, e, "rt_trace_rays");
+    return RT_OK;
+}
+
+/* ---- synthetic meshes ---------------------------------------------------- */
+
+static void mesh_grid(uint32_t n_tris, uint32_t *nt, uint32_t *np)
+{
+    uint32_t t = 2;
+    while (4ull * t * (t - 1) < n_tris) ++t;
+    *nt = t;     /* latitude bands */
+    *np = 2 * t; /* longitude segments */
+}
+
+uint32_t rt_mesh_vertex_count(uint32_t n_tris)
+{
+    uint32_t nt, np;
+    mesh_grid(n_tris, &nt, &np);
+    return 2 + (nt - 1) * np;
+}
+
+int rt_make_mesh(uint32_t n_tris, float cx, float cy, float cz, float r, float *verts, int32_t *idx)
+{
+    if (!n_tris || !verts || !idx) return RT_ERR_ARG;
+    uint32_t nt, np;
+    mesh_grid(n_tris, &nt, &np);
+    const float pi = RT_M_PI_F;
+    auto put = [&](uint32_t v, float th, float ph) {
+        /* displaced sphere: two bump frequencies, deterministic (rt_math.h only) */
+        const float bump = 0.08f * rt_sinf(9.0f * th) * rt_sinf(8.0f * ph) +
+                           0.04f * rt_sinf(23.0f * th + 3.0f * ph) * rt_cosf(19.0f * ph - 2.0f * th);
+        const float rr = r * (1.0f + bump);
+        const float st = rt_sinf(th), ct = rt_cosf(th);
+        verts[3ull * v + 0] = cx + rr * st * rt_cosf(ph);
+        verts[3ull * v + 1] = cy + rr * ct;
+        verts[3ull * v + 2] = cz + rr * st * rt_sinf(ph);
+    };
+    const uint32_t top = 0, bottom = 1 + (nt - 1) * np;
+    put(top, 0.0f, 0.0f);
+    put(bottom, pi, 0.0f);
+    for (uint32_t i = 1; i < nt; ++i) {
+        const float th = pi * (float)i / (float)nt;
+        for (uint32_t j = 0; j < np; ++j) put(1 + (i - 1) * np + j, th, 2.0f * pi * (float)j / (float)np);
+    }
+    auto ring = [&](uint32_t i, uint32_t j) -> int32_t { return (int32_t)(1 + (i - 1) * np + (j % np)); };
+    /* winding chosen so that cross(e2, e1) (the reference's normal,
+       rtcommon.h:389) points outward */
+    uint64_t k = 0;
+    auto tri = [&](int32_t a, int32_t b, int32_t c) {
+        if (k >= n_tris) return;
+        idx[3 * k + 0] = a;
+        idx[3 * k + 1] = b;
+        idx[3 * k + 2] = c;
+        ++k;
+    };
+    for (uint32_t j = 0; j < np; ++j) tri((int32_t)top, ring(1, j), ring(1, j + 1));
+    for (uint32_t i = 1; i + 1 < nt; ++i)
+        for (uint32_t j = 0; j < np; ++j) {
+            tri(ring(i, j), ring(i + 1, j), ring(i + 1, j + 1));
+            tri(ring(i, j), ring(i + 1, j + 1), ring(i, j + 1));
+        }
+    for (uint32_t j = 0; j < np; ++j) tri(ring(nt - 1, j), (int32_t)bottom, ring(nt - 1, j + 1));
+    return k == n_tris ? RT_OK : RT_ERR_STATE;
+}
+
+} /* extern "C" */

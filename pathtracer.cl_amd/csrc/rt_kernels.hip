@@ -1,0 +1,731 @@
+/*
+ * rt_kernels.hip — gfx950 kernels of the MI355X path tracer.
+ *
+ *   k_spheres<SS>      raytrace / raytrace_ss   (clrt/ocl/raytracer.cl:46-104, :120-166)
+ *   k_tris<LIN, CNT>   raytrace_tris            (clrt/ocl/raytracer.cl:184-243)
+ *   k_trace_rays       closest / any-hit queries (rtcommon.h:39-68), parity tests
+ *
+ * k_tris is a persistent wavefront state machine: every loop iteration each
+ * live lane performs exactly ONE ray query (a path segment's closest hit or one
+ * shadow ray) through a shared traversal loop, then advances its path.  Lanes
+ * whose pixel finished are refilled from a global pixel queue with one
+ * ballot + popcount + atomicAdd per wave (prefix-rank assignment), so SIMD
+ * lanes stay busy until the queue drains.  The traversal stack lives in LDS
+ * ([depth][lane] stride 256: conflict-free), BVH nodes and triangles are
+ * 16-B-aligned float4 records read with dwordx4 loads.  See DESIGN.md.
+ */
+#include <hip/hip_runtime.h>
+
+#include "rt_device.h"
+#include "rt_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kInf = __builtin_huge_valf();
+
+/* ------------------------------------------------------------------------ */
+/* Ray/triangle test (geometryFuncs.h:160-245): barycentric part shared by the
+   closest-hit and any-hit forms.  Returns false on rejection, else t.        */
+__device__ __forceinline__ bool mt_test(V3 o, V3 d, const float4 &a, const float4 &b, const float4 &c, float &t)
+{
+    const V3 v0 = v3(a.x, a.y, a.z);
+    const V3 e1 = v3(b.x, b.y, b.z);
+    const V3 e2 = v3(c.x, c.y, c.z);
+    const V3 p = cross3(d, e2);
+    float det = dot3(p, e1);
+    if (rt_fabsf(det) < RT_SMALL_F) return false;
+    det = 1.0f / det;
+    const V3 to = v3(o.x - v0.x, o.y - v0.y, o.z - v0.z);
+    const V3 q = cross3(to, e1);
+    const float u = dot3(p, to) * det;
+    if (u < 0 || u > 1) return false;
+    const float v = dot3(q, d) * det;
+    if (v < 0 || v + u > 1) return false;
+    t = dot3(q, e2) * det;
+    return true;
+}
+
+/* Conservative slab test against one child box (culling only: no parity
+   constraint, explicit FMAs allowed). */
+__device__ __forceinline__ float slab(float lo_x, float hi_x, float lo_y, float hi_y, float lo_z, float hi_z, V3 inv,
+                                      V3 oi, float tmin_c, float tmax_c, bool &hit)
+{
+    const float x0 = __builtin_fmaf(lo_x, inv.x, -oi.x);
+    const float x1 = __builtin_fmaf(hi_x, inv.x, -oi.x);
+    const float y0 = __builtin_fmaf(lo_y, inv.y, -oi.y);
+    const float y1 = __builtin_fmaf(hi_y, inv.y, -oi.y);
+    const float z0 = __builtin_fmaf(lo_z, inv.z, -oi.z);
+    const float z1 = __builtin_fmaf(hi_z, inv.z, -oi.z);
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                     __builtin_fmaxf(__builtin_fminf(z0, z1), tmin_c));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                     __builtin_fminf(__builtin_fmaxf(z0, z1), tmax_c));
+    hit = tn <= tf;
+    return tn;
+}
+
+__device__ __forceinline__ float safe_rcp(float d)
+{
+    const float e = 1e-18f;
+    const float dd = (rt_fabsf(d) > e) ? d : (d < 0.0f ? -e : e);
+    return __builtin_amdgcn_rcpf(dd);
+}
+
+/* Culling margin on the t interval: covers the rounding of the reference's
+   intersection t relative to the box slabs (boxes are padded as well). */
+__device__ __forceinline__ float t_slack(float t) { return t * 1.0009765625f + 1e-4f; }
+
+struct TravCounts {
+    uint32_t nodes;
+    uint32_t tests;
+};
+
+/* One ray query.  Closest hit (any_hit = false): returns the leaf-order slot of
+   the hit (or -1) with t in tmax; the result equals the reference's linear
+   loop: minimum t, ties to the highest original index (rtcommon.h:39-52 with
+   intersects_triangle's `t > tmax` rejection).  Any hit: returns >= 0 iff some
+   triangle has tmin < t < tmax (rtcommon.h:59-68). */
+template <bool LINEAR, bool COUNT>
+__device__ __forceinline__ int traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                        uint32_t n_tris, V3 o, V3 d, float tmin, float &tmax, bool any_hit,
+                                        int *stk, TravCounts &cnt)
+{
+    int best = -1;
+    int best_orig = -1;
+    float best_t = tmax;
+    if (LINEAR) {
+        /* The reference algorithm: every triangle, in a wave-uniform loop (the
+           slot index is uniform, so the records come in through scalar loads). */
+        bool live = true;
+        for (uint32_t s = 0; s < n_tris; ++s) {
+            if (live) {
+                const float4 a = tris[3 * s], b = tris[3 * s + 1], c = tris[3 * s + 2];
+                float t;
+                if (COUNT) cnt.tests++;
+                if (mt_test(o, d, a, b, c, t)) {
+                    if (any_hit) {
+                        if (t < tmax && t > tmin) {
+                            best = (int)s;
+                            live = false;
+                        }
+                    } else {
+                        const int orig = __float_as_int(a.w);
+                        if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
+                            best = (int)s;
+                            best_orig = orig;
+                            best_t = t;
+                        }
+                    }
+                }
+            }
+            if (!__any(live)) break;
+        }
+        if (!any_hit) tmax = best_t;
+        return best;
+    }
+
+    const V3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    const float tmin_c = -1e-3f;
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        if (node >= 0) {
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
+            if (COUNT) cnt.nodes++;
+            const float tmax_c = t_slack(best_t);
+            bool h0, h1;
+            const float t0 = slab(n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, inv, oi, tmin_c, tmax_c, h0);
+            const float t1 = slab(n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, inv, oi, tmin_c, tmax_c, h1);
+            const int c0 = __float_as_int(n3.x);
+            const int c1 = __float_as_int(n3.y);
+            if (h0 && h1) {
+                int nearc = c0, farc = c1;
+                if (t1 < t0) {
+                    nearc = c1;
+                    farc = c0;
+                }
+                stk[sp * RT_BLOCK] = farc;
+                ++sp;
+                node = nearc;
+            } else if (h0) {
+                node = c0;
+            } else if (h1) {
+                node = c1;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                node = stk[sp * RT_BLOCK];
+            }
+            continue;
+        }
+        /* leaf */
+        const int enc = ~node;
+        const int first = enc >> 3;
+        const int count = (enc & 7) + 1;
+        bool done = false;
+        for (int k = 0; k < count; ++k) {
+            const int s = first + k;
+            const float4 a = tris[3 * s], b = tris[3 * s + 1], c = tris[3 * s + 2];
+            float t;
+            if (COUNT) cnt.tests++;
+            if (mt_test(o, d, a, b, c, t)) {
+                if (any_hit) {
+                    if (t < tmax && t > tmin) {
+                        best = s;
+                        done = true;
+                        break;
+                    }
+                } else {
+                    const int orig = __float_as_int(a.w);
+                    if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
+                        best = s;
+                        best_orig = orig;
+                        best_t = t;
+                    }
+                }
+            }
+        }
+        if (done || sp == 0) break;
+        --sp;
+        node = stk[sp * RT_BLOCK];
+    }
+    if (!any_hit) tmax = best_t;
+    return best;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
+{
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ void flush_counters(unsigned long long *dst, unsigned long long a, unsigned long long b,
+                                               unsigned long long c, unsigned long long d, bool with_trav)
+{
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (with_trav) {
+        c = wave_sum(c);
+        d = wave_sum(d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&dst[0], a);
+        atomicAdd(&dst[1], b);
+        if (with_trav) {
+            atomicAdd(&dst[2], c);
+            atomicAdd(&dst[3], d);
+        }
+    }
+}
+
+/* raytracer.cl:81-85: normalize(view + right*a + up*b), float4 lanes incl. w,
+   normalize pinned as v / sqrt(dot(v, v)). */
+__device__ __forceinline__ V3 camera_dir(const rt_camera &cam, float a, float b)
+{
+    const float x = (cam.view.x + cam.right.x * a) + cam.up.x * b;
+    const float y = (cam.view.y + cam.right.y * a) + cam.up.y * b;
+    const float z = (cam.view.z + cam.right.z * a) + cam.up.z * b;
+    const float w = (cam.view.w + cam.right.w * a) + cam.up.w * b;
+    const float len = rt_sqrtf(((x * x + y * y) + z * z) + w * w);
+    return v3(x / len, y / len, z / len);
+}
+
+__device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uint32_t n_ranks, uint32_t rank)
+{
+    if (n_ranks <= 1) return yl;
+    return ((yl / stripe) * n_ranks + rank) * stripe + (yl % stripe);
+}
+
+/* ======================================================================== */
+/* Triangle kernel: raytrace_tris + trace_path_tri (rtcommon.h:371-470).     */
+
+constexpr int kMaxLights = 16;
+
+enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_PIXDONE = 4, M_DONE = 5 };
+
+template <bool LINEAR, bool COUNT>
+__global__ __launch_bounds__(RT_BLOCK) void k_tris(RtTriLaunch a)
+{
+    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
+    __shared__ float s_light[kMaxLights * 8];
+
+    /* emissive spheres: center.xyz, radius, emission.xyz (materials.h:232, rtcommon.h:97-99) */
+    const uint32_t n_lights = a.n_lights < (uint32_t)kMaxLights ? a.n_lights : (uint32_t)kMaxLights;
+    if (threadIdx.x < n_lights) {
+        const rt_sphere &L = a.lights[threadIdx.x];
+        float *dst = s_light + threadIdx.x * 8;
+        dst[0] = L.center.x;
+        dst[1] = L.center.y;
+        dst[2] = L.center.z;
+        dst[3] = L.radius;
+        dst[4] = L.mat.emission.x;
+        dst[5] = L.mat.emission.y;
+        dst[6] = L.mat.emission.z;
+        dst[7] = 0.0f;
+    }
+    __syncthreads();
+
+    int *stk = s_stack + threadIdx.x;
+    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
+    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
+    float4 *__restrict__ out = reinterpret_cast<float4 *>(a.out);
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t spp = a.sample_rate * a.sample_rate;
+    const uint32_t plane = a.Wpad * a.Hpad;
+    const uint32_t tiles_x = (a.W + 7u) >> 3;
+    const uint32_t tiles_y = (a.Hl + 7u) >> 3;
+    const uint32_t n_items = tiles_x * tiles_y * 64u;
+    const float hw = ((float)a.W) / 2.0f;
+    const float hh = ((float)a.H) / 2.0f;
+    const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
+
+    int mode = M_IDLE;
+    uint32_t x = 0, yl = 0, y = 0, slot = 0;
+    Seed seed = {0u, 0u};
+    float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f; /* pixel sum over samples (raytracer.cl:228-230) */
+    float col_x = 0.0f, col_y = 0.0f, col_z = 0.0f; /* this path's radiance (trace_path_tri's pixelColor) */
+    V3 prop = v3(1.0f, 1.0f, 1.0f);
+    uint32_t sample = 0, depth = 0, light = 0;
+    V3 ro = v3(0.0f, 0.0f, 0.0f), rd = v3(0.0f, 0.0f, 1.0f);
+    V3 hp = ro, hn = ro, so = ro, sd = rd, direct = ro;
+    float stmax = 0.0f;
+    bool tri_hit = false;
+    unsigned long long n_closest = 0, n_shadow = 0, n_nodes = 0, n_tests = 0;
+
+    for (;;) {
+        /* ---- A: refill idle lanes from the pixel queue: one atomic per wave,
+                lanes ranked by a prefix popcount of the idle ballot ---- */
+        const unsigned long long idle = __ballot(mode == M_IDLE);
+        if (idle) {
+            const int leader = __ffsll((long long)idle) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.work_counter, (uint32_t)__popcll(idle));
+            base = __shfl(base, leader);
+            if (mode == M_IDLE) {
+                const uint32_t item = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                if (item >= n_items) {
+                    mode = M_DONE;
+                } else {
+                    /* 8 x 8 pixel tiles, row-major over the (local) frame */
+                    const uint32_t tile = item >> 6, in = item & 63u;
+                    x = (tile % tiles_x) * 8u + (in & 7u);
+                    yl = (tile / tiles_x) * 8u + (in >> 3);
+                    if (x < a.W && yl < a.Hl) {
+                        y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                        slot = y * a.Wpad + x; /* raytracer.cl:207-209: unshifted seed slot */
+                        seed.x = a.seeds[slot];
+                        seed.y = a.seeds[plane + slot];
+                        acc_x = acc_y = acc_z = 0.0f;
+                        sample = 0;
+                        mode = (spp > 0) ? M_NEWSAMPLE : M_PIXDONE;
+                    }
+                }
+            }
+        }
+        if (!__any(mode != M_DONE)) break;
+
+        /* ---- B: camera ray of a new sample (raytracer.cl:216-224; sx outer,
+                sy inner, the x draw before the y draw) ---- */
+        if (mode == M_NEWSAMPLE) {
+            const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
+            const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
+            const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
+            ro = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+            rd = camera_dir(a.cam, fa - hw, fb - hh);
+            prop = v3(1.0f, 1.0f, 1.0f);
+            col_x = col_y = col_z = 0.0f;
+            depth = 0;
+            mode = M_CLOSEST;
+        }
+
+        /* ---- C: this iteration's single ray query ---- */
+        int res = -1;
+        float qt = kInf;
+        if (mode == M_CLOSEST || mode == M_SHADOW) {
+            const bool shadow = (mode == M_SHADOW);
+            if (shadow) qt = stmax;
+            TravCounts tc = {0u, 0u};
+            /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
+               returns true): skip the traversal, same result */
+            if (!shadow || qt > RT_SMALL_F)
+                res = traverse<LINEAR, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F,
+                                              qt, shadow, stk, tc);
+            if (COUNT) {
+                n_nodes += tc.nodes;
+                n_tests += tc.tests;
+            }
+        }
+
+        /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
+        bool want_shadow = false, seg_done = false, sample_done = false;
+        if (mode == M_CLOSEST) {
+            ++n_closest;
+            bool surface = true;
+            if (res >= 0) {
+                const float4 e1 = tris[3 * res + 1];
+                const float4 e2 = tris[3 * res + 2];
+                hp = v3(ro.x + rd.x * qt, ro.y + rd.y * qt, ro.z + rd.z * qt);
+                hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z)); /* unnormalised, rtcommon.h:389 */
+                tri_hit = true;
+            } else {
+                /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
+                const float hd = intersect_box(ro, rd, RT_SMALL_F, bw, bh, bw);
+                if (hd > RT_SMALL_F && hd < kInf) {
+                    hp = v3(ro.x + rd.x * hd, ro.y + rd.y * hd, ro.z + rd.z * hd);
+                    hn = box_normal(hp, bw, bh, bw);
+                    tri_hit = false;
+                } else {
+                    surface = false;
+                    sample_done = true; /* path terminates (rtcommon.h:463-466) */
+                }
+            }
+            if (surface) { /* sample_direct_illumination_tri, rtcommon.h:78-105 */
+                so = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
+                direct = v3(0.0f, 0.0f, 0.0f);
+                light = 0;
+                if (n_lights > 0) want_shadow = true;
+                else seg_done = true;
+            }
+        } else if (mode == M_SHADOW) {
+            ++n_shadow;
+            if (res < 0) { /* unoccluded: rtcommon.h:93-101 */
+                const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
+                if (cw > 0) {
+                    direct.x += s_light[light * 8 + 4] * cw;
+                    direct.y += s_light[light * 8 + 5] * cw;
+                    direct.z += s_light[light * 8 + 6] * cw;
+                }
+            }
+            ++light;
+            if (light < n_lights) want_shadow = true;
+            else seg_done = true;
+        }
+        if (want_shadow) { /* one sample per light: frand r1 then r2 (rtcommon.h:92) */
+            const float r1 = frand(seed);
+            const float r2 = frand(seed);
+            const V3 lc = v3(s_light[light * 8 + 0], s_light[light * 8 + 1], s_light[light * 8 + 2]);
+            sd = sphere_light_dir(so, lc, s_light[light * 8 + 3], r1, r2, stmax);
+            mode = M_SHADOW;
+        }
+        if (seg_done) {
+            const float scale = 1.0f * RT_M_1_PI_F;
+            if (tri_hit) { /* rtcommon.h:411-421: no bounce off triangles */
+                col_x += prop.x * direct.x * scale * 0.7f;
+                col_y += prop.y * direct.y * scale * 0.7f;
+                col_z += prop.z * direct.z * scale * 0.7f;
+                sample_done = true;
+            } else { /* rtcommon.h:435-461: albedo 0.7, Lambert bounce (drawn even at the last depth) */
+                prop.x *= 0.7f;
+                prop.y *= 0.7f;
+                prop.z *= 0.7f;
+                col_x += prop.x * direct.x * scale;
+                col_y += prop.y * direct.y * scale;
+                col_z += prop.z * direct.z * scale;
+                ro = hp;
+                const float r1 = frand(seed);
+                const float r2 = frand(seed);
+                rd = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
+                ++depth;
+                if (depth > a.max_depth) sample_done = true;
+                else mode = M_CLOSEST;
+            }
+        }
+        if (sample_done) {
+            acc_x += col_x;
+            acc_y += col_y;
+            acc_z += col_z;
+            ++sample;
+            mode = (sample < spp) ? M_NEWSAMPLE : M_PIXDONE;
+        }
+        if (mode == M_PIXDONE) { /* raytracer.cl:234-242 */
+            const float n = (float)spp;
+            float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
+            float4 *dst = out + ((size_t)yl * a.W + x);
+            if (a.progressive > 0) {
+                const float4 old = *dst;
+                const float t = 1.0f / (float)a.progressive;
+                p.x = old.x + (p.x - old.x) * t;
+                p.y = old.y + (p.y - old.y) * t;
+                p.z = old.z + (p.z - old.z) * t;
+                p.w = old.w + (p.w - old.w) * t;
+            }
+            *dst = p;
+            a.seeds[slot] = seed.x;
+            a.seeds[plane + slot] = seed.y;
+            mode = M_IDLE;
+        }
+    }
+    flush_counters(a.counters, n_closest, n_shadow, n_nodes, n_tests, COUNT);
+}
+
+/* ======================================================================== */
+/* Sphere kernel: raytrace (SS = false) / raytrace_ss (SS = true)            */
+/* (raytracer.cl:46-166, trace_path rtcommon.h:267-365).                     */
+
+__device__ V3 trace_path(PathRay &r, const rt_sphere *__restrict__ sph, uint32_t n, uint32_t max_depth, Seed &seed,
+                         unsigned long long &n_closest, unsigned long long &n_shadow)
+{
+    const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
+    V3 color = v3(0.0f, 0.0f, 0.0f);
+    for (uint32_t depth = 0; depth <= max_depth; ++depth) {
+        ++n_closest;
+        /* scene_intersection, rtcommon.h:107-121 */
+        int hit = -1;
+        for (uint32_t i = 0; i < n; ++i) {
+            const float dd = intersect_sphere(r.o, r.d, r.tmin, v3f(sph[i].center), sph[i].radius);
+            if (dd > r.tmin && dd < r.tmax) {
+                hit = (int)i;
+                r.tmax = dd;
+            }
+        }
+        V3 hp, hn;
+        float kd = 0.0f;
+        V3 diff = v3(0.0f, 0.0f, 0.0f);
+        if (hit >= 0) {
+            const rt_sphere &s = sph[hit];
+            hp = v3(r.o.x + r.d.x * r.tmax, r.o.y + r.d.y * r.tmax, r.o.z + r.d.z * r.tmax);
+            const float inv_r = 1.0f / s.radius; /* sphereNormal, geometryFuncs.h:58-69 */
+            hn = v3((hp.x - s.center.x) * inv_r, (hp.y - s.center.y) * inv_r, (hp.z - s.center.z) * inv_r);
+            if (r.ext.x > 0.0f) r.prop.x *= rt_expf(rt_logf(r.ext.x) * r.tmax);
+            if (r.ext.y > 0.0f) r.prop.y *= rt_expf(rt_logf(r.ext.y) * r.tmax);
+            if (r.ext.z > 0.0f) r.prop.z *= rt_expf(rt_logf(r.ext.z) * r.tmax);
+            if (!r.diffuse && s.mat.emission_power != 0) {
+                color.x += r.prop.x * s.mat.emission.x;
+                color.y += r.prop.y * s.mat.emission.y;
+                color.z += r.prop.z * s.mat.emission.z;
+            }
+            kd = s.mat.kd;
+            diff = v3f(s.mat.diffuse);
+        } else {
+            const float hd = intersect_box(r.o, r.d, r.tmin, bw, bh, bw);
+            if (!(hd > r.tmin && hd < r.tmax)) break;
+            r.tmax = hd;
+            hp = v3(r.o.x + r.d.x * r.tmax, r.o.y + r.d.y * r.tmax, r.o.z + r.d.z * r.tmax);
+            hn = box_normal(hp, bw, bh, bw);
+        }
+        /* sample_direct_illumination, rtcommon.h:148-174 (box, or kd > 0) */
+        V3 direct = v3(0.0f, 0.0f, 0.0f);
+        if (hit < 0 || kd > 0.0f) {
+            const V3 so = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
+            const float inv_samples = 1.0f / (float)RT_LIGHT_SAMPLES;
+            for (uint32_t k = 0; k < n; ++k) {
+                if (sph[k].mat.emission_power != 0) {
+                    const V3 lc = v3f(sph[k].center);
+                    const float lr = sph[k].radius;
+                    for (int i = 0; i < (int)RT_LIGHT_SAMPLES; ++i) {
+                        const float r1 = frand(seed);
+                        const float r2 = strat_rand(seed, i, (int)RT_LIGHT_SAMPLES);
+                        float stmax;
+                        const V3 sd = sphere_light_dir(so, lc, lr, r1, r2, stmax);
+                        ++n_shadow;
+                        bool vis = true; /* visibility_test, rtcommon.h:128-138 */
+                        for (uint32_t j = 0; j < n; ++j) {
+                            const float dd = intersect_sphere(so, sd, RT_SMALL_F, v3f(sph[j].center), sph[j].radius);
+                            if (dd > RT_SMALL_F && dd < stmax) {
+                                vis = false;
+                                break;
+                            }
+                        }
+                        if (vis) {
+                            const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
+                            if (cw > 0) {
+                                direct.x += sph[k].mat.emission.x * cw * inv_samples;
+                                direct.y += sph[k].mat.emission.y * cw * inv_samples;
+                                direct.z += sph[k].mat.emission.z * cw * inv_samples;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (hit >= 0) {
+            if (kd > 0.0f) {
+                const float scale = kd * RT_M_1_PI_F;
+                color.x += r.prop.x * direct.x * diff.x * scale;
+                color.y += r.prop.y * direct.y * diff.y * scale;
+                color.z += r.prop.z * direct.z * diff.z * scale;
+            }
+            if (depth == max_depth) break;
+            if (!sample_material(r, hp, hn, sph[hit].mat, seed)) break;
+        } else {
+            const float scale = RT_M_1_PI_F;
+            r.prop.x *= 0.7f;
+            r.prop.y *= 0.7f;
+            r.prop.z *= 0.7f;
+            color.x += r.prop.x * direct.x * scale;
+            color.y += r.prop.y * direct.y * scale;
+            color.z += r.prop.z * direct.z * scale;
+            r.o = hp;
+            r.tmin = RT_SMALL_F;
+            r.tmax = kInf;
+            const float r1 = frand(seed);
+            const float r2 = frand(seed);
+            r.d = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
+            r.diffuse = 1;
+        }
+    }
+    return color;
+}
+
+template <bool SS>
+__global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
+{
+    /* 16 x 16 pixel tile per block; a wave covers 16 x 4 pixels */
+    const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u);
+    const uint32_t yl = blockIdx.y * 16u + (threadIdx.x >> 4);
+    unsigned long long n_closest = 0, n_shadow = 0;
+    if (x < a.W && yl < a.Hl) {
+        const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+        const uint32_t plane = a.Wpad * a.Hpad;
+        /* get_seed (raytracer.cl:20-24): rows shifted by `progressive`; raytrace_ss unshifted */
+        const uint32_t slot = SS ? (y * a.Wpad + x) : (((y + a.progressive) % a.Hpad) * a.Wpad + x);
+        Seed seed = {a.seeds[slot], a.seeds[plane + slot]};
+        const float hw = ((float)a.W) / 2.0f, hh = ((float)a.H) / 2.0f;
+        float4 pc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (SS) {
+            const float fa = (float)x + frand(seed);
+            const float fb = (float)y + frand(seed);
+            PathRay r;
+            r.o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+            r.d = camera_dir(a.cam, fa - hw, fb - hh);
+            r.tmin = RT_SMALL_F;
+            r.tmax = kInf;
+            r.prop = v3(1.0f, 1.0f, 1.0f);
+            r.ext = v3(0.0f, 0.0f, 0.0f);
+            r.diffuse = 0;
+            const V3 c = trace_path(r, a.spheres, a.n_spheres, a.max_depth, seed, n_closest, n_shadow);
+            pc = make_float4(c.x, c.y, c.z, 0.0f);
+        } else {
+            const uint32_t sr = a.sample_rate;
+            for (uint32_t sx = 0; sx < sr; ++sx) {
+                for (uint32_t sy = 0; sy < sr; ++sy) {
+                    const float fa = (float)x + strat_rand(seed, (int)sx, (int)sr);
+                    const float fb = (float)y + strat_rand(seed, (int)sy, (int)sr);
+                    PathRay r;
+                    r.o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+                    r.d = camera_dir(a.cam, fa - hw, fb - hh);
+                    r.tmin = RT_SMALL_F;
+                    r.tmax = kInf;
+                    r.prop = v3(1.0f, 1.0f, 1.0f);
+                    r.ext = v3(0.0f, 0.0f, 0.0f);
+                    r.diffuse = 0;
+                    const V3 c = trace_path(r, a.spheres, a.n_spheres, a.max_depth, seed, n_closest, n_shadow);
+                    pc.x += c.x;
+                    pc.y += c.y;
+                    pc.z += c.z;
+                }
+            }
+            const float n = (float)(sr * sr);
+            pc.x /= n;
+            pc.y /= n;
+            pc.z /= n;
+            pc.w /= n;
+        }
+        float4 *dst = reinterpret_cast<float4 *>(a.out) + ((size_t)yl * a.W + x);
+        if (a.progressive > 0) {
+            const float4 old = *dst;
+            const float t = 1.0f / (float)a.progressive;
+            pc.x = old.x + (pc.x - old.x) * t;
+            pc.y = old.y + (pc.y - old.y) * t;
+            pc.z = old.z + (pc.z - old.z) * t;
+            pc.w = old.w + (pc.w - old.w) * t;
+        }
+        *dst = pc;
+        a.seeds[slot] = seed.x;
+        a.seeds[plane + slot] = seed.y;
+    }
+    flush_counters(a.counters, n_closest, n_shadow, 0, 0, false);
+}
+
+/* ======================================================================== */
+/* Batch ray queries (hit-index parity).                                     */
+template <bool LINEAR>
+__global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restrict__ nodes,
+                                                         const float4 *__restrict__ tris, uint32_t n_tris,
+                                                         const rt_ray *__restrict__ rays, uint32_t n, int any_hit,
+                                                         int32_t *__restrict__ out_idx, float *__restrict__ out_t)
+{
+    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
+    const uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const rt_ray r = rays[i];
+    float t = r.tmax;
+    TravCounts tc = {0u, 0u};
+    const int s = traverse<LINEAR, false>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0,
+                                          s_stack + threadIdx.x, tc);
+    if (any_hit) {
+        out_idx[i] = (s >= 0) ? 1 : 0;
+        if (out_t) out_t[i] = r.tmax;
+    } else {
+        out_idx[i] = (s >= 0) ? __float_as_int(tris[3 * s].w) : -1;
+        if (out_t) out_t[i] = t;
+    }
+}
+
+} // namespace
+
+/* ======================================================================== */
+/* Launchers                                                                 */
+
+int rt_launch_tris(const RtTriLaunch &a, bool linear, bool count, int grid_blocks, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((unsigned)grid_blocks), block(RT_BLOCK);
+    if (linear) {
+        if (count) hipLaunchKernelGGL((k_tris<true, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_tris<true, false>), grid, block, 0, st, a);
+    } else {
+        if (count) hipLaunchKernelGGL((k_tris<false, true>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_tris<false, false>), grid, block, 0, st, a);
+    }
+    return (int)hipGetLastError();
+}
+
+int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((a.W + 15u) / 16u, (a.Hl + 15u) / 16u), block(RT_BLOCK);
+    if (single_sample) hipLaunchKernelGGL((k_spheres<true>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_spheres<false>), grid, block, 0, st, a);
+    return (int)hipGetLastError();
+}
+
+int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
+                         int any_hit, bool linear, int32_t *out_idx, float *out_t, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK), block(RT_BLOCK);
+    const float4 *nd = reinterpret_cast<const float4 *>(nodes);
+    const float4 *tr = reinterpret_cast<const float4 *>(tris);
+    if (linear)
+        hipLaunchKernelGGL((k_trace_rays<true>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, out_idx, out_t);
+    else
+        hipLaunchKernelGGL((k_trace_rays<false>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, out_idx,
+                           out_t);
+    return (int)hipGetLastError();
+}
+
+int rt_tris_grid_blocks(int device, bool linear, bool count, int *blocks)
+{
+    int per_cu = 0;
+    hipError_t e;
+    if (linear)
+        e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<true, true>, RT_BLOCK, 0)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<true, false>, RT_BLOCK, 0);
+    else
+        e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<false, true>, RT_BLOCK, 0)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<false, false>, RT_BLOCK, 0);
+    if (e != hipSuccess) return (int)e;
+    int n_cu = 0;
+    e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return (int)e;
+    if (per_cu < 1) per_cu = 1;
+    *blocks = per_cu * n_cu;
+    return 0;
+}

@@ -1,0 +1,71 @@
+"""Multi-GPU frame sharding: one process per GPU, interleaved row stripes, RCCL gather.
+
+Every pixel of raytrace_tris is independent (its own seed slot, its own read-modify-write
+of its output pixel — raytracer.cl:207-242), so a frame splits into row stripes dealt
+round-robin over ranks (load balance: the mesh sits mid-frame).  Each rank keeps a full
+scene/BVH replica and the full seed planes, renders its rows into a compact local
+framebuffer (rt_tile), and the frame is assembled on the root with ONE collective: a
+gather of the compact tiles over RCCL (torch.distributed backend "nccl" = RCCL on ROCm),
+which over xGMI is one point-to-point transfer per sender.
+
+Progressive accumulation stays local (each rank mixes into its own rows), so the gather is
+only needed when the root wants to display/store the frame.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def tile_rows(height: int, stripe: int, n_ranks: int, rank: int) -> np.ndarray:
+    """Global row indices owned by `rank`, in the order they are stored (rt_tile_rows)."""
+    y = np.arange(height)
+    return y[(y // stripe) % n_ranks == rank]
+
+
+def max_tile_rows(height: int, stripe: int, n_ranks: int) -> int:
+    return max(len(tile_rows(height, stripe, n_ranks, r)) for r in range(n_ranks))
+
+
+def assemble(tiles, height: int, width: int, stripe: int):
+    """Scatter gathered compact tiles (rank order; each [>=rows_r, W, 4]) into a full
+    [H, W, 4] frame.  Works on numpy arrays or torch tensors."""
+    n = len(tiles)
+    first = tiles[0]
+    if isinstance(first, np.ndarray):
+        full = np.empty((height, width, 4), first.dtype)
+    else:
+        import torch
+
+        full = torch.empty((height, width, 4), dtype=first.dtype, device=first.device)
+    for r, t in enumerate(tiles):
+        rows = tile_rows(height, stripe, n, r)
+        if len(rows) == 0:
+            continue
+        t = t.reshape(-1, width, 4)[: len(rows)]
+        if isinstance(full, np.ndarray):
+            full[rows] = t
+        else:
+            import torch
+
+            full[torch.as_tensor(rows, device=full.device)] = t
+    return full
+
+
+def gather_frame(local, height: int, width: int, stripe: int, group=None, root: int = 0):
+    """Gather every rank's compact tile to `root` with one torch.distributed.gather
+    (RCCL over xGMI for CUDA tensors; gloo on CPU).  `local` is the rank's framebuffer
+    padded to max_tile_rows rows.  Returns the assembled [H, W, 4] frame on root, else None."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    rows_max = max_tile_rows(height, stripe, world)
+    local = local.reshape(-1)[: rows_max * width * 4]
+    if local.numel() != rows_max * width * 4:
+        raise ValueError("local framebuffer must hold max_tile_rows rows")
+    gathered = [torch.empty_like(local) for _ in range(world)] if rank == root else None
+    dist.gather(local, gathered, dst=root, group=group)
+    if rank != root:
+        return None
+    return assemble([g.reshape(rows_max, width, 4) for g in gathered], height, width, stripe)

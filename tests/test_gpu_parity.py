@@ -1,0 +1,308 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the reference fixtures and the oracle.
+
+Bar: bit-exact radiance, seeds and hit indices (the arithmetic model is pinned, so the
+north-star's 1e-5 relative tolerance is met with zero error).  Run on the
+MI355X box with `pytest -m gpu`.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import bits
+
+pytestmark = pytest.mark.gpu
+
+SPHERE_CASES = ["spheres_64x64_sr1", "spheres_48x40_sr2", "spheres_ss_64x64"]
+TRI_CASES = ["tris_64x48_sr1", "tris_40x30_sr2"]
+
+
+def _setup(rt, pt, g, m, kernel_tris=False):
+    rt.setSpheres(g["spheres"].view(pt._abi.SPHERE_DTYPE))
+    rt.setCamera(g["camera"])
+    rt.setSampleRate(m["sample_rate"])
+    rt.setMaxPathDepth(m["max_depth"])
+    rt.setNDRange(m["nd_y"])
+    if kernel_tris:
+        rt.setMesh(g["verts"], g["idx"])
+    # a fresh size so the seed layout below is the one consumed
+    rt.setSeeds(m["Wpad"], m["Hpad"], g["seeds_in"])
+
+
+@pytest.mark.parametrize("name", SPHERE_CASES)
+def test_golden_spheres(name, tracer, pt, golden, golden_meta):
+    g, m = golden(name), golden_meta["cases"][name]
+    rt = pt.RayTracer(0)
+    _setup(rt, pt, g, m)
+    out = np.zeros(m["W"] * m["H"] * 4, np.float32)
+    for p in range(m["frames"]):
+        rt.rayTrace(out, m["W"], m["H"], p, kernel=m["kernel"])
+        np.testing.assert_array_equal(bits(out), bits(g["frames"][p]), err_msg=f"{name} frame {p}")
+    np.testing.assert_array_equal(rt.getSeeds(), g["seeds_out"])
+    rt.close()
+
+
+@pytest.mark.parametrize("linear", [False, True])
+@pytest.mark.parametrize("name", TRI_CASES)
+def test_golden_tris(name, linear, tracer, pt, golden, golden_meta):
+    g, m = golden(name), golden_meta["cases"][name]
+    rt = pt.RayTracer(0)
+    _setup(rt, pt, g, m, kernel_tris=True)
+    rt.setTraversal(linear)
+    out = np.zeros(m["W"] * m["H"] * 4, np.float32)
+    for p in range(m["frames"]):
+        rt.rayTrace(out, m["W"], m["H"], p, kernel=2)
+        np.testing.assert_array_equal(bits(out), bits(g["frames"][p]), err_msg=f"{name} frame {p}")
+    np.testing.assert_array_equal(rt.getSeeds(), g["seeds_out"])
+    rt.close()
+
+
+@pytest.mark.parametrize("linear", [False, True])
+def test_golden_hit_indices(linear, tracer, pt, golden):
+    g = golden("hits_2000")
+    R = pt._abi.RAY_DTYPE
+    tracer.setMesh(g["verts"], g["idx"])
+    tracer.setTraversal(linear)
+    for key in ("primary", "random"):
+        idx, t = tracer.traceRays(g[f"{key}_rays"].view(R))
+        np.testing.assert_array_equal(idx, g[f"{key}_hit"])
+        np.testing.assert_array_equal(bits(t), bits(g[f"{key}_t"]))
+    occ, _ = tracer.traceRays(g["shadow_rays"].view(R), any_hit=True)
+    np.testing.assert_array_equal(occ, g["shadow_occluded"])
+    tracer.setTraversal(False)
+
+
+def test_spheres_vs_oracle_progressive(tracer, pt, oracle):
+    sc = pt.scenes
+    W, H, sr, frames = 200, 150, 2, 3
+    Wp, Hp = sc.padded_dims(W, H)
+    S = sc.main_scene()
+    cam = sc.camera_spherical(W, **sc.MAIN_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=1234)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    for p in range(frames):
+        rt.rayTrace(got, W, H, p, kernel=0)
+        c_or = oracle.render_spheres(exp, cam, S, W, H, Wp, Hp, sr, 6, p, sd)
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
+        c = rt.counters()
+        assert (c["rays_closest"], c["rays_shadow"]) == c_or
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
+    rt.close()
+
+
+@pytest.mark.parametrize("n_tris", [69_451])
+def test_tris_vs_oracle_mesh(n_tris, tracer, pt, oracle):
+    """Bunny-class mesh, BVH traversal, against the oracle's linear loop."""
+    sc = pt.scenes
+    W, H, sr = 48, 36, 1
+    Wp, Hp = sc.padded_dims(W, H)
+    S = sc.ply_scene()
+    verts, idx = sc.make_mesh(n_tris)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=99)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    rt.rayTrace(got, W, H, 0, kernel=2)
+    c_or = oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx)
+    np.testing.assert_array_equal(bits(got), bits(exp))
+    c = rt.counters()
+    assert (c["rays_closest"], c["rays_shadow"]) == c_or
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
+    rt.close()
+
+
+def test_bvh_equals_linear_dragon(tracer, pt):
+    """Dragon-class mesh: closest-hit indices/t and any-hit flags, BVH vs the linear loop."""
+    sc = pt.scenes
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    cam = sc.camera_spherical(320, **sc.PLY_CAMERA)
+    rays = sc.camera_rays(cam, 320, 180)
+    rng = np.random.default_rng(7)
+    n = 16384
+    rr = np.zeros(n, pt._abi.RAY_DTYPE)
+    rr["o"] = rng.uniform([-5.5, -4.9, -5.5], [5.5, 4.9, 5.5], (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    rr["d"] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rr["tmin"] = np.float32(1e-4)
+    rr["tmax"] = np.float32(np.inf)
+    rs = rr.copy()
+    rs["tmax"] = rng.uniform(0.0, 8.0, n).astype(np.float32)
+    rt = tracer
+    rt.setMesh(verts, idx)
+    res = {}
+    for linear in (False, True):
+        rt.setTraversal(linear)
+        res[linear] = (rt.traceRays(rays), rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
+    rt.setTraversal(False)
+    for k in range(3):
+        np.testing.assert_array_equal(res[False][k][0], res[True][k][0])
+        np.testing.assert_array_equal(bits(res[False][k][1]), bits(res[True][k][1]))
+    assert (res[False][0][0] >= 0).mean() > 0.2  # visible
+
+
+def test_bvh_equals_linear_fuzz_grazing(tracer, pt):
+    """Large triangles and near-grazing rays stress the conservative culling margins."""
+    rng = np.random.default_rng(11)
+    nt = 3000
+    v = rng.uniform(-4, 4, (nt * 3, 3)).astype(np.float32)
+    idx = np.arange(nt * 3, dtype=np.int32).reshape(nt, 3)
+    # a few exactly coplanar / duplicated triangles to exercise the tie rule
+    v[3:6] = v[0:3]
+    v[9:12] = v[6:9][[1, 2, 0]]
+    n = 32768
+    rr = np.zeros(n, pt._abi.RAY_DTYPE)
+    tgt = v[rng.integers(0, nt * 3, n)] + rng.normal(scale=0.05, size=(n, 3)).astype(np.float32)
+    o = rng.uniform(-6, 6, (n, 3)).astype(np.float32)
+    d = tgt - o
+    rr["o"] = o
+    rr["d"] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rr["tmin"] = np.float32(1e-4)
+    rr["tmax"] = np.where(rng.uniform(size=n) < 0.5, np.inf, rng.uniform(0, 10, n)).astype(np.float32)
+    rt = tracer
+    rt.setMesh(v, idx)
+    out = {}
+    for linear in (False, True):
+        rt.setTraversal(linear)
+        out[linear] = (rt.traceRays(rr), rt.traceRays(rr, any_hit=True))
+    rt.setTraversal(False)
+    np.testing.assert_array_equal(out[False][0][0], out[True][0][0])
+    np.testing.assert_array_equal(bits(out[False][0][1]), bits(out[True][0][1]))
+    np.testing.assert_array_equal(out[False][1][0], out[True][1][0])
+
+
+@pytest.mark.parametrize("kernel,prog", [(2, 0), (2, 3), (0, 0), (1, 2)])
+def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt):
+    """Row-stripe tiles (the multi-GPU partition) reassemble to the single-device frame."""
+    sc = pt.scenes
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    W, H, sr = 72, 53, 1
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(5000)
+    seeds = sc.default_seeds(Wp, Hp)
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    prev = np.random.default_rng(3).uniform(0, 1, (H, W, 4)).astype(np.float32)
+
+    def make():
+        rt = pt.RayTracer(0)
+        rt.setSpheres(S)
+        rt.setCamera(cam)
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        return rt
+
+    rt = make()
+    full = prev.copy().reshape(-1)
+    rt.rayTrace(full, W, H, prog, kernel=kernel)
+    full_seeds = rt.getSeeds()
+    rt.close()
+    for n_ranks, stripe in [(2, 8), (3, 5), (4, 16)]:
+        tiles = []
+        for r in range(n_ranks):
+            rows = dist.tile_rows(H, stripe, n_ranks, r)
+            rt = make()
+            t = np.ascontiguousarray(prev[rows]).reshape(-1)
+            rt.rayTrace(t, W, H, prog, kernel=kernel, tile=(stripe, n_ranks, r))
+            s = rt.getSeeds().reshape(2, Hp, Wp)
+            np.testing.assert_array_equal(s[:, rows], full_seeds.reshape(2, Hp, Wp)[:, rows])
+            rt.close()
+            tiles.append(t.reshape(len(rows), W, 4))
+        frame = dist.assemble(tiles, H, W, stripe)
+        np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full))
+
+
+def test_device_framebuffer_matches_host(tracer, pt):
+    import torch
+
+    sc = pt.scenes
+    W, H = 96, 64
+    Wp, Hp = sc.padded_dims(W, H)
+    seeds = sc.default_seeds(Wp, Hp)
+    rt = tracer
+    rt.setSpheres(sc.ply_scene())
+    rt.setCamera(sc.camera_spherical(W, **sc.PLY_CAMERA))
+    rt.setSampleRate(2)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(*sc.make_mesh(20000))
+    host = np.zeros(W * H * 4, np.float32)
+    dev = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
+    for out in (host, dev):
+        rt.setSeeds(Wp, Hp, seeds)
+        for p in range(2):
+            rt.rayTrace(out, W, H, p, kernel=2)
+    np.testing.assert_array_equal(bits(host), bits(dev.cpu().numpy()))
+
+
+def test_dragon_full_size_properties(tracer, pt, oracle):
+    """BASELINE config 4 at full size (1920x1080, 871k tris), sampleRate 1 for the oracle
+    subset: a strided pixel subset is bit-exact against the oracle's linear loop; the frame
+    is finite, alpha 0, deterministic, and every pixel's seed advanced."""
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 1
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp)
+    rt = tracer
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    out = np.zeros(W * H * 4, np.float32)
+    rt.setSeeds(Wp, Hp, seeds)
+    rt.rayTrace(out, W, H, 0, kernel=2)
+    s_gpu = rt.getSeeds()
+    out2 = np.zeros_like(out)
+    rt.setSeeds(Wp, Hp, seeds)
+    rt.rayTrace(out2, W, H, 0, kernel=2)
+    np.testing.assert_array_equal(bits(out), bits(out2))
+    img = out.reshape(H, W, 4)
+    assert np.isfinite(img).all() and (img[..., 3] == 0).all() and img[..., :3].max() > 0
+    changed = (s_gpu.reshape(2, Hp, Wp)[:, :H, :W] != seeds.reshape(2, Hp, Wp)[:, :H, :W]).any(0)
+    assert changed.all()
+    pix = np.arange(0, W * H, 32_407, dtype=np.uint32)  # 64 pixels spread over the frame
+    exp = np.zeros_like(out)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix)
+    e = exp.reshape(-1, 4)[pix]
+    gpx = out.reshape(-1, 4)[pix]
+    np.testing.assert_array_equal(bits(gpx), bits(e))
+
+
+def test_errors_are_loud(tracer, pt):
+    rt = pt.RayTracer(0)
+    out = np.zeros(16 * 16 * 4, np.float32)
+    with pytest.raises(pt.RtError):
+        rt.rayTrace(out, 16, 16, 0, kernel=0)  # no spheres
+    rt.setSpheres(pt.scenes.main_scene())
+    with pytest.raises(pt.RtError):
+        rt.rayTrace(out, 16, 16, 0, kernel=2)  # no mesh
+    with pytest.raises(pt.RtError):
+        rt.rayTrace(out, 16, 16, 1, kernel=0, tile=(4, 2, 0))  # shifted seeds cross stripes
+    with pytest.raises(pt.RtError):
+        rt.setMesh(np.array([[0, 0, 0], [1, 0, 0], [np.nan, 1, 0]], np.float32), np.array([[0, 1, 2]], np.int32))
+    with pytest.raises(pt.RtError):
+        rt.setMesh(np.zeros((3, 3), np.float32), np.array([[0, 1, 3]], np.int32))
+    rt.close()

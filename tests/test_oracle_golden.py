@@ -1,0 +1,189 @@
+"""Pin the CPU oracle (oracle/pt_oracle.c) against the reference's own outputs.
+
+Every fixture in tests/golden/ was produced by the reference kernel clrt/ocl/raytracer.cl
+compiled unchanged for x86-64 (tests/golden/make_golden.py).  The oracle restatement must
+reproduce each of them bit for bit — whole frames over several progressive passes, the
+seed planes it leaves behind, closest/any-hit triangle queries and the per-function
+known answers.  CPU only.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import bits
+
+SPHERE_CASES = ["spheres_64x64_sr1", "spheres_48x40_sr2", "spheres_ss_64x64"]
+TRI_CASES = ["tris_64x48_sr1", "tris_40x30_sr2"]
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+@pytest.mark.parametrize("name", SPHERE_CASES)
+def test_sphere_frames_bit_exact(name, golden, golden_meta, oracle, pt):
+    g = golden(name)
+    m = golden_meta["cases"][name]
+    spheres = g["spheres"].view(pt._abi.SPHERE_DTYPE)
+    out = np.zeros(m["W"] * m["H"] * 4, np.float32)
+    seeds = g["seeds_in"].copy()
+    for p in range(m["frames"]):
+        oracle.render_spheres(out, g["camera"], spheres, m["W"], m["H"], m["Wpad"], m["Hpad"], m["sample_rate"],
+                              m["max_depth"], p, seeds, single_sample=(m["kernel"] == 1))
+        np.testing.assert_array_equal(bits(out), bits(g["frames"][p]), err_msg=f"frame {p}")
+    np.testing.assert_array_equal(seeds, g["seeds_out"])
+
+
+@pytest.mark.parametrize("name", TRI_CASES)
+def test_tri_frames_bit_exact(name, golden, golden_meta, oracle, pt):
+    g = golden(name)
+    m = golden_meta["cases"][name]
+    spheres = g["spheres"].view(pt._abi.SPHERE_DTYPE)
+    out = np.zeros(m["W"] * m["H"] * 4, np.float32)
+    seeds = g["seeds_in"].copy()
+    for p in range(m["frames"]):
+        oracle.render_tris(out, g["camera"], spheres, m["W"], m["H"], m["Wpad"], m["Hpad"], m["sample_rate"],
+                           m["max_depth"], p, seeds, g["verts"], g["idx"])
+        np.testing.assert_array_equal(bits(out), bits(g["frames"][p]), err_msg=f"frame {p}")
+    np.testing.assert_array_equal(seeds, g["seeds_out"])
+
+
+def test_alpha_channel_zero(golden):
+    for name in SPHERE_CASES + TRI_CASES:
+        f = golden(name)["frames"].reshape(-1, 4)
+        assert np.all(f[:, 3] == 0.0)
+
+
+def test_hit_queries(golden, oracle, pt):
+    g = golden("hits_2000")
+    R = pt._abi.RAY_DTYPE
+    for key in ("primary", "random"):
+        rays = g[f"{key}_rays"].view(R)
+        idx, t = oracle.closest_hits(rays, g["verts"], g["idx"])
+        np.testing.assert_array_equal(idx, g[f"{key}_hit"])
+        np.testing.assert_array_equal(bits(t), bits(g[f"{key}_t"]))
+    occ = oracle.any_hits(g["shadow_rays"].view(R), g["verts"], g["idx"])
+    np.testing.assert_array_equal(occ, g["shadow_occluded"])
+    assert 0.3 < (g["primary_hit"] >= 0).mean() < 1.0  # the mesh is visible and not everywhere
+
+
+def test_kat_frand(golden, oracle):
+    g = golden("kat")
+    L = oracle.lib
+    L.or_frand.argtypes = [ctypes.c_void_p]
+    L.or_frand.restype = ctypes.c_float
+    for s, expect in zip(g["frand_seeds"], g["frand"]):
+        st = s.copy()
+        got = np.array([L.or_frand(_p(st)) for _ in range(expect.size)], np.float32)
+        np.testing.assert_array_equal(bits(got), bits(expect))
+
+
+def test_kat_triangle(golden, oracle, pt):
+    g = golden("kat")
+    L = oracle.lib
+    L.or_intersects_triangle.argtypes = [ctypes.c_void_p] * 4
+    L.or_intersects_triangle_p.argtypes = [ctypes.c_void_p] * 2
+    rays = g["tri_rays"].view(pt._abi.RAY_DTYPE)
+    for k in range(len(rays)):
+        r = rays[k:k + 1].copy()
+        u = np.zeros(1, np.float32)
+        v = np.zeros(1, np.float32)
+        tr = g["tri"][k].copy()
+        assert L.or_intersects_triangle_p(_p(r), _p(tr)) == g["tri_p"][k]
+        assert L.or_intersects_triangle(_p(r), _p(u), _p(v), _p(tr)) == g["tri_hit"][k]
+        got = np.array([u[0], v[0], r["tmax"][0]], np.float32)
+        np.testing.assert_array_equal(bits(got), bits(g["tri_uvt"][k]))
+    assert 0.2 < g["tri_hit"].mean() < 0.9
+
+
+def test_kat_sphere_and_box(golden, oracle, pt):
+    g = golden("kat")
+    L = oracle.lib
+    L.or_kat_intersect_sphere.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float]
+    L.or_kat_intersect_sphere.restype = ctypes.c_float
+    L.or_intersects_box.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+    L.or_intersects_box.restype = ctypes.c_float
+    L.or_box_normal.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+    rays = g["tri_rays"].view(pt._abi.RAY_DTYPE)
+    brays = g["box_rays"].view(pt._abi.RAY_DTYPE)
+    sd = np.zeros(len(rays), np.float32)
+    bt = np.zeros(len(rays), np.float32)
+    bn = np.zeros((len(rays), 3), np.float32)
+    for k in range(len(rays)):
+        c = g["sph_c"][k].copy()
+        sd[k] = L.or_kat_intersect_sphere(_p(rays[k:k + 1].copy()), _p(c), float(g["sph_r"][k]))
+        rb = brays[k:k + 1].copy()
+        bt[k] = L.or_intersects_box(_p(rb), 6.0, 5.0, 6.0)
+        hit = np.zeros(6, np.float32)
+        hit[:3] = rb["o"][0] + rb["d"][0] * bt[k]
+        L.or_box_normal(_p(hit), 6.0, 5.0, 6.0)
+        bn[k] = hit[3:]
+    np.testing.assert_array_equal(bits(sd), bits(g["sph_d"]))
+    np.testing.assert_array_equal(bits(bt), bits(g["box_t"]))
+    np.testing.assert_array_equal(bits(bn), bits(g["box_n"]))
+
+
+def test_kat_sample_material(golden, oracle, pt):
+    g = golden("kat")
+    L = oracle.lib
+    L.or_sample_material.argtypes = [ctypes.c_void_p] * 4
+    R = pt._abi.RAY_DTYPE
+    rin, rout = g["mat_in"].view(R), g["mat_out"].view(R)
+    mats = g["mats"].view(pt._abi.SPHERE_DTYPE)
+    for k in range(len(rin)):
+        r = rin[k:k + 1].copy()
+        h = g["mat_hits"][k].copy()
+        mm = mats[g["mat_idx"][k]:g["mat_idx"][k] + 1].copy()
+        s = g["mat_seed"][k].copy()
+        assert L.or_sample_material(_p(r), _p(h), _p(mm), _p(s)) == g["mat_ret"][k]
+        np.testing.assert_array_equal(s, g["mat_seed_out"][k])
+        assert r.tobytes() == rout[k:k + 1].tobytes(), k
+
+
+def test_kat_emissive(golden, oracle, pt):
+    g = golden("kat")
+    L = oracle.lib
+    L.or_kat_emissive.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+    R = pt._abi.RAY_DTYPE
+    rin, rout = g["em_rays"].view(R), g["em_out"].view(R)
+    c = g["light_c"].copy()
+    for k in range(len(rin)):
+        r = rin[k:k + 1].copy()
+        L.or_kat_emissive(_p(r), _p(c), 0.5, float(g["em_r12"][k, 0]), float(g["em_r12"][k, 1]))
+        assert r.tobytes() == rout[k:k + 1].tobytes(), k
+
+
+def test_host_camera_matches_gmtl(golden, golden_meta, pt):
+    """librtmi's restated camera math == the reference host math compiled against gmtl."""
+    g = golden("kat")
+    for w, setup, expect in zip(g["cam_widths"], golden_meta["cases"]["kat"]["cameras"], g["cams"]):
+        s = dict(setup)
+        s.pop("width")
+        cam = pt.scenes.camera_spherical(int(w), **s)
+        np.testing.assert_array_equal(bits(cam), bits(expect))
+
+
+def test_math_model_sanity(oracle):
+    """The pinned transcendentals are accurate (<= 4 ulp on the kernels' argument ranges)."""
+    L = oracle.lib
+    x = np.linspace(0, 2 * np.pi, 4001, dtype=np.float32)
+    for f, ref in (("sin", np.sin), ("cos", np.cos)):
+        got = np.array([getattr(L, f"or_math_{f}")(float(v)) for v in x], np.float32)
+        err = np.abs(got.astype(np.float64) - ref(x.astype(np.float64)))
+        assert err.max() < 4 * np.finfo(np.float32).eps
+    y = np.linspace(-20, 5, 2001, dtype=np.float32)
+    got = np.array([L.or_math_exp(float(v)) for v in y], np.float32)
+    rel = np.abs(got / np.exp(y.astype(np.float64)) - 1)
+    assert rel.max() < 4 * np.finfo(np.float32).eps
+    z = np.linspace(1e-6, 3, 2001, dtype=np.float32)
+    got = np.array([L.or_math_log(float(v)) for v in z], np.float32)
+    err = np.abs(got - np.log(z.astype(np.float64)))
+    assert np.all(err <= 4 * np.finfo(np.float32).eps * np.maximum(1, np.abs(np.log(z))))
+    r1 = np.linspace(0, 1, 1001, dtype=np.float32)[:-1]
+    for e in (100.0, 1000.0, 50.0):
+        got = np.array([L.or_math_pow(float(a), 1.0 / (e + 1.0)) for a in r1], np.float32)
+        ref = np.power(r1.astype(np.float64), 1.0 / np.float64(np.float32(1.0) / np.float32(e + 1.0)) ** -1)
+        assert np.allclose(got, ref, rtol=2e-7, atol=0)

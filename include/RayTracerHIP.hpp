@@ -1,0 +1,133 @@
+/*
+ * RayTracerHIP.hpp — header-only C++ host class over the C-ABI (librtmi.so).
+ *
+ * The drop-in for the reference's C++ host API: the public surface of
+ * RayTracer (clrt/RayTracer.h:51-70) and RayTracerCL::rayTrace
+ * (clrt/RayTracerCL.h:111-112) with the same method names, argument meaning,
+ * defaults (fov 53, sampleRate 8, maxPathDepth 4: RayTracer.cpp:16-22) and
+ * RGBA32F framebuffer layout.  Like the reference (which throws cl::Error),
+ * failures throw — here std::runtime_error carrying the C-ABI status text.
+ *
+ * The scene is re-uploaded only when it changed, as RayTracerCL does when the
+ * sphere count changes (RayTracerCL.cpp:251-264).
+ */
+#ifndef RAYTRACER_HIP_HPP
+#define RAYTRACER_HIP_HPP
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pathtracer_rt.h"
+
+class RayTracerHIP {
+public:
+    explicit RayTracerHIP(int device = 0)
+    {
+        check(rt_create(device, &ctx_), "rt_create");
+        check(rt_set_params(ctx_, sampleRate_, maxPathDepth_), "rt_set_params");
+    }
+    ~RayTracerHIP()
+    {
+        if (ctx_) rt_destroy(ctx_);
+    }
+    RayTracerHIP(const RayTracerHIP &) = delete;
+    RayTracerHIP &operator=(const RayTracerHIP &) = delete;
+
+    /* ---- camera: RayTracer.h:56-60 ---- */
+    /* 4x4 matrix, column-major (gmtl's storage order). */
+    void setCameraMatrix(const float m_colmajor[16]) { check(rt_set_view_matrix(ctx_, m_colmajor), "setCameraMatrix"); }
+    void setCameraSpherical(const float target[3], float elevationDeg, float azimuthDeg, float distance)
+    {
+        check(rt_set_camera_spherical(ctx_, target[0], target[1], target[2], elevationDeg, azimuthDeg, distance),
+              "setCameraSpherical");
+    }
+    void setFoVAngle(float fovDeg)
+    {
+        fov_ = fovDeg;
+        check(rt_set_fov(ctx_, fovDeg), "setFoVAngle");
+    }
+    float getFoVAngle() const { return fov_; }
+
+    /* ---- settings: RayTracer.h:62-66 ---- */
+    void setSampleRate(unsigned s)
+    {
+        sampleRate_ = s;
+        check(rt_set_params(ctx_, sampleRate_, maxPathDepth_), "setSampleRate");
+    }
+    unsigned getSampleRate() const { return sampleRate_; }
+    void setMaxPathDepth(unsigned d)
+    {
+        maxPathDepth_ = d;
+        check(rt_set_params(ctx_, sampleRate_, maxPathDepth_), "setMaxPathDepth");
+    }
+    unsigned getMaxPathDepth() const { return maxPathDepth_; }
+
+    /* ---- scene: RayTracer.h:68-70 ---- */
+    void addSphere(const rt_sphere &s)
+    {
+        spheres_.push_back(s);
+        dirty_ = true;
+    }
+    /* The reference leaves removeSphere a stub (RayTracer.cpp:55-58); this removes
+       the first byte-identical sphere. */
+    void removeSphere(const rt_sphere &s)
+    {
+        for (size_t i = 0; i < spheres_.size(); ++i)
+            if (std::memcmp(&spheres_[i], &s, sizeof(rt_sphere)) == 0) {
+                spheres_.erase(spheres_.begin() + (long)i);
+                dirty_ = true;
+                return;
+            }
+    }
+    void clearSpheres()
+    {
+        spheres_.clear();
+        dirty_ = true;
+    }
+
+    /* ---- mesh for raytrace_tris (raytracer.cl:184-188); builds the BVH ---- */
+    void setMesh(const float *verts_xyz, unsigned n_verts, const int *idx, unsigned n_tris)
+    {
+        check(rt_set_mesh(ctx_, verts_xyz, n_verts, idx, n_tris), "setMesh");
+    }
+    void setTraversal(int traversal) { check(rt_set_traversal(ctx_, traversal), "setTraversal"); }
+
+    /* ---- RayTracerCL::rayTrace(cl_mem*, W, H, progression) ----
+       `buff` is W*H*4 floats; a device pointer when on_device, else host memory. */
+    void rayTrace(float *buff, unsigned width, unsigned height, unsigned progression,
+                  int kernel = RT_KERNEL_SPHERES, bool on_device = false, const rt_tile *tile = nullptr)
+    {
+        if (dirty_) {
+            check(rt_set_spheres(ctx_, spheres_.empty() ? nullptr : spheres_.data(), (uint32_t)spheres_.size()),
+                  "scene upload");
+            dirty_ = false;
+        }
+        check(rt_render(ctx_, buff, width, height, progression, kernel, tile, on_device ? RT_OUT_DEVICE : 0),
+              "rayTrace");
+    }
+
+    rt_counters counters() const
+    {
+        rt_counters c;
+        check(rt_get_counters(ctx_, &c), "counters");
+        return c;
+    }
+    rt_ctx *handle() { return ctx_; }
+
+private:
+    void check(int st, const char *what) const
+    {
+        if (st != RT_OK)
+            throw std::runtime_error(std::string(what) + ": " + rt_status_string(st) + " (" +
+                                     (ctx_ ? rt_last_error(ctx_) : "") + ")");
+    }
+    rt_ctx *ctx_ = nullptr;
+    std::vector<rt_sphere> spheres_;
+    bool dirty_ = true;
+    float fov_ = 53.0f;
+    unsigned sampleRate_ = 8, maxPathDepth_ = 4;
+};
+
+#endif /* RAYTRACER_HIP_HPP */

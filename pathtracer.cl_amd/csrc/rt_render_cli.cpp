@@ -1,0 +1,166 @@
+/*
+ * rt_render — headless C++ host over RayTracerHIP.hpp: the reference's
+ * clrt/main.cpp (sphere scene) and clrt/plymain.cpp (+ a triangle mesh) without
+ * the GLUT window.  Frames are driven like GlutCLWindow (progression 0, 1, 2, ...;
+ * GlutCLWindow.cpp:144-158) and the last frame is written as raw RGBA32F
+ * (W*H*4 little-endian floats) and/or a PFM.
+ *
+ *   rt_render [--scene main|ply] [--width W] [--height H] [--frames F]
+ *             [--sample-rate S] [--depth D] [--mesh N_TRIS] [--linear]
+ *             [--raw out.f32] [--pfm out.pfm] [--device K]
+ */
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "RayTracerHIP.hpp"
+
+namespace {
+
+/* init_material / init_sphere, clrt/main.cpp:13-42 */
+rt_sphere init_sphere()
+{
+    rt_sphere s;
+    std::memset(&s, 0, sizeof(s));
+    s.radius = 1.0f;
+    s.mat.specExp = 1000000.0f;
+    s.mat.ior = 1.0f;
+    s.mat.refExp = 1000000.0f;
+    return s;
+}
+
+/* clrt/main.cpp:44-110 (ply = clrt/plymain.cpp:45-111) */
+void add_scene(RayTracerHIP &rt, bool ply)
+{
+    rt_sphere s = init_sphere();
+    s.center = {-2.0f, -4.0f, -2.0f};
+    s.mat.kd = 1.0f;
+    s.mat.diffuse = {0.0f, 0.7f, 0.7f};
+    rt.addSphere(s);
+    s = init_sphere();
+    s.center = {2.0f, -3.0f, 2.0f};
+    s.mat.ks = 0.2f;
+    s.mat.kt = 0.8f;
+    s.mat.extinction = ply ? rt_vec3{0.95f, 0.85f, 0.90f} : rt_vec3{0.99f, 0.95f, 0.95f};
+    s.mat.ior = 1.1f;
+    rt.addSphere(s);
+    s = init_sphere();
+    s.center = {0.0f, -4.0f, 0.0f};
+    s.mat.ks = 1.0f;
+    rt.addSphere(s);
+    s = init_sphere();
+    s.center = {2.0f, -4.0f, -2.0f};
+    s.mat.kd = 0.2f;
+    s.mat.ks = 0.8f;
+    s.mat.diffuse = {0.7f, 0.7f, 0.0f};
+    s.mat.specExp = 100.0f;
+    rt.addSphere(s);
+    s = init_sphere();
+    s.center = {-2.0f, -4.0f, 2.0f};
+    s.mat.kd = 0.6f;
+    s.mat.ks = 0.4f;
+    s.mat.diffuse = {0.7f, 0.0f, 0.8f};
+    s.mat.specExp = 1000.0f;
+    rt.addSphere(s);
+    s = init_sphere();
+    s.center = ply ? rt_vec3{0.0f, 4.0f, 2.0f} : rt_vec3{2.2f, 1.0f, 2.0f};
+    s.radius = 0.5f;
+    s.mat.emission_power = 1.0f;
+    const float e = ply ? 1.1f : 1.8f;
+    s.mat.emission = {e, e, e};
+    rt.addSphere(s);
+}
+
+int usage()
+{
+    std::fprintf(stderr, "usage: rt_render [--scene main|ply] [--width W] [--height H] [--frames F] "
+                         "[--sample-rate S] [--depth D] [--mesh N] [--linear] [--raw f] [--pfm f] [--device K]\n");
+    return 2;
+}
+
+} // namespace
+
+int main(int argc, char **argv)
+{
+    std::string scene = "main", raw, pfm;
+    unsigned W = 512, H = 512, frames = 1, sr = 1, depth = 6, n_tris = 0;
+    int device = 0;
+    bool linear = false;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&]() -> const char * { return i + 1 < argc ? argv[++i] : nullptr; };
+        const char *v = nullptr;
+        if (a == "--linear") {
+            linear = true;
+            continue;
+        }
+        if (!(v = next())) return usage();
+        if (a == "--scene") scene = v;
+        else if (a == "--width") W = (unsigned)std::atoi(v);
+        else if (a == "--height") H = (unsigned)std::atoi(v);
+        else if (a == "--frames") frames = (unsigned)std::atoi(v);
+        else if (a == "--sample-rate") sr = (unsigned)std::atoi(v);
+        else if (a == "--depth") depth = (unsigned)std::atoi(v);
+        else if (a == "--mesh") n_tris = (unsigned)std::atoi(v);
+        else if (a == "--raw") raw = v;
+        else if (a == "--pfm") pfm = v;
+        else if (a == "--device") device = std::atoi(v);
+        else return usage();
+    }
+    const bool ply = scene == "ply" || n_tris > 0;
+    try {
+        RayTracerHIP rt(device);
+        add_scene(rt, ply);
+        rt.setSampleRate(sr);
+        rt.setMaxPathDepth(depth);
+        const float target[3] = {0.0f, -4.0f, 0.0f};
+        if (ply) rt.setCameraSpherical(target, 40.0f, 105.0f, 5.0f); /* plymain.cpp:115-117 */
+        else rt.setCameraSpherical(target, 14.0f, 118.0f, 5.0f);     /* main.cpp:127-128 */
+        int kernel = RT_KERNEL_SPHERES;
+        if (n_tris) {
+            std::vector<float> v(3ull * rt_mesh_vertex_count(n_tris));
+            std::vector<int> idx(3ull * n_tris);
+            if (rt_make_mesh(n_tris, 0.0f, -2.2f, 0.0f, 2.5f, v.data(), idx.data()) != RT_OK) return 1;
+            rt.setMesh(v.data(), (unsigned)(v.size() / 3), idx.data(), n_tris);
+            rt.setTraversal(linear ? RT_TRAVERSAL_LINEAR : RT_TRAVERSAL_BVH);
+            kernel = RT_KERNEL_TRIS;
+        }
+        float *dbuf = nullptr;
+        if (hipMalloc(&dbuf, (size_t)W * H * 16) != hipSuccess) return 1;
+        double rays = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned p = 0; p < frames; ++p) {
+            rt.rayTrace(dbuf, W, H, p, kernel, true);
+            const rt_counters c = rt.counters();
+            rays += (double)(c.rays_closest + c.rays_shadow);
+        }
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::vector<float> img((size_t)W * H * 4);
+        if (hipMemcpy(img.data(), dbuf, img.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+        (void)hipFree(dbuf);
+        std::printf("{\"frames\": %u, \"seconds\": %.6f, \"frames_per_sec\": %.4f, \"mrays_per_sec\": %.2f}\n", frames,
+                    dt, frames / dt, rays / dt / 1e6);
+        if (!raw.empty()) {
+            FILE *f = std::fopen(raw.c_str(), "wb");
+            if (!f || std::fwrite(img.data(), 4, img.size(), f) != img.size()) return 1;
+            std::fclose(f);
+        }
+        if (!pfm.empty()) { /* PFM: bottom-to-top rows, RGB, little-endian */
+            FILE *f = std::fopen(pfm.c_str(), "wb");
+            if (!f) return 1;
+            std::fprintf(f, "PF\n%u %u\n-1.0\n", W, H);
+            for (int y = (int)H - 1; y >= 0; --y)
+                for (unsigned x = 0; x < W; ++x) std::fwrite(&img[((size_t)y * W + x) * 4], 4, 3, f);
+            std::fclose(f);
+        }
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "rt_render: %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

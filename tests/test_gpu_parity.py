@@ -306,3 +306,22 @@ def test_errors_are_loud(tracer, pt):
     with pytest.raises(pt.RtError):
         rt.setMesh(np.zeros((3, 3), np.float32), np.array([[0, 1, 3]], np.int32))
     rt.close()
+
+
+@pytest.mark.parametrize("args,name", [(["--scene", "main", "--width", "64", "--height", "64", "--frames", "4"],
+                                        "spheres_64x64_sr1"),
+                                       (["--mesh", "2000", "--width", "64", "--height", "48", "--frames", "3"],
+                                        "tris_64x48_sr1")])
+def test_cpp_host_replays_reference_app(args, name, tracer, golden, tmp_path):
+    """The C++ host class (RayTracerHIP.hpp) driven like main.cpp / plymain.cpp + GlutCLWindow's
+    progression loop reproduces the reference kernel's frames from the default glibc seeds."""
+    import subprocess
+
+    from conftest import ROOT
+
+    raw = tmp_path / "out.f32"
+    subprocess.run([str(ROOT / "pathtracer.cl_amd" / "rt_render"), *args, "--raw", str(raw)], check=True,
+                   timeout=120)
+    got = np.fromfile(raw, np.float32)
+    exp = golden(name)["frames"][-1]
+    np.testing.assert_array_equal(bits(got), bits(exp))

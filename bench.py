@@ -64,9 +64,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = local_rank if world > 1 else 0
+        # one process per GPU; BENCH_DIST_BACKEND=gloo rehearses the N>1 path on one device
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        dev = local_rank % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    device = (local_rank % max(torch.cuda.device_count(), 1)) if world > 1 else 0
     torch.cuda.set_device(device)
 
     import ptload
@@ -179,6 +185,17 @@ def main():
                 "nodes_per_ray": round(cnt["nodes_visited"] / max(rays_cnt, 1), 2),
                 "tris_per_ray": round(cnt["tris_tested"] / max(rays_cnt, 1), 2)}
 
+    # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
+    # when they were taken on this exact workload and kernel variant
+    tp = ROOT / "profiles" / "pmc_traffic.json"
+    workload = workload_name(cfg, n_tris, W, H, sr, args.linear)
+    if tp.exists() and kernel == pt.RayTracer.KERNEL_TRIS and not args.linear and n_ranks == 1:
+        t = json.loads(tp.read_text())
+        if t.get("workload") == workload:
+            roofline["traffic"] = t["hbm_bytes_per_launch"]
+            roofline["traffic_unit"] = "bytes/launch (2*FETCH_SIZE + WRITE_SIZE)"
+            roofline["traffic_source"] = t["source"]
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds0, Wp, Hp, kernel, args.cpu_seconds,
@@ -198,10 +215,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": f"raytrace_tris {cfg}-class synthetic mesh {n_tris} tris, {W}x{H}, "
-                               f"sampleRate {sr} ({sr * sr} spp, one launch), maxDepth 6, "
-                               f"{'linear' if args.linear else 'BVH'} traversal" if n_tris else
-                               f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}",
+        "config": {"workload": workload,
                    "W": W, "H": H, "spp": sr * sr, "n_tris": n_tris,
                    "parallelism": f"row-stripes({args.stripe})x{world}" + (" + rccl gather" if world > 1 else ""),
                    "rays_per_frame": int(rays / steps), "mesh": mesh_info},
@@ -211,6 +225,13 @@ def main():
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def workload_name(cfg, n_tris, W, H, sr, linear):
+    if n_tris:
+        return (f"raytrace_tris {cfg}-class synthetic mesh {n_tris} tris, {W}x{H}, sampleRate {sr} "
+                f"({sr * sr} spp, one launch), maxDepth 6, {'linear' if linear else 'BVH'} traversal")
+    return f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}"
 
 
 def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, verts, idx):
@@ -226,13 +247,25 @@ def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, vert
     out = np.zeros(W * H * 4, np.float32)
     sd = seeds.copy()
     if kernel == 2:
+        # batches of `threads` whole pixels (all sr*sr samples each), strided over the frame with a
+        # different phase per batch, until the sample has taken target_s seconds (bounded)
+        closest = shadow = 0
+        dt = 0.0
+        batches = 0
         n_px = threads
-        pix = (np.arange(n_px, dtype=np.uint64) * (W * H // n_px) + (W * H // (2 * n_px))).astype(np.uint32)
-        t0 = time.perf_counter()
-        closest, shadow = orc.render_tris(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix,
-                                          nthreads=threads)
-        dt = time.perf_counter() - t0
-        sample = f"{n_px} pixels x {sr * sr} samples (strided over the frame), linear traversal (reference algorithm)"
+        stride = W * H // n_px
+        while dt < target_s and batches < 64:
+            phase = (batches * 7919 + stride // 2) % stride
+            pix = (np.arange(n_px, dtype=np.uint64) * stride + phase).astype(np.uint32)
+            t0 = time.perf_counter()
+            c, s = orc.render_tris(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix,
+                                   nthreads=threads)
+            dt += time.perf_counter() - t0
+            closest += c
+            shadow += s
+            batches += 1
+        sample = (f"{batches * n_px} whole pixels x {sr * sr} samples ({batches} strided batches over the frame), "
+                  "linear traversal (the reference algorithm)")
     else:
         t0 = time.perf_counter()
         closest, shadow = orc.render_spheres(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, nthreads=threads)

@@ -60,6 +60,8 @@ def gather_frame(local, height: int, width: int, stripe: int, group=None, root: 
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":  # CPU rehearsal of the RCCL path
+        local = local.cpu()
     rows_max = max_tile_rows(height, stripe, world)
     local = local.reshape(-1)[: rows_max * width * 4]
     if local.numel() != rows_max * width * 4:

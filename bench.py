@@ -217,7 +217,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": workload,
                    "W": W, "H": H, "spp": sr * sr, "n_tris": n_tris,
-                   "parallelism": f"row-stripes({args.stripe})x{world}" + (" + rccl gather" if world > 1 else ""),
+                   "parallelism": f"row-stripes({args.stripe})x{world}" + ((" + rccl gather" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl" else " + gloo gather") if world > 1 else ""),
                    "rays_per_frame": int(rays / steps), "mesh": mesh_info},
         "roofline": roofline,
         "cpu_baseline": cpu,

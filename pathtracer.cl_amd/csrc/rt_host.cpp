@@ -707,11 +707,14 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
     if (e == hipSuccess) e = hipMalloc(&d_idx, n * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&d_t, n * sizeof(float));
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, n * sizeof(rt_ray), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
     if (e == hipSuccess) {
         const int le = rt_launch_trace_rays(c->d_nodes, c->d_tris, c->n_tris, d_rays, n, any_hit,
                                             c->traversal == RT_TRAVERSAL_LINEAR, d_idx, d_t, c->stream);
         e = (hipError_t)le;
     }
+    if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);
+    if (e == hipSuccess) c->have_timing = true;
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out_idx, d_idx, n * sizeof(int32_t), hipMemcpyDeviceToHost);
     if (e == hipSuccess && out_t) e = hipMemcpy(out_t, d_t, n * sizeof(float), hipMemcpyDeviceToHost);

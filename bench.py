@@ -32,7 +32,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-NODE_BYTES = 64  # one BVH node (both child boxes + links), csrc/rt_internal.h
+NODE_BYTES = {"bvh": 112, "bvh2": 64, "linear": 0}  # bytes read per node visit, csrc/rt_internal.h
 TRI_BYTES = 48   # one triangle record (v0+orig, e1, e2 as float4), csrc/rt_internal.h
 PIXEL_BYTES = 16 + 8 + 8  # RGBA32F store + seed read + seed write per pixel
 
@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--sample-rate", type=int, default=None)
     ap.add_argument("--stripe", type=int, default=8)
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
+    ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh2", "linear"],
+                    help="bvh: 4-wide BVH (default); bvh2: binary BVH; linear: the reference loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
@@ -102,7 +104,10 @@ def main():
     rt.setFoVAngle(sc.DEFAULT_FOV)
     rt.setSampleRate(sr)
     rt.setMaxPathDepth(6)
-    rt.setTraversal(args.linear)
+    if args.linear:
+        args.traversal = "linear"
+    args.linear = args.traversal == "linear"
+    rt.setTraversal(args.traversal)
     mesh_info = {}
     if n_tris:
         t0 = time.time()
@@ -174,13 +179,13 @@ def main():
     rays_cnt = cnt["rays_closest"] + cnt["rays_shadow"]
     pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0)) if n_ranks > 1 else H)
     if kernel == pt.RayTracer.KERNEL_TRIS:
-        alg_bytes = cnt["nodes_visited"] * NODE_BYTES + cnt["tris_tested"] * TRI_BYTES + pix * PIXEL_BYTES
+        alg_bytes = cnt["nodes_visited"] * NODE_BYTES[args.traversal] + cnt["tris_tested"] * TRI_BYTES + pix * PIXEL_BYTES
     else:
         alg_bytes = pix * PIXEL_BYTES
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_tris<BVH>" if kernel == 2 and not args.linear else ("k_tris<LINEAR>" if kernel == 2 else "k_spheres"),
+                "kernel": f"k_tris<{args.traversal.upper()}>" if kernel == 2 else "k_spheres",
                 "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
                 "nodes_per_ray": round(cnt["nodes_visited"] / max(rays_cnt, 1), 2),
                 "tris_per_ray": round(cnt["tris_tested"] / max(rays_cnt, 1), 2)}
@@ -188,7 +193,7 @@ def main():
     # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
     # when they were taken on this exact workload and kernel variant
     tp = ROOT / "profiles" / "pmc_traffic.json"
-    workload = workload_name(cfg, n_tris, W, H, sr, args.linear)
+    workload = workload_name(cfg, n_tris, W, H, sr, args.traversal)
     if tp.exists() and kernel == pt.RayTracer.KERNEL_TRIS and not args.linear and n_ranks == 1:
         t = json.loads(tp.read_text())
         if t.get("workload") == workload:
@@ -227,10 +232,13 @@ def main():
         dist.destroy_process_group()
 
 
-def workload_name(cfg, n_tris, W, H, sr, linear):
+TRAVERSAL_NAMES = {"bvh": "4-wide BVH", "bvh2": "binary BVH", "linear": "linear (reference)"}
+
+
+def workload_name(cfg, n_tris, W, H, sr, traversal):
     if n_tris:
         return (f"raytrace_tris {cfg}-class synthetic mesh {n_tris} tris, {W}x{H}, sampleRate {sr} "
-                f"({sr * sr} spp, one launch), maxDepth 6, {'linear' if linear else 'BVH'} traversal")
+                f"({sr * sr} spp, one launch), maxDepth 6, {TRAVERSAL_NAMES[traversal]} traversal")
     return f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}"
 
 

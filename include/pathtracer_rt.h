@@ -44,9 +44,11 @@ enum {
     RT_KERNEL_TRIS = 2        /* raytrace_tris raytracer.cl:184-243 (mesh lit by the emissive spheres) */
 };
 
-/* Triangle traversal: the reference's linear loop (rtcommon.h:39-68) or the BVH
-   (identical results: closest hit = minimum t, ties to the highest index). */
-enum { RT_TRAVERSAL_BVH = 0, RT_TRAVERSAL_LINEAR = 1 };
+/* Triangle traversal: the reference's linear loop (rtcommon.h:39-68) or a BVH
+   (identical results: closest hit = minimum t, ties to the highest index).
+   RT_TRAVERSAL_BVH is the 4-wide tree; RT_TRAVERSAL_BVH2 the binary tree it is
+   collapsed from (kept for A/B measurement). */
+enum { RT_TRAVERSAL_BVH = 0, RT_TRAVERSAL_LINEAR = 1, RT_TRAVERSAL_BVH2 = 2 };
 
 /* rt_render flags */
 enum {
@@ -84,8 +86,15 @@ int rt_set_spheres(rt_ctx *ctx, const rt_sphere *spheres, uint32_t n);
 /* ---- mesh: the tri_verts / tri_vert_idx / n_tris kernel arguments of
    raytrace_tris (raytracer.cl:184-188); the context builds the BVH. ---- */
 int rt_set_mesh(rt_ctx *ctx, const float *verts_xyz, uint32_t n_verts, const int32_t *idx, uint32_t n_tris);
-/* BVH statistics of the current mesh: nodes, leaves, depth, build seconds. */
-int rt_mesh_info(const rt_ctx *ctx, uint32_t *n_nodes, uint32_t *depth, double *build_seconds);
+/* BVH statistics of the current mesh. */
+typedef struct rt_mesh_stats {
+    uint32_t n_tris;
+    uint32_t n_nodes2, depth2; /* binary tree */
+    uint32_t n_nodes4, depth4; /* 4-wide tree */
+    uint32_t stack4;           /* worst-case traversal stack of the 4-wide tree */
+    double build_seconds;
+} rt_mesh_stats;
+int rt_mesh_info(const rt_ctx *ctx, rt_mesh_stats *out);
 
 /* ---- camera: RayTracer::setCameraMatrix / setCameraSpherical / setFoVAngle
    (RayTracer.h:56-60, RayTracer.cpp:24-47); the Camera struct is derived per

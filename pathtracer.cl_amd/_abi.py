@@ -35,6 +35,7 @@ RT_KERNEL_TRIS = 2
 
 RT_TRAVERSAL_BVH = 0
 RT_TRAVERSAL_LINEAR = 1
+RT_TRAVERSAL_BVH2 = 2
 
 RT_OUT_DEVICE = 1
 
@@ -79,6 +80,12 @@ class RtTile(ctypes.Structure):
     _fields_ = [("stripe_rows", ctypes.c_uint32), ("n_ranks", ctypes.c_uint32), ("rank", ctypes.c_uint32)]
 
 
+class RtMeshStats(ctypes.Structure):
+    _fields_ = [("n_tris", ctypes.c_uint32), ("n_nodes2", ctypes.c_uint32), ("depth2", ctypes.c_uint32),
+                ("n_nodes4", ctypes.c_uint32), ("depth4", ctypes.c_uint32), ("stack4", ctypes.c_uint32),
+                ("build_seconds", ctypes.c_double)]
+
+
 class RtCounters(ctypes.Structure):
     _fields_ = [
         ("rays_closest", ctypes.c_uint64),
@@ -97,7 +104,7 @@ SIGNATURES = {
     "rt_status_string": (ctypes.c_char_p, [_i32]),
     "rt_set_spheres": (_i32, [_vp, _vp, _u32]),
     "rt_set_mesh": (_i32, [_vp, _vp, _u32, _vp, _u32]),
-    "rt_mesh_info": (_i32, [_vp, ctypes.POINTER(_u32), ctypes.POINTER(_u32), ctypes.POINTER(ctypes.c_double)]),
+    "rt_mesh_info": (_i32, [_vp, ctypes.POINTER(RtMeshStats)]),
     "rt_set_view_matrix": (_i32, [_vp, _vp]),
     "rt_set_camera_spherical": (_i32, [_vp, _f32, _f32, _f32, _f32, _f32, _f32]),
     "rt_set_fov": (_i32, [_vp, _f32]),

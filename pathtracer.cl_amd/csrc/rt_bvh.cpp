@@ -328,6 +328,98 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
     }
     out.n_leaves = n_leaves;
 
+    /* 4-wide tree: collapse the binary tree, expanding the largest-area inner
+       child first until a node has 4 children (or only leaves remain). */
+    {
+        std::vector<int> n4_src;      /* TmpNode behind each 4-wide node */
+        std::vector<int> kids_of;     /* 4 TmpNode children per 4-wide node (-1 = empty) */
+        auto gather = [&](int id, int *kids) {
+            int k[4] = {-1, -1, -1, -1};
+            int n = 0;
+            if (b.nodes[id].left < 0) { /* a leaf root */
+                k[n++] = id;
+            } else {
+                k[n++] = b.nodes[id].left;
+                k[n++] = b.nodes[id].right;
+                while (n < 4) {
+                    int best = -1;
+                    float best_a = -1.0f;
+                    for (int i = 0; i < n; ++i) {
+                        const TmpNode &c = b.nodes[k[i]];
+                        if (c.left >= 0 && c.box.area() > best_a) {
+                            best_a = c.box.area();
+                            best = i;
+                        }
+                    }
+                    if (best < 0) break;
+                    const int e = k[best];
+                    k[best] = b.nodes[e].left;
+                    k[n++] = b.nodes[e].right;
+                }
+            }
+            for (int i = 0; i < 4; ++i) kids[i] = k[i];
+        };
+        /* BFS-free DFS preorder numbering */
+        std::vector<int> st{root};
+        while (!st.empty()) {
+            const int id = st.back();
+            st.pop_back();
+            const int me = (int)n4_src.size();
+            n4_src.push_back(id);
+            kids_of.resize(4 * n4_src.size());
+            gather(id, &kids_of[4 * me]);
+            for (int i = 3; i >= 0; --i) {
+                const int c = kids_of[4 * me + i];
+                if (c >= 0 && b.nodes[c].left >= 0) st.push_back(c);
+            }
+        }
+        std::vector<int> idx4(b.nodes.size(), -1);
+        for (size_t i = 0; i < n4_src.size(); ++i) idx4[n4_src[i]] = (int)i;
+        out.n_nodes4 = (uint32_t)n4_src.size();
+        out.nodes4.assign(32ull * out.n_nodes4, 0.0f);
+        for (uint32_t i = 0; i < out.n_nodes4; ++i) {
+            float *n = out.nodes4.data() + 32ull * i;
+            for (int k = 0; k < 4; ++k) {
+                const int c = kids_of[4 * i + k];
+                int32_t code = RT_EMPTY_CHILD;
+                if (c >= 0) {
+                    const TmpNode &cn = b.nodes[c];
+                    n[0 + k] = cn.box.lo[0];
+                    n[4 + k] = cn.box.hi[0];
+                    n[8 + k] = cn.box.lo[1];
+                    n[12 + k] = cn.box.hi[1];
+                    n[16 + k] = cn.box.lo[2];
+                    n[20 + k] = cn.box.hi[2];
+                    code = (cn.left >= 0) ? idx4[c] : leaf_code(cn.first, cn.count);
+                } else { /* unused slot: a zero box that is never entered (masked by the code) */
+                    n[0 + k] = n[4 + k] = n[8 + k] = n[12 + k] = n[16 + k] = n[20 + k] = 0.0f;
+                }
+                std::memcpy(&n[24 + k], &code, 4);
+            }
+        }
+        /* depth and worst-case stack: at a node the nearest hit child is taken
+           next and up to (children - 1) are pushed; entries of all ancestors can
+           be live at once. */
+        out.depth4 = 0;
+        out.stack4 = 0;
+        std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> s4; /* node, depth, stack */
+        s4.push_back({0u, {1u, 0u}});
+        while (!s4.empty()) {
+            auto [ni, dd] = s4.back();
+            s4.pop_back();
+            const uint32_t d = dd.first;
+            uint32_t nk = 0;
+            for (int k = 0; k < 4; ++k) nk += kids_of[4 * ni + k] >= 0;
+            const uint32_t stk = dd.second + (nk > 0 ? nk - 1 : 0);
+            out.depth4 = std::max(out.depth4, d);
+            out.stack4 = std::max(out.stack4, stk);
+            for (int k = 0; k < 4; ++k) {
+                const int c = kids_of[4 * ni + k];
+                if (c >= 0 && b.nodes[c].left >= 0) s4.push_back({(uint32_t)idx4[c], {d + 1, stk}});
+            }
+        }
+    }
+
     /* Triangles in leaf order: (v0, orig), (e1 = v1 - v0), (e2 = v2 - v0). */
     out.tris.assign(12ull * n_tris, 0.0f);
     for (uint32_t s = 0; s < n_tris; ++s) {

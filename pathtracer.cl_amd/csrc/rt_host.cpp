@@ -78,9 +78,12 @@ struct rt_ctx {
 
     /* mesh */
     RtBvh bvh;
-    float *d_nodes = nullptr;
+    float *d_nodes = nullptr;  /* binary tree */
+    float *d_nodes4 = nullptr; /* 4-wide tree */
     float *d_tris = nullptr;
     uint32_t n_tris = 0;
+    int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
+    size_t spill_entries = 0;
 
     /* camera state (RayTracer.h:21-29) */
     float view[4][4]; /* viewMatrix, row-major; identity by default (gmtl) */
@@ -110,7 +113,7 @@ struct rt_ctx {
     size_t stage_bytes = 0;
     rt_counters last = {0, 0, 0, 0};
     bool have_timing = false;
-    int grid_cache[4] = {0, 0, 0, 0};
+    int grid_cache[6] = {0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -255,12 +258,37 @@ int ensure_seeds(rt_ctx *c, uint32_t wpad, uint32_t hpad, const uint32_t *src)
     return RT_OK;
 }
 
-int grid_blocks(rt_ctx *c, bool linear, bool count, int *out)
+int trav_kind(const rt_ctx *c)
 {
-    const int key = (linear ? 2 : 0) + (count ? 1 : 0);
+    if (c->traversal == RT_TRAVERSAL_LINEAR) return RT_TRAV_LINEAR;
+    if (c->traversal == RT_TRAVERSAL_BVH2) return RT_TRAV_BVH2;
+    return RT_TRAV_BVH4;
+}
+
+uint32_t spill_cap(const rt_ctx *c)
+{
+    return trav_kind(c) == RT_TRAV_BVH4 && c->bvh.stack4 > RT_STACK_DEPTH ? c->bvh.stack4 - RT_STACK_DEPTH : 0;
+}
+
+const float *trav_nodes(const rt_ctx *c) { return trav_kind(c) == RT_TRAV_BVH4 ? c->d_nodes4 : c->d_nodes; }
+
+int ensure_spill(rt_ctx *c, size_t entries)
+{
+    if (entries <= c->spill_entries) return RT_OK;
+    free_dev(c->d_spill);
+    c->d_spill = nullptr;
+    c->spill_entries = 0;
+    HIPCHK(c, hipMalloc(&c->d_spill, entries * sizeof(int32_t)));
+    c->spill_entries = entries;
+    return RT_OK;
+}
+
+int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
+{
+    const int key = trav * 2 + (count ? 1 : 0);
     if (!c->grid_cache[key]) {
         int b = 0;
-        const int e = rt_tris_grid_blocks(c->device, linear, count, &b);
+        const int e = rt_tris_grid_blocks(c->device, trav, count, &b);
         if (e) return hip_fail(c, (hipError_t)e, "occupancy query");
         c->grid_cache[key] = b;
     }
@@ -319,6 +347,8 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_spheres);
     free_dev(c->d_lights);
     free_dev(c->d_nodes);
+    free_dev(c->d_nodes4);
+    free_dev(c->d_spill);
     free_dev(c->d_tris);
     free_dev(c->d_seeds);
     free_dev(c->d_work);
@@ -365,28 +395,38 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
     free_dev(c->d_nodes);
+    free_dev(c->d_nodes4);
     free_dev(c->d_tris);
-    c->d_nodes = c->d_tris = nullptr;
+    c->d_nodes = c->d_nodes4 = c->d_tris = nullptr;
     c->n_tris = 0;
     HIPCHK(c, hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->d_nodes4, b.nodes4.size() * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
     HIPCHK(c, hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_tris, b.tris.data(), b.tris.size() * sizeof(float), hipMemcpyHostToDevice));
     c->n_tris = n_tris;
     c->bvh.n_nodes = b.n_nodes;
     c->bvh.n_leaves = b.n_leaves;
     c->bvh.depth = b.depth;
+    c->bvh.n_nodes4 = b.n_nodes4;
+    c->bvh.depth4 = b.depth4;
+    c->bvh.stack4 = b.stack4;
     c->bvh.build_seconds = b.build_seconds;
     return RT_OK;
 }
 
-int rt_mesh_info(const rt_ctx *c, uint32_t *n_nodes, uint32_t *depth, double *build_seconds)
+int rt_mesh_info(const rt_ctx *c, rt_mesh_stats *out)
 {
-    if (!c) return RT_ERR_ARG;
+    if (!c || !out) return RT_ERR_ARG;
     if (!c->n_tris) return RT_ERR_NO_MESH;
-    if (n_nodes) *n_nodes = c->bvh.n_nodes;
-    if (depth) *depth = c->bvh.depth;
-    if (build_seconds) *build_seconds = c->bvh.build_seconds;
+    out->n_tris = c->n_tris;
+    out->n_nodes2 = c->bvh.n_nodes;
+    out->depth2 = c->bvh.depth;
+    out->n_nodes4 = c->bvh.n_nodes4;
+    out->depth4 = c->bvh.depth4;
+    out->stack4 = c->bvh.stack4;
+    out->build_seconds = c->bvh.build_seconds;
     return RT_OK;
 }
 
@@ -448,7 +488,7 @@ int rt_set_params(rt_ctx *c, uint32_t sample_rate, uint32_t max_depth)
 
 int rt_set_traversal(rt_ctx *c, int t)
 {
-    if (!c || (t != RT_TRAVERSAL_BVH && t != RT_TRAVERSAL_LINEAR)) return RT_ERR_ARG;
+    if (!c || (t != RT_TRAVERSAL_BVH && t != RT_TRAVERSAL_LINEAR && t != RT_TRAVERSAL_BVH2)) return RT_ERR_ARG;
     c->traversal = t;
     return RT_OK;
 }
@@ -535,7 +575,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                     "the full frame on one device");
     if (kernel == RT_KERNEL_TRIS && c->n_tris == 0) return fail(c, RT_ERR_NO_MESH, "no mesh set");
     if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
-    if (kernel == RT_KERNEL_TRIS && c->bvh.depth > RT_STACK_DEPTH) return fail(c, RT_ERR_LIMIT, "BVH too deep");
+    if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && c->bvh.depth > RT_STACK_DEPTH)
+        return fail(c, RT_ERR_LIMIT, "binary BVH deeper than the traversal stack");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
 
@@ -585,7 +626,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         RtTriLaunch a;
         a.out = dout;
         a.seeds = c->d_seeds;
-        a.nodes = c->d_nodes;
+        a.nodes = trav_nodes(c);
         a.tris = c->d_tris;
         a.n_tris = c->n_tris;
         a.lights = c->d_lights;
@@ -605,16 +646,22 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.rank = rk;
         a.work_counter = c->d_work;
         a.counters = c->d_counters;
-        const bool linear = c->traversal == RT_TRAVERSAL_LINEAR;
+        const int trav = trav_kind(c);
         int blocks = 0;
-        const int r = grid_blocks(c, linear, c->counting, &blocks);
+        const int r = grid_blocks(c, trav, c->counting, &blocks);
         if (r != RT_OK) return r;
         const uint64_t items = (uint64_t)((W + 7) / 8) * ((hl + 7) / 8) * 64;
         blocks = (int)std::min<uint64_t>((uint64_t)blocks, (items + RT_BLOCK - 1) / RT_BLOCK);
         if (blocks < 1) blocks = 1;
+        a.spill_cap = spill_cap(c);
+        if (a.spill_cap) {
+            const int rs = ensure_spill(c, (size_t)blocks * RT_BLOCK * a.spill_cap);
+            if (rs != RT_OK) return rs;
+        }
+        a.spill = c->d_spill;
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         HIPCHK(c, hipEventRecord(c->ev0, st));
-        e = rt_launch_tris(a, linear, c->counting, blocks, st);
+        e = rt_launch_tris(a, trav, c->counting, blocks, st);
         HIPCHK(c, hipEventRecord(c->ev1, st));
     } else {
         RtSphLaunch a;
@@ -707,10 +754,18 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
     if (e == hipSuccess) e = hipMalloc(&d_idx, n * sizeof(int32_t));
     if (e == hipSuccess) e = hipMalloc(&d_t, n * sizeof(float));
     if (e == hipSuccess) e = hipMemcpy(d_rays, rays, n * sizeof(rt_ray), hipMemcpyHostToDevice);
+    const uint32_t cap = spill_cap(c);
+    if (e == hipSuccess && cap) {
+        const int rs = ensure_spill(c, (size_t)n * cap);
+        if (rs != RT_OK) {
+            cleanup();
+            return rs;
+        }
+    }
     if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
     if (e == hipSuccess) {
-        const int le = rt_launch_trace_rays(c->d_nodes, c->d_tris, c->n_tris, d_rays, n, any_hit,
-                                            c->traversal == RT_TRAVERSAL_LINEAR, d_idx, d_t, c->stream);
+        const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, trav_kind(c),
+                                            c->d_spill, cap, d_idx, d_t, c->stream);
         e = (hipError_t)le;
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);

@@ -30,12 +30,24 @@
      t0 = (v0.xyz, original index as int bits), t1 = (e1.xyz, 0), t2 = (e2.xyz, 0)
    with e1 = v1 - v0, e2 = v2 - v0 computed exactly as get_triangle()
    (rtcommon.h:20-37), so the intersection arithmetic is unchanged. */
+/* 4-wide node = 8 x float4 = 128 B (one cache line), children in SoA:
+     f[0] = lo.x[0..3], f[1] = hi.x[0..3], f[2] = lo.y[0..3], f[3] = hi.y[0..3],
+     f[4] = lo.z[0..3], f[5] = hi.z[0..3], f[6] = child[0..3] (int bits), f[7] = 0
+   child >= 0: 4-wide node index; child < 0: leaf ~((first << 3) | (count - 1));
+   RT_EMPTY_CHILD marks an unused slot.  Collapsed from the binary SAH tree
+   (largest-area child expanded first). */
+#define RT_EMPTY_CHILD 0x7fffffff
+
 struct RtBvh {
-    std::vector<float> nodes; /* 16 floats per node */
+    std::vector<float> nodes; /* binary: 16 floats per node */
     std::vector<float> tris;  /* 12 floats per triangle */
     uint32_t n_nodes = 0;
     uint32_t n_leaves = 0;
     uint32_t depth = 0;
+    std::vector<float> nodes4; /* 4-wide: 32 floats per node */
+    uint32_t n_nodes4 = 0;
+    uint32_t depth4 = 0;
+    uint32_t stack4 = 0; /* worst-case traversal stack entries of the 4-wide tree */
     double build_seconds = 0.0;
 };
 
@@ -59,6 +71,8 @@ struct RtTriLaunch {
     uint32_t stripe, n_ranks, rank;
     uint32_t *work_counter;
     unsigned long long *counters; /* [4] */
+    int32_t *spill;      /* per-lane stack overflow (4-wide traversal), spill_cap entries per lane */
+    uint32_t spill_cap;
 };
 
 struct RtSphLaunch {
@@ -74,11 +88,15 @@ struct RtSphLaunch {
 };
 
 /* All return a hipError_t as int (0 = success). */
-int rt_launch_tris(const RtTriLaunch &a, bool linear, bool count, int grid_blocks, void *stream);
+/* traversal kinds (kernel template parameter) */
+enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH2 = 1, RT_TRAV_BVH4 = 2 };
+
+int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream);
 int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
-                         int any_hit, bool linear, int32_t *out_idx, float *out_t, void *stream);
+                         int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
+                         void *stream);
 /* Persistent-grid size for the triangle kernel on this device. */
-int rt_tris_grid_blocks(int device, bool linear, bool count, int *blocks);
+int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks);
 
 #endif /* RT_INTERNAL_H */

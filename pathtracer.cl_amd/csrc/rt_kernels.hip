@@ -82,20 +82,81 @@ struct TravCounts {
     uint32_t tests;
 };
 
+/* Leaf: the reference's triangle tests on slots [first, first+count). */
+template <bool COUNT>
+__device__ __forceinline__ bool leaf_tests(const float4 *__restrict__ tris, int first, int count, V3 o, V3 d,
+                                           float tmin, float tmax, bool any_hit, int &best, int &best_orig,
+                                           float &best_t, TravCounts &cnt)
+{
+    for (int k = 0; k < count; ++k) {
+        const int s = first + k;
+        const float4 a = tris[3 * s], b = tris[3 * s + 1], c = tris[3 * s + 2];
+        float t;
+        if (COUNT) cnt.tests++;
+        if (mt_test(o, d, a, b, c, t)) {
+            if (any_hit) {
+                if (t < tmax && t > tmin) {
+                    best = s;
+                    return true;
+                }
+            } else {
+                const int orig = __float_as_int(a.w);
+                if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
+                    best = s;
+                    best_orig = orig;
+                    best_t = t;
+                }
+            }
+        }
+    }
+    return false;
+}
+
+/* Per-lane traversal stack: [depth][lane] in LDS (stride RT_BLOCK dwords, bank
+   conflict free) with an overflow tail in global memory for the rare rays of a
+   4-wide tree whose worst-case stack exceeds RT_STACK_DEPTH. */
+struct Stack {
+    int *lds;
+    int32_t *spill;
+    int sp;
+    __device__ __forceinline__ void push(int v)
+    {
+        if (sp < RT_STACK_DEPTH) lds[sp * RT_BLOCK] = v;
+        else spill[sp - RT_STACK_DEPTH] = v;
+        ++sp;
+    }
+    __device__ __forceinline__ int pop()
+    {
+        --sp;
+        return (sp < RT_STACK_DEPTH) ? lds[sp * RT_BLOCK] : spill[sp - RT_STACK_DEPTH];
+    }
+};
+
+__device__ __forceinline__ void cas(float &ta, int &ca, float &tb, int &cb)
+{
+    const bool sw = tb < ta;
+    const float t = sw ? tb : ta;
+    const int c = sw ? cb : ca;
+    tb = sw ? ta : tb;
+    cb = sw ? ca : cb;
+    ta = t;
+    ca = c;
+}
+
 /* One ray query.  Closest hit (any_hit = false): returns the leaf-order slot of
    the hit (or -1) with t in tmax; the result equals the reference's linear
    loop: minimum t, ties to the highest original index (rtcommon.h:39-52 with
    intersects_triangle's `t > tmax` rejection).  Any hit: returns >= 0 iff some
    triangle has tmin < t < tmax (rtcommon.h:59-68). */
-template <bool LINEAR, bool COUNT>
+template <int TRAV, bool COUNT>
 __device__ __forceinline__ int traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                         uint32_t n_tris, V3 o, V3 d, float tmin, float &tmax, bool any_hit,
-                                        int *stk, TravCounts &cnt)
+                                        Stack &stk, TravCounts &cnt)
 {
     int best = -1;
     int best_orig = -1;
     float best_t = tmax;
-    if (LINEAR) {
+    if (TRAV == RT_TRAV_LINEAR) {
         /* The reference algorithm: every triangle, in a wave-uniform loop (the
            slot index is uniform, so the records come in through scalar loads). */
         bool live = true;
@@ -129,71 +190,105 @@ __device__ __forceinline__ int traverse(const float4 *__restrict__ nodes, const 
     const V3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
     const float tmin_c = -1e-3f;
-    int sp = 0;
+    stk.sp = 0;
     int node = 0;
+    if (TRAV == RT_TRAV_BVH2) {
+        for (;;) {
+            if (node >= 0) {
+                const float4 n0 = nodes[4 * node + 0];
+                const float4 n1 = nodes[4 * node + 1];
+                const float4 n2 = nodes[4 * node + 2];
+                const float4 n3 = nodes[4 * node + 3];
+                if (COUNT) cnt.nodes++;
+                const float tmax_c = t_slack(best_t);
+                bool h0, h1;
+                const float t0 = slab(n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, inv, oi, tmin_c, tmax_c, h0);
+                const float t1 = slab(n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, inv, oi, tmin_c, tmax_c, h1);
+                const int c0 = __float_as_int(n3.x);
+                const int c1 = __float_as_int(n3.y);
+                if (h0 && h1) {
+                    int nearc = c0, farc = c1;
+                    if (t1 < t0) {
+                        nearc = c1;
+                        farc = c0;
+                    }
+                    stk.push(farc);
+                    node = nearc;
+                } else if (h0) {
+                    node = c0;
+                } else if (h1) {
+                    node = c1;
+                } else {
+                    if (stk.sp == 0) break;
+                    node = stk.pop();
+                }
+                continue;
+            }
+            const int enc = ~node;
+            if (leaf_tests<COUNT>(tris, enc >> 3, (enc & 7) + 1, o, d, tmin, tmax, any_hit, best, best_orig, best_t,
+                                  cnt))
+                break;
+            if (stk.sp == 0) break;
+            node = stk.pop();
+        }
+        if (!any_hit) tmax = best_t;
+        return best;
+    }
+
+    /* 4-wide: near/far slab planes picked once per ray by the direction signs, so
+       each child costs 6 FMAs + max3/min3 and no min/max pairs. */
+    const int nxo = inv.x >= 0.0f ? 0 : 1, nyo = inv.y >= 0.0f ? 2 : 3, nzo = inv.z >= 0.0f ? 4 : 5;
+    const int fxo = 1 - nxo, fyo = 5 - nyo, fzo = 9 - nzo;
     for (;;) {
         if (node >= 0) {
-            const float4 n0 = nodes[4 * node + 0];
-            const float4 n1 = nodes[4 * node + 1];
-            const float4 n2 = nodes[4 * node + 2];
-            const float4 n3 = nodes[4 * node + 3];
+            const float4 *nd = nodes + 8 * node;
+            const float4 nx = nd[nxo], fx = nd[fxo], ny = nd[nyo], fy = nd[fyo], nz = nd[nzo], fz = nd[fzo];
+            const float4 cc = nd[6];
             if (COUNT) cnt.nodes++;
             const float tmax_c = t_slack(best_t);
-            bool h0, h1;
-            const float t0 = slab(n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, inv, oi, tmin_c, tmax_c, h0);
-            const float t1 = slab(n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, inv, oi, tmin_c, tmax_c, h1);
-            const int c0 = __float_as_int(n3.x);
-            const int c1 = __float_as_int(n3.y);
-            if (h0 && h1) {
-                int nearc = c0, farc = c1;
-                if (t1 < t0) {
-                    nearc = c1;
-                    farc = c0;
-                }
-                stk[sp * RT_BLOCK] = farc;
-                ++sp;
-                node = nearc;
-            } else if (h0) {
-                node = c0;
-            } else if (h1) {
-                node = c1;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                node = stk[sp * RT_BLOCK];
+            float t[4];
+            int c[4];
+            const float nxs[4] = {nx.x, nx.y, nx.z, nx.w}, fxs[4] = {fx.x, fx.y, fx.z, fx.w};
+            const float nys[4] = {ny.x, ny.y, ny.z, ny.w}, fys[4] = {fy.x, fy.y, fy.z, fy.w};
+            const float nzs[4] = {nz.x, nz.y, nz.z, nz.w}, fzs[4] = {fz.x, fz.y, fz.z, fz.w};
+            const int cs[4] = {__float_as_int(cc.x), __float_as_int(cc.y), __float_as_int(cc.z),
+                               __float_as_int(cc.w)};
+            int nhit = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float tn = __builtin_fmaxf(
+                    __builtin_fmaxf(__builtin_fmaf(nxs[i], inv.x, -oi.x), __builtin_fmaf(nys[i], inv.y, -oi.y)),
+                    __builtin_fmaxf(__builtin_fmaf(nzs[i], inv.z, -oi.z), tmin_c));
+                const float tf = __builtin_fminf(
+                    __builtin_fminf(__builtin_fmaf(fxs[i], inv.x, -oi.x), __builtin_fmaf(fys[i], inv.y, -oi.y)),
+                    __builtin_fminf(__builtin_fmaf(fzs[i], inv.z, -oi.z), tmax_c));
+                const bool h = (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
+                t[i] = h ? tn : kInf;
+                c[i] = cs[i];
+                nhit += h ? 1 : 0;
             }
+            if (nhit == 0) {
+                if (stk.sp == 0) break;
+                node = stk.pop();
+                continue;
+            }
+            /* sort the (entry distance, child) pairs: misses (inf) sink to the end */
+            cas(t[0], c[0], t[1], c[1]);
+            cas(t[2], c[2], t[3], c[3]);
+            cas(t[0], c[0], t[2], c[2]);
+            cas(t[1], c[1], t[3], c[3]);
+            cas(t[1], c[1], t[2], c[2]);
+            if (nhit >= 4) stk.push(c[3]);
+            if (nhit >= 3) stk.push(c[2]);
+            if (nhit >= 2) stk.push(c[1]);
+            node = c[0];
             continue;
         }
-        /* leaf */
         const int enc = ~node;
-        const int first = enc >> 3;
-        const int count = (enc & 7) + 1;
-        bool done = false;
-        for (int k = 0; k < count; ++k) {
-            const int s = first + k;
-            const float4 a = tris[3 * s], b = tris[3 * s + 1], c = tris[3 * s + 2];
-            float t;
-            if (COUNT) cnt.tests++;
-            if (mt_test(o, d, a, b, c, t)) {
-                if (any_hit) {
-                    if (t < tmax && t > tmin) {
-                        best = s;
-                        done = true;
-                        break;
-                    }
-                } else {
-                    const int orig = __float_as_int(a.w);
-                    if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
-                        best = s;
-                        best_orig = orig;
-                        best_t = t;
-                    }
-                }
-            }
-        }
-        if (done || sp == 0) break;
-        --sp;
-        node = stk[sp * RT_BLOCK];
+        if (leaf_tests<COUNT>(tris, enc >> 3, (enc & 7) + 1, o, d, tmin, tmax, any_hit, best, best_orig, best_t, cnt))
+            break;
+        if (stk.sp == 0) break;
+        node = stk.pop();
     }
     if (!any_hit) tmax = best_t;
     return best;
@@ -249,8 +344,8 @@ constexpr int kMaxLights = 16;
 
 enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_PIXDONE = 4, M_DONE = 5 };
 
-template <bool LINEAR, bool COUNT>
-__global__ __launch_bounds__(RT_BLOCK) void k_tris(RtTriLaunch a)
+template <int TRAV, bool COUNT>
+__global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     __shared__ float s_light[kMaxLights * 8];
@@ -271,7 +366,10 @@ __global__ __launch_bounds__(RT_BLOCK) void k_tris(RtTriLaunch a)
     }
     __syncthreads();
 
-    int *stk = s_stack + threadIdx.x;
+    Stack stk;
+    stk.lds = s_stack + threadIdx.x;
+    stk.spill = a.spill + (size_t)(blockIdx.x * RT_BLOCK + threadIdx.x) * a.spill_cap;
+    stk.sp = 0;
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
     float4 *__restrict__ out = reinterpret_cast<float4 *>(a.out);
@@ -354,8 +452,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_tris(RtTriLaunch a)
             /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
                returns true): skip the traversal, same result */
             if (!shadow || qt > RT_SMALL_F)
-                res = traverse<LINEAR, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F,
-                                              qt, shadow, stk, tc);
+                res = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F,
+                                            qt, shadow, stk, tc);
             if (COUNT) {
                 n_nodes += tc.nodes;
                 n_tests += tc.tests;
@@ -645,10 +743,11 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
 
 /* ======================================================================== */
 /* Batch ray queries (hit-index parity).                                     */
-template <bool LINEAR>
+template <int TRAV>
 __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restrict__ nodes,
                                                          const float4 *__restrict__ tris, uint32_t n_tris,
                                                          const rt_ray *__restrict__ rays, uint32_t n, int any_hit,
+                                                         int32_t *spill, uint32_t spill_cap,
                                                          int32_t *__restrict__ out_idx, float *__restrict__ out_t)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
@@ -657,8 +756,11 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     const rt_ray r = rays[i];
     float t = r.tmax;
     TravCounts tc = {0u, 0u};
-    const int s = traverse<LINEAR, false>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0,
-                                          s_stack + threadIdx.x, tc);
+    Stack stk;
+    stk.lds = s_stack + threadIdx.x;
+    stk.spill = spill + (size_t)i * spill_cap;
+    stk.sp = 0;
+    const int s = traverse<TRAV, false>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0, stk, tc);
     if (any_hit) {
         out_idx[i] = (s >= 0) ? 1 : 0;
         if (out_t) out_t[i] = r.tmax;
@@ -673,17 +775,25 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
 /* ======================================================================== */
 /* Launchers                                                                 */
 
-int rt_launch_tris(const RtTriLaunch &a, bool linear, bool count, int grid_blocks, void *stream)
+template <typename K>
+static int occupancy(K kern, int *per_cu)
+{
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, kern, RT_BLOCK, 0);
+}
+
+int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)grid_blocks), block(RT_BLOCK);
-    if (linear) {
-        if (count) hipLaunchKernelGGL((k_tris<true, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((k_tris<true, false>), grid, block, 0, st, a);
-    } else {
-        if (count) hipLaunchKernelGGL((k_tris<false, true>), grid, block, 0, st, a);
-        else hipLaunchKernelGGL((k_tris<false, false>), grid, block, 0, st, a);
-    }
+#define RT_LAUNCH_TRIS(T)                                                                                              \
+    do {                                                                                                               \
+        if (count) hipLaunchKernelGGL((k_tris<T, true>), grid, block, 0, st, a);                                       \
+        else hipLaunchKernelGGL((k_tris<T, false>), grid, block, 0, st, a);                                            \
+    } while (0)
+    if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR);
+    else if (trav == RT_TRAV_BVH2) RT_LAUNCH_TRIS(RT_TRAV_BVH2);
+    else RT_LAUNCH_TRIS(RT_TRAV_BVH4);
+#undef RT_LAUNCH_TRIS
     return (int)hipGetLastError();
 }
 
@@ -697,34 +807,39 @@ int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream)
 }
 
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
-                         int any_hit, bool linear, int32_t *out_idx, float *out_t, void *stream)
+                         int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
+                         void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK), block(RT_BLOCK);
     const float4 *nd = reinterpret_cast<const float4 *>(nodes);
     const float4 *tr = reinterpret_cast<const float4 *>(tris);
-    if (linear)
-        hipLaunchKernelGGL((k_trace_rays<true>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, out_idx, out_t);
+    if (trav == RT_TRAV_LINEAR)
+        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_LINEAR>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
+                           spill_cap, out_idx, out_t);
+    else if (trav == RT_TRAV_BVH2)
+        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH2>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
+                           spill_cap, out_idx, out_t);
     else
-        hipLaunchKernelGGL((k_trace_rays<false>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, out_idx,
-                           out_t);
+        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
+                           spill_cap, out_idx, out_t);
     return (int)hipGetLastError();
 }
 
-int rt_tris_grid_blocks(int device, bool linear, bool count, int *blocks)
+int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
 {
     int per_cu = 0;
-    hipError_t e;
-    if (linear)
-        e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<true, true>, RT_BLOCK, 0)
-                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<true, false>, RT_BLOCK, 0);
+    int e;
+    if (trav == RT_TRAV_LINEAR)
+        e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true>, &per_cu) : occupancy(k_tris<RT_TRAV_LINEAR, false>, &per_cu);
+    else if (trav == RT_TRAV_BVH2)
+        e = count ? occupancy(k_tris<RT_TRAV_BVH2, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH2, false>, &per_cu);
     else
-        e = count ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<false, true>, RT_BLOCK, 0)
-                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tris<false, false>, RT_BLOCK, 0);
-    if (e != hipSuccess) return (int)e;
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4, false>, &per_cu);
+    if (e) return e;
     int n_cu = 0;
-    e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
-    if (e != hipSuccess) return (int)e;
+    const hipError_t he = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
+    if (he != hipSuccess) return (int)he;
     if (per_cu < 1) per_cu = 1;
     *blocks = per_cu * n_cu;
     return 0;

@@ -100,8 +100,10 @@ class RayTracer:
     def getMaxPathDepth(self) -> int:
         return self._max_depth
 
-    def setTraversal(self, linear: bool) -> None:
-        t = _abi.RT_TRAVERSAL_LINEAR if linear else _abi.RT_TRAVERSAL_BVH
+    def setTraversal(self, linear) -> None:
+        """False/"bvh": 4-wide BVH (default); True/"linear": the reference loop; "bvh2": binary BVH."""
+        t = {False: _abi.RT_TRAVERSAL_BVH, True: _abi.RT_TRAVERSAL_LINEAR, "bvh": _abi.RT_TRAVERSAL_BVH,
+             "linear": _abi.RT_TRAVERSAL_LINEAR, "bvh2": _abi.RT_TRAVERSAL_BVH2}[linear]
         self._check(self._lib.rt_set_traversal(self._h, t), "rt_set_traversal")
 
     def setNDRange(self, nd_y: int) -> None:
@@ -140,10 +142,9 @@ class RayTracer:
         self._mesh = (v.shape[0], i.shape[0])
 
     def meshInfo(self) -> dict:
-        nn, dp, bs = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_double()
-        self._check(self._lib.rt_mesh_info(self._h, ctypes.byref(nn), ctypes.byref(dp), ctypes.byref(bs)),
-                    "rt_mesh_info")
-        return {"nodes": nn.value, "depth": dp.value, "build_seconds": bs.value}
+        st = _abi.RtMeshStats()
+        self._check(self._lib.rt_mesh_info(self._h, ctypes.byref(st)), "rt_mesh_info")
+        return {f: getattr(st, f) for f, _ in _abi.RtMeshStats._fields_}
 
     def _sync_scene(self):
         if self._scene_dirty:

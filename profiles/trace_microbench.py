@@ -32,13 +32,17 @@ rr["tmax"] = np.float32(np.inf)
 sh = rr.copy()
 sh["tmax"] = rng.uniform(0, 10, n).astype(np.float32)
 res = {}
-for name, rays, anyhit in [("primary_closest", prim, False), ("random_closest", rr, False), ("random_anyhit", sh, True)]:
-    rt.traceRays(rays[:1024], anyhit)
-    best = None
-    for _ in range(3):
-        hit, _t = rt.traceRays(rays, anyhit)
-        ms = rt.lastKernelMs()
-        best = ms if best is None else min(best, ms)
-    res[name] = {"rays": len(rays), "kernel_ms": round(best, 3), "mrays_per_s": round(len(rays) / best / 1e3, 1),
-                 "hit_frac": round(float((hit > 0).mean() if anyhit else (hit >= 0).mean()), 4)}
+for trav in ("bvh", "bvh2"):
+    rt.setTraversal(trav)
+    for name, rays, anyhit in [("primary_closest", prim, False), ("random_closest", rr, False),
+                               ("random_anyhit", sh, True)]:
+        rt.traceRays(rays[:1024], anyhit)
+        best = None
+        for _ in range(3):
+            hit, _t = rt.traceRays(rays, anyhit)
+            ms = rt.lastKernelMs()
+            best = ms if best is None else min(best, ms)
+        res[f"{trav}/{name}"] = {"rays": len(rays), "kernel_ms": round(best, 3),
+                                 "mrays_per_s": round(len(rays) / best / 1e3, 1),
+                                 "hit_frac": round(float((hit > 0).mean() if anyhit else (hit >= 0).mean()), 4)}
 print(json.dumps({"n_tris": n_tris, "bvh": rt.meshInfo(), "results": res}))

@@ -42,13 +42,16 @@ def test_golden_spheres(name, tracer, pt, golden, golden_meta):
     rt.close()
 
 
-@pytest.mark.parametrize("linear", [False, True])
+TRAVERSALS = ["bvh", "bvh2", "linear"]
+
+
+@pytest.mark.parametrize("trav", TRAVERSALS)
 @pytest.mark.parametrize("name", TRI_CASES)
-def test_golden_tris(name, linear, tracer, pt, golden, golden_meta):
+def test_golden_tris(name, trav, tracer, pt, golden, golden_meta):
     g, m = golden(name), golden_meta["cases"][name]
     rt = pt.RayTracer(0)
     _setup(rt, pt, g, m, kernel_tris=True)
-    rt.setTraversal(linear)
+    rt.setTraversal(trav)
     out = np.zeros(m["W"] * m["H"] * 4, np.float32)
     for p in range(m["frames"]):
         rt.rayTrace(out, m["W"], m["H"], p, kernel=2)
@@ -57,12 +60,12 @@ def test_golden_tris(name, linear, tracer, pt, golden, golden_meta):
     rt.close()
 
 
-@pytest.mark.parametrize("linear", [False, True])
-def test_golden_hit_indices(linear, tracer, pt, golden):
+@pytest.mark.parametrize("trav", TRAVERSALS)
+def test_golden_hit_indices(trav, tracer, pt, golden):
     g = golden("hits_2000")
     R = pt._abi.RAY_DTYPE
     tracer.setMesh(g["verts"], g["idx"])
-    tracer.setTraversal(linear)
+    tracer.setTraversal(trav)
     for key in ("primary", "random"):
         idx, t = tracer.traceRays(g[f"{key}_rays"].view(R))
         np.testing.assert_array_equal(idx, g[f"{key}_hit"])
@@ -146,14 +149,15 @@ def test_bvh_equals_linear_dragon(tracer, pt):
     rt = tracer
     rt.setMesh(verts, idx)
     res = {}
-    for linear in (False, True):
-        rt.setTraversal(linear)
-        res[linear] = (rt.traceRays(rays), rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
-    rt.setTraversal(False)
-    for k in range(3):
-        np.testing.assert_array_equal(res[False][k][0], res[True][k][0])
-        np.testing.assert_array_equal(bits(res[False][k][1]), bits(res[True][k][1]))
-    assert (res[False][0][0] >= 0).mean() > 0.2  # visible
+    for trav in TRAVERSALS:
+        rt.setTraversal(trav)
+        res[trav] = (rt.traceRays(rays), rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
+    rt.setTraversal("bvh")
+    for trav in ("bvh", "bvh2"):
+        for k in range(3):
+            np.testing.assert_array_equal(res[trav][k][0], res["linear"][k][0])
+            np.testing.assert_array_equal(bits(res[trav][k][1]), bits(res["linear"][k][1]))
+    assert (res["bvh"][0][0] >= 0).mean() > 0.2  # visible
 
 
 def test_bvh_equals_linear_fuzz_grazing(tracer, pt):
@@ -177,13 +181,14 @@ def test_bvh_equals_linear_fuzz_grazing(tracer, pt):
     rt = tracer
     rt.setMesh(v, idx)
     out = {}
-    for linear in (False, True):
-        rt.setTraversal(linear)
-        out[linear] = (rt.traceRays(rr), rt.traceRays(rr, any_hit=True))
-    rt.setTraversal(False)
-    np.testing.assert_array_equal(out[False][0][0], out[True][0][0])
-    np.testing.assert_array_equal(bits(out[False][0][1]), bits(out[True][0][1]))
-    np.testing.assert_array_equal(out[False][1][0], out[True][1][0])
+    for trav in TRAVERSALS:
+        rt.setTraversal(trav)
+        out[trav] = (rt.traceRays(rr), rt.traceRays(rr, any_hit=True))
+    rt.setTraversal("bvh")
+    for trav in ("bvh", "bvh2"):
+        np.testing.assert_array_equal(out[trav][0][0], out["linear"][0][0])
+        np.testing.assert_array_equal(bits(out[trav][0][1]), bits(out["linear"][0][1]))
+        np.testing.assert_array_equal(out[trav][1][0], out["linear"][1][0])
 
 
 @pytest.mark.parametrize("kernel,prog", [(2, 0), (2, 3), (0, 0), (1, 2)])

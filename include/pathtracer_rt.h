@@ -46,9 +46,10 @@ enum {
 
 /* Triangle traversal: the reference's linear loop (rtcommon.h:39-68) or a BVH
    (identical results: closest hit = minimum t, ties to the highest index).
-   RT_TRAVERSAL_BVH is the 4-wide tree; RT_TRAVERSAL_BVH2 the binary tree it is
-   collapsed from (kept for A/B measurement). */
-enum { RT_TRAVERSAL_BVH = 0, RT_TRAVERSAL_LINEAR = 1, RT_TRAVERSAL_BVH2 = 2 };
+   RT_TRAVERSAL_BVH is the 4-wide tree traversed per lane; RT_TRAVERSAL_BVH2 the
+   binary tree it is collapsed from; RT_TRAVERSAL_PACKET the 4-wide tree walked
+   wave-coherently (one node sequence per wave, scalar node fetches). */
+enum { RT_TRAVERSAL_BVH = 0, RT_TRAVERSAL_LINEAR = 1, RT_TRAVERSAL_BVH2 = 2, RT_TRAVERSAL_PACKET = 3 };
 
 /* rt_render flags */
 enum {

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -83,6 +84,12 @@ struct rt_ctx {
     float *d_tris = nullptr;
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
+    uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
+    uint8_t *d_flags = nullptr;  /* probe flags */
+    size_t flags_bytes = 0;
+    std::vector<uint32_t> order_key; /* what the cached order was computed for */
+    bool schedule = true;
+    uint64_t mesh_serial = 0;
     size_t spill_entries = 0;
 
     /* camera state (RayTracer.h:21-29) */
@@ -113,7 +120,7 @@ struct rt_ctx {
     size_t stage_bytes = 0;
     rt_counters last = {0, 0, 0, 0};
     bool have_timing = false;
-    int grid_cache[6] = {0, 0, 0, 0, 0, 0};
+    int grid_cache[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -262,6 +269,7 @@ int trav_kind(const rt_ctx *c)
 {
     if (c->traversal == RT_TRAVERSAL_LINEAR) return RT_TRAV_LINEAR;
     if (c->traversal == RT_TRAVERSAL_BVH2) return RT_TRAV_BVH2;
+    if (c->traversal == RT_TRAVERSAL_PACKET) return RT_TRAV_PACKET4;
     return RT_TRAV_BVH4;
 }
 
@@ -270,7 +278,11 @@ uint32_t spill_cap(const rt_ctx *c)
     return trav_kind(c) == RT_TRAV_BVH4 && c->bvh.stack4 > RT_STACK_DEPTH ? c->bvh.stack4 - RT_STACK_DEPTH : 0;
 }
 
-const float *trav_nodes(const rt_ctx *c) { return trav_kind(c) == RT_TRAV_BVH4 ? c->d_nodes4 : c->d_nodes; }
+const float *trav_nodes(const rt_ctx *c)
+{
+    const int k = trav_kind(c);
+    return (k == RT_TRAV_BVH4 || k == RT_TRAV_PACKET4) ? c->d_nodes4 : c->d_nodes;
+}
 
 int ensure_spill(rt_ctx *c, size_t entries)
 {
@@ -293,6 +305,60 @@ int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
         c->grid_cache[key] = b;
     }
     *out = c->grid_cache[key];
+    return RT_OK;
+}
+
+/* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by
+   its paths: a camera ray that hits the mesh ends after one shadow query per
+   light (rtcommon.h:411-421), one that misses bounces off the box up to
+   maxDepth+1 times with shadow queries at each (rtcommon.h:425-461).  A probe
+   of one centre ray per pixel estimates each 8x8 tile's cost, and the queue
+   hands out the most expensive tiles first, so the launch does not end on a
+   tail of long box-pixel paths.  Scheduling only: every pixel's result is
+   independent of when it is rendered.  Cached until camera, mesh, frame, tile
+   or path depth change. */
+int tile_order(rt_ctx *c, uint32_t W, uint32_t H, uint32_t hl, uint32_t stripe, uint32_t nr, uint32_t rk,
+               hipStream_t st)
+{
+    std::vector<uint32_t> key = {W, H, hl, stripe, nr, rk, c->max_depth, (uint32_t)c->lights.size(),
+                                 (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32)};
+    const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
+    key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
+    const uint32_t tx = (W + 7) / 8, ty = (hl + 7) / 8, n_t = tx * ty;
+    if (key == c->order_key) return RT_OK;
+    if (c->bvh.stack4 > 64) { /* the wave-coherent probe needs the per-wave stack: keep row-major order */
+        free_dev(c->d_order);
+        c->d_order = nullptr;
+        c->order_key = key;
+        return RT_OK;
+    }
+    const size_t npx = (size_t)W * hl;
+    if (c->flags_bytes < npx) {
+        free_dev(c->d_flags);
+        c->d_flags = nullptr;
+        c->flags_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_flags, npx));
+        c->flags_bytes = npx;
+    }
+    const int e = rt_launch_probe(c->d_nodes4, c->d_tris, c->cam, W, H, hl, stripe, nr, rk, c->d_flags, st);
+    if (e) return hip_fail(c, (hipError_t)e, "probe launch");
+    std::vector<uint8_t> f(npx);
+    HIPCHK(c, hipMemcpyAsync(f.data(), c->d_flags, npx, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    const uint64_t c_mesh = 1 + c->lights.size();
+    const uint64_t c_box = (1 + c->lights.size()) * (uint64_t)(c->max_depth + 1);
+    std::vector<uint64_t> cost(n_t, 0);
+    for (uint32_t y = 0; y < hl; ++y)
+        for (uint32_t x = 0; x < W; ++x) cost[(y / 8) * tx + x / 8] += f[(size_t)y * W + x] ? c_mesh : c_box;
+    std::vector<uint32_t> o(n_t);
+    for (uint32_t i = 0; i < n_t; ++i) o[i] = i;
+    std::stable_sort(o.begin(), o.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    free_dev(c->d_order);
+    c->d_order = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_order, n_t * sizeof(uint32_t)));
+    HIPCHK(c, hipMemcpyAsync(c->d_order, o.data(), n_t * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->order_key = key;
     return RT_OK;
 }
 
@@ -329,6 +395,7 @@ int rt_create(int device, rt_ctx **out)
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) c->view[i][j] = (i == j) ? 1.0f : 0.0f;
     c->rng.seed(1);
+    if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0"; /* A/B knob */
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess) {
@@ -349,6 +416,8 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_nodes);
     free_dev(c->d_nodes4);
     free_dev(c->d_spill);
+    free_dev(c->d_order);
+    free_dev(c->d_flags);
     free_dev(c->d_tris);
     free_dev(c->d_seeds);
     free_dev(c->d_work);
@@ -406,6 +475,7 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_tris, b.tris.data(), b.tris.size() * sizeof(float), hipMemcpyHostToDevice));
     c->n_tris = n_tris;
+    c->mesh_serial++;
     c->bvh.n_nodes = b.n_nodes;
     c->bvh.n_leaves = b.n_leaves;
     c->bvh.depth = b.depth;
@@ -488,7 +558,7 @@ int rt_set_params(rt_ctx *c, uint32_t sample_rate, uint32_t max_depth)
 
 int rt_set_traversal(rt_ctx *c, int t)
 {
-    if (!c || (t != RT_TRAVERSAL_BVH && t != RT_TRAVERSAL_LINEAR && t != RT_TRAVERSAL_BVH2)) return RT_ERR_ARG;
+    if (!c || t < RT_TRAVERSAL_BVH || t > RT_TRAVERSAL_PACKET) return RT_ERR_ARG;
     c->traversal = t;
     return RT_OK;
 }
@@ -577,6 +647,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
     if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
     if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && c->bvh.depth > RT_STACK_DEPTH)
         return fail(c, RT_ERR_LIMIT, "binary BVH deeper than the traversal stack");
+    if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_PACKET && c->bvh.stack4 > 64)
+        return fail(c, RT_ERR_LIMIT, "4-wide BVH stack exceeds the per-wave stack (64)");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
 
@@ -659,6 +731,12 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
+        a.tile_order = nullptr;
+        if (c->schedule) {
+            const int ro = tile_order(c, W, H, hl, stripe, nr, rk, st);
+            if (ro != RT_OK) return ro;
+            a.tile_order = c->d_order;
+        }
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         HIPCHK(c, hipEventRecord(c->ev0, st));
         e = rt_launch_tris(a, trav, c->counting, blocks, st);

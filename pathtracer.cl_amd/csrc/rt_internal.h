@@ -73,6 +73,7 @@ struct RtTriLaunch {
     unsigned long long *counters; /* [4] */
     int32_t *spill;      /* per-lane stack overflow (4-wide traversal), spill_cap entries per lane */
     uint32_t spill_cap;
+    const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
 };
 
 struct RtSphLaunch {
@@ -89,13 +90,16 @@ struct RtSphLaunch {
 
 /* All return a hipError_t as int (0 = success). */
 /* traversal kinds (kernel template parameter) */
-enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH2 = 1, RT_TRAV_BVH4 = 2 };
+enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH2 = 1, RT_TRAV_BVH4 = 2, RT_TRAV_PACKET4 = 3 };
 
 int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream);
 int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
                          void *stream);
+/* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
+int rt_launch_probe(const float *nodes4, const float *tris, const rt_camera &cam, uint32_t W, uint32_t H, uint32_t Hl,
+                    uint32_t stripe, uint32_t n_ranks, uint32_t rank, uint8_t *flags, void *stream);
 /* Persistent-grid size for the triangle kernel on this device. */
 int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks);
 

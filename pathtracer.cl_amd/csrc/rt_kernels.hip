@@ -294,6 +294,131 @@ __device__ __forceinline__ int traverse(const float4 *__restrict__ nodes, const 
     return best;
 }
 
+/* Wave-coherent (packet) traversal of the 4-wide tree.  All participating
+   lanes of the wave walk ONE node sequence: the node index and the stack are
+   wave-uniform (SGPRs / a per-wave LDS stack), node and triangle records come
+   in through scalar loads (one fetch per wave, operands in SGPRs), and every
+   lane tests the fetched children / triangles against its own ray, culling by
+   its own [tmin, best_t].  A child is entered when any live lane hits it; the
+   order follows the first live lane's entry distances.  Suited to the coherent
+   queries of raytrace_tris (an 8x8 pixel tile's camera rays, and the shadow rays
+   from those surface points to the same light).  The result per lane is the
+   same as the per-lane traversal (same accept rule, conservative culling). */
+constexpr int kWaveStack = 64;
+
+/* Read-only scene records through the constant address space: with a
+   wave-uniform address the loads become s_load (scalar cache, SGPR operands). */
+typedef float v4f __attribute__((ext_vector_type(4)));
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(4))) const v4f cfloat4;
+#else
+typedef const v4f cfloat4;
+#endif
+__device__ __forceinline__ float4 ld4(const cfloat4 *p)
+{
+    const v4f v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ int traverse_packet4(const float4 *__restrict__ nodes_g, const float4 *__restrict__ tris_g,
+                                                V3 o, V3 d, float tmin, float &tmax, bool any_hit, int *wstack,
+                                                TravCounts &cnt)
+{
+    const cfloat4 *nodes = (const cfloat4 *)nodes_g;
+    const cfloat4 *tris = (const cfloat4 *)tris_g;
+    int best = -1;
+    int best_orig = -1;
+    float best_t = tmax;
+    bool live = true;
+    const V3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
+    const float tmin_c = -1e-3f;
+    int sp = 0;
+    int node = 0;
+    const bool rep = COUNT && (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
+                               (uint32_t)__builtin_ctzll(__ballot(1)));
+    for (;;) {
+        if (node >= 0) {
+            const cfloat4 *nd = nodes + 8 * node;
+            const float4 lx = ld4(nd + 0), hx = ld4(nd + 1), ly = ld4(nd + 2), hy = ld4(nd + 3), lz = ld4(nd + 4),
+                         hz = ld4(nd + 5), cc = ld4(nd + 6);
+            if (COUNT && rep) cnt.nodes++; /* one fetch per wave */
+            const float tmax_c = t_slack(any_hit ? tmax : best_t);
+            const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, hxs[4] = {hx.x, hx.y, hx.z, hx.w};
+            const float lys[4] = {ly.x, ly.y, ly.z, ly.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w};
+            const float lzs[4] = {lz.x, lz.y, lz.z, lz.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
+            const int cs[4] = {__float_as_int(cc.x), __float_as_int(cc.y), __float_as_int(cc.z),
+                               __float_as_int(cc.w)};
+            float key[4];
+            int c[4];
+            int nhit = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float x0 = __builtin_fmaf(lxs[i], inv.x, -oi.x), x1 = __builtin_fmaf(hxs[i], inv.x, -oi.x);
+                const float y0 = __builtin_fmaf(lys[i], inv.y, -oi.y), y1 = __builtin_fmaf(hys[i], inv.y, -oi.y);
+                const float z0 = __builtin_fmaf(lzs[i], inv.z, -oi.z), z1 = __builtin_fmaf(hzs[i], inv.z, -oi.z);
+                const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                                 __builtin_fmaxf(__builtin_fminf(z0, z1), tmin_c));
+                const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                                 __builtin_fminf(__builtin_fmaxf(z0, z1), tmax_c));
+                const bool h = live && (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
+                const bool any = __any(h);
+                /* the first participating lane's entry distance orders the children */
+                const float k = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(tn)));
+                key[i] = any ? k : kInf;
+                c[i] = cs[i];
+                nhit += any ? 1 : 0;
+            }
+            if (nhit == 0) {
+                if (sp == 0) break;
+                --sp;
+                node = __builtin_amdgcn_readfirstlane(wstack[sp]);
+                continue;
+            }
+            cas(key[0], c[0], key[1], c[1]);
+            cas(key[2], c[2], key[3], c[3]);
+            cas(key[0], c[0], key[2], c[2]);
+            cas(key[1], c[1], key[3], c[3]);
+            cas(key[1], c[1], key[2], c[2]);
+            if (nhit >= 4) wstack[sp++] = c[3];
+            if (nhit >= 3) wstack[sp++] = c[2];
+            if (nhit >= 2) wstack[sp++] = c[1];
+            node = __builtin_amdgcn_readfirstlane(c[0]);
+            continue;
+        }
+        const int enc = ~node;
+        const int first = enc >> 3, count = (enc & 7) + 1;
+        for (int k = 0; k < count; ++k) {
+            const int s = first + k;
+            const float4 a = ld4(tris + 3 * s), b = ld4(tris + 3 * s + 1), cc = ld4(tris + 3 * s + 2);
+            if (COUNT && rep) cnt.tests++; /* one fetch per wave */
+            float t;
+            if (live && mt_test(o, d, a, b, cc, t)) {
+                if (any_hit) {
+                    if (t < tmax && t > tmin) {
+                        best = s;
+                        live = false;
+                    }
+                } else {
+                    const int orig = __float_as_int(a.w);
+                    if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
+                        best = s;
+                        best_orig = orig;
+                        best_t = t;
+                    }
+                }
+            }
+        }
+        if (any_hit && !__any(live)) break;
+        if (sp == 0) break;
+        --sp;
+        node = __builtin_amdgcn_readfirstlane(wstack[sp]);
+    }
+    if (!any_hit) tmax = best_t;
+    return best;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -347,7 +472,8 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_PIXDONE
 template <int TRAV, bool COUNT>
 __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
 {
-    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
+    constexpr bool PACKET = TRAV == RT_TRAV_PACKET4;
+    __shared__ int s_stack[PACKET ? (RT_BLOCK / 64) * kWaveStack : RT_STACK_DEPTH * RT_BLOCK];
     __shared__ float s_light[kMaxLights * 8];
 
     /* emissive spheres: center.xyz, radius, emission.xyz (materials.h:232, rtcommon.h:97-99) */
@@ -411,7 +537,9 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                     mode = M_DONE;
                 } else {
                     /* 8 x 8 pixel tiles, row-major over the (local) frame */
-                    const uint32_t tile = item >> 6, in = item & 63u;
+                    uint32_t tile = item >> 6;
+                    const uint32_t in = item & 63u;
+                    if (a.tile_order) tile = a.tile_order[tile];
                     x = (tile % tiles_x) * 8u + (in & 7u);
                     yl = (tile / tiles_x) * 8u + (in >> 3);
                     if (x < a.W && yl < a.Hl) {
@@ -442,18 +570,32 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
             mode = M_CLOSEST;
         }
 
-        /* ---- C: this iteration's single ray query ---- */
+        /* ---- C: this iteration's ray query ---- */
         int res = -1;
         float qt = kInf;
-        if (mode == M_CLOSEST || mode == M_SHADOW) {
+        bool go = (mode == M_CLOSEST || mode == M_SHADOW);
+        if (PACKET) {
+            /* one query type per wave and iteration (the majority); the other lanes wait */
+            const int nc = __popcll(__ballot(mode == M_CLOSEST));
+            const int ns = __popcll(__ballot(mode == M_SHADOW));
+            go = (ns > nc) ? (mode == M_SHADOW) : (mode == M_CLOSEST);
+            /* a trivially unoccluded shadow ray never waits */
+            go = go || (mode == M_SHADOW && !(stmax > RT_SMALL_F));
+        }
+        if (go) {
             const bool shadow = (mode == M_SHADOW);
             if (shadow) qt = stmax;
             TravCounts tc = {0u, 0u};
             /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
                returns true): skip the traversal, same result */
-            if (!shadow || qt > RT_SMALL_F)
-                res = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F,
-                                            qt, shadow, stk, tc);
+            if (!shadow || qt > RT_SMALL_F) {
+                if (PACKET)
+                    res = traverse_packet4<COUNT>(nodes, tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F, qt,
+                                                  shadow, s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
+                else
+                    res = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd,
+                                                RT_SMALL_F, qt, shadow, stk, tc);
+            }
             if (COUNT) {
                 n_nodes += tc.nodes;
                 n_tests += tc.tests;
@@ -462,7 +604,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
 
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
         bool want_shadow = false, seg_done = false, sample_done = false;
-        if (mode == M_CLOSEST) {
+        if (mode == M_CLOSEST && go) {
             ++n_closest;
             bool surface = true;
             if (res >= 0) {
@@ -490,7 +632,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                 if (n_lights > 0) want_shadow = true;
                 else seg_done = true;
             }
-        } else if (mode == M_SHADOW) {
+        } else if (mode == M_SHADOW && go) {
             ++n_shadow;
             if (res < 0) { /* unoccluded: rtcommon.h:93-101 */
                 const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
@@ -760,7 +902,12 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     stk.lds = s_stack + threadIdx.x;
     stk.spill = spill + (size_t)i * spill_cap;
     stk.sp = 0;
-    const int s = traverse<TRAV, false>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0, stk, tc);
+    int s;
+    if (TRAV == RT_TRAV_PACKET4)
+        s = traverse_packet4<false>(nodes, tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0,
+                                    s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
+    else
+        s = traverse<TRAV, false>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0, stk, tc);
     if (any_hit) {
         out_idx[i] = (s >= 0) ? 1 : 0;
         if (out_t) out_t[i] = r.tmax;
@@ -768,6 +915,33 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
         out_idx[i] = (s >= 0) ? __float_as_int(tris[3 * s].w) : -1;
         if (out_t) out_t[i] = t;
     }
+}
+
+/* Scheduling probe: one pixel-centre camera ray per pixel (8x8 tiles, a wave per
+   tile: coherent, so the wave-coherent traversal), flag = the primary ray hits
+   the mesh.  Used only to order the pixel queue (expensive tiles first); no
+   result of the render depends on it. */
+__global__ __launch_bounds__(RT_BLOCK) void k_probe(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                                    rt_camera cam, uint32_t W, uint32_t H, uint32_t Hl,
+                                                    uint32_t stripe, uint32_t n_ranks, uint32_t rank,
+                                                    uint8_t *__restrict__ flags)
+{
+    __shared__ int s_wstack[(RT_BLOCK / 64) * kWaveStack];
+    const uint32_t tiles_x = (W + 7u) >> 3;
+    const uint32_t g = blockIdx.x * RT_BLOCK + threadIdx.x;
+    const uint32_t tile = g >> 6, in = g & 63u;
+    const uint32_t x = (tile % tiles_x) * 8u + (in & 7u);
+    const uint32_t yl = (tile / tiles_x) * 8u + (in >> 3);
+    if (tile >= tiles_x * ((Hl + 7u) >> 3)) return; /* whole waves exit together */
+    const bool valid = x < W && yl < Hl;
+    const uint32_t y = global_row(valid ? yl : 0u, stripe, n_ranks, rank);
+    const V3 o = v3(cam.position.x, cam.position.y, cam.position.z);
+    const V3 d = camera_dir(cam, ((float)x + 0.5f) - ((float)W) / 2.0f, ((float)y + 0.5f) - ((float)H) / 2.0f);
+    float t = kInf;
+    TravCounts tc = {0u, 0u};
+    const int hit = traverse_packet4<false>(nodes, tris, o, d, RT_SMALL_F, t, false,
+                                            s_wstack + (threadIdx.x >> 6) * kWaveStack, tc);
+    if (valid) flags[(size_t)yl * W + x] = hit >= 0 ? 1 : 0;
 }
 
 } // namespace
@@ -792,6 +966,7 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
     } while (0)
     if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR);
     else if (trav == RT_TRAV_BVH2) RT_LAUNCH_TRIS(RT_TRAV_BVH2);
+    else if (trav == RT_TRAV_PACKET4) RT_LAUNCH_TRIS(RT_TRAV_PACKET4);
     else RT_LAUNCH_TRIS(RT_TRAV_BVH4);
 #undef RT_LAUNCH_TRIS
     return (int)hipGetLastError();
@@ -820,6 +995,9 @@ int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris,
     else if (trav == RT_TRAV_BVH2)
         hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH2>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
                            spill_cap, out_idx, out_t);
+    else if (trav == RT_TRAV_PACKET4)
+        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_PACKET4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit,
+                           spill, spill_cap, out_idx, out_t);
     else
         hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
                            spill_cap, out_idx, out_t);
@@ -834,6 +1012,9 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
         e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true>, &per_cu) : occupancy(k_tris<RT_TRAV_LINEAR, false>, &per_cu);
     else if (trav == RT_TRAV_BVH2)
         e = count ? occupancy(k_tris<RT_TRAV_BVH2, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH2, false>, &per_cu);
+    else if (trav == RT_TRAV_PACKET4)
+        e = count ? occupancy(k_tris<RT_TRAV_PACKET4, true>, &per_cu)
+                  : occupancy(k_tris<RT_TRAV_PACKET4, false>, &per_cu);
     else
         e = count ? occupancy(k_tris<RT_TRAV_BVH4, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4, false>, &per_cu);
     if (e) return e;
@@ -843,4 +1024,14 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
     if (per_cu < 1) per_cu = 1;
     *blocks = per_cu * n_cu;
     return 0;
+}
+
+int rt_launch_probe(const float *nodes4, const float *tris, const rt_camera &cam, uint32_t W, uint32_t H, uint32_t Hl,
+                    uint32_t stripe, uint32_t n_ranks, uint32_t rank, uint8_t *flags, void *stream)
+{
+    const uint32_t tiles = ((W + 7u) >> 3) * ((Hl + 7u) >> 3);
+    dim3 grid((tiles * 64u + RT_BLOCK - 1) / RT_BLOCK), block(RT_BLOCK);
+    hipLaunchKernelGGL(k_probe, grid, block, 0, (hipStream_t)stream, reinterpret_cast<const float4 *>(nodes4),
+                       reinterpret_cast<const float4 *>(tris), cam, W, H, Hl, stripe, n_ranks, rank, flags);
+    return (int)hipGetLastError();
 }

@@ -103,7 +103,8 @@ class RayTracer:
     def setTraversal(self, linear) -> None:
         """False/"bvh": 4-wide BVH (default); True/"linear": the reference loop; "bvh2": binary BVH."""
         t = {False: _abi.RT_TRAVERSAL_BVH, True: _abi.RT_TRAVERSAL_LINEAR, "bvh": _abi.RT_TRAVERSAL_BVH,
-             "linear": _abi.RT_TRAVERSAL_LINEAR, "bvh2": _abi.RT_TRAVERSAL_BVH2}[linear]
+             "linear": _abi.RT_TRAVERSAL_LINEAR, "bvh2": _abi.RT_TRAVERSAL_BVH2,
+             "packet": _abi.RT_TRAVERSAL_PACKET}[linear]
         self._check(self._lib.rt_set_traversal(self._h, t), "rt_set_traversal")
 
     def setNDRange(self, nd_y: int) -> None:

@@ -32,7 +32,7 @@ rr["tmax"] = np.float32(np.inf)
 sh = rr.copy()
 sh["tmax"] = rng.uniform(0, 10, n).astype(np.float32)
 res = {}
-for trav in ("bvh", "bvh2"):
+for trav in ("bvh", "bvh2", "packet"):
     rt.setTraversal(trav)
     for name, rays, anyhit in [("primary_closest", prim, False), ("random_closest", rr, False),
                                ("random_anyhit", sh, True)]:

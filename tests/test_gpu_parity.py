@@ -42,7 +42,7 @@ def test_golden_spheres(name, tracer, pt, golden, golden_meta):
     rt.close()
 
 
-TRAVERSALS = ["bvh", "bvh2", "linear"]
+TRAVERSALS = ["bvh", "bvh2", "packet", "linear"]
 
 
 @pytest.mark.parametrize("trav", TRAVERSALS)
@@ -153,7 +153,7 @@ def test_bvh_equals_linear_dragon(tracer, pt):
         rt.setTraversal(trav)
         res[trav] = (rt.traceRays(rays), rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
     rt.setTraversal("bvh")
-    for trav in ("bvh", "bvh2"):
+    for trav in ("bvh", "bvh2", "packet"):
         for k in range(3):
             np.testing.assert_array_equal(res[trav][k][0], res["linear"][k][0])
             np.testing.assert_array_equal(bits(res[trav][k][1]), bits(res["linear"][k][1]))
@@ -185,7 +185,7 @@ def test_bvh_equals_linear_fuzz_grazing(tracer, pt):
         rt.setTraversal(trav)
         out[trav] = (rt.traceRays(rr), rt.traceRays(rr, any_hit=True))
     rt.setTraversal("bvh")
-    for trav in ("bvh", "bvh2"):
+    for trav in ("bvh", "bvh2", "packet"):
         np.testing.assert_array_equal(out[trav][0][0], out["linear"][0][0])
         np.testing.assert_array_equal(bits(out[trav][0][1]), bits(out["linear"][0][1]))
         np.testing.assert_array_equal(out[trav][1][0], out["linear"][1][0])

@@ -89,6 +89,7 @@ struct rt_ctx {
     size_t flags_bytes = 0;
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
+    bool vote = false;
     uint64_t mesh_serial = 0;
     size_t spill_entries = 0;
 
@@ -396,6 +397,7 @@ int rt_create(int device, rt_ctx **out)
         for (int j = 0; j < 4; ++j) c->view[i][j] = (i == j) ? 1.0f : 0.0f;
     c->rng.seed(1);
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0"; /* A/B knob */
+    if (const char *v = getenv("RT_VOTE")) c->vote = std::string(v) == "1";               /* A/B knob */
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess) {
@@ -731,6 +733,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
+        a.vote = c->vote ? 1u : 0u;
         a.tile_order = nullptr;
         if (c->schedule) {
             const int ro = tile_order(c, W, H, hl, stripe, nr, rk, st);

@@ -74,6 +74,7 @@ struct RtTriLaunch {
     int32_t *spill;      /* per-lane stack overflow (4-wide traversal), spill_cap entries per lane */
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
+    uint32_t vote;              /* 1: one query type per wave iteration (majority vote) */
 };
 
 struct RtSphLaunch {

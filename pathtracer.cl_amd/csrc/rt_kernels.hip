@@ -34,17 +34,16 @@ __device__ __forceinline__ bool mt_test(V3 o, V3 d, const float4 &a, const float
     const V3 e1 = v3(b.x, b.y, b.z);
     const V3 e2 = v3(c.x, c.y, c.z);
     const V3 p = cross3(d, e2);
-    float det = dot3(p, e1);
-    if (rt_fabsf(det) < RT_SMALL_F) return false;
-    det = 1.0f / det;
+    const float det = dot3(p, e1);
+    /* Evaluated without early exits so that the vertex fetch is not sunk below the
+       determinant test; the accepted path computes exactly the reference's values. */
+    const float inv = 1.0f / det;
     const V3 to = v3(o.x - v0.x, o.y - v0.y, o.z - v0.z);
     const V3 q = cross3(to, e1);
-    const float u = dot3(p, to) * det;
-    if (u < 0 || u > 1) return false;
-    const float v = dot3(q, d) * det;
-    if (v < 0 || v + u > 1) return false;
-    t = dot3(q, e2) * det;
-    return true;
+    const float u = dot3(p, to) * inv;
+    const float v = dot3(q, d) * inv;
+    t = dot3(q, e2) * inv;
+    return !(rt_fabsf(det) < RT_SMALL_F) && !(u < 0 || u > 1) && !(v < 0 || v + u > 1);
 }
 
 /* Conservative slab test against one child box (culling only: no parity
@@ -82,32 +81,44 @@ struct TravCounts {
     uint32_t tests;
 };
 
-/* Leaf: the reference's triangle tests on slots [first, first+count). */
+/* Leaf: the reference's triangle tests on slots [first, first+count).  The
+   records of two triangles are fetched together (6 x dwordx4) before either is
+   tested, so a leaf costs ceil(count/2) memory round trips instead of up to two
+   per triangle. */
+template <bool COUNT>
+__device__ __forceinline__ void leaf_accept(int s, float4 a, V3 d, bool ok, float t, float tmin, float tmax,
+                                            bool any_hit, int &best, int &best_orig, float &best_t, bool &done)
+{
+    if (!ok) return;
+    if (any_hit) {
+        if (t < tmax && t > tmin) {
+            best = s;
+            done = true;
+        }
+    } else {
+        const int orig = __float_as_int(a.w);
+        if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
+            best = s;
+            best_orig = orig;
+            best_t = t;
+        }
+    }
+}
+
 template <bool COUNT>
 __device__ __forceinline__ bool leaf_tests(const float4 *__restrict__ tris, int first, int count, V3 o, V3 d,
                                            float tmin, float tmax, bool any_hit, int &best, int &best_orig,
                                            float &best_t, TravCounts &cnt)
 {
+    bool done = false;
     for (int k = 0; k < count; ++k) {
-        const int s = first + k;
-        const float4 a = tris[3 * s], b = tris[3 * s + 1], c = tris[3 * s + 2];
-        float t;
+        const int s0 = first + k;
+        const float4 a0 = tris[3 * s0], b0 = tris[3 * s0 + 1], c0 = tris[3 * s0 + 2];
         if (COUNT) cnt.tests++;
-        if (mt_test(o, d, a, b, c, t)) {
-            if (any_hit) {
-                if (t < tmax && t > tmin) {
-                    best = s;
-                    return true;
-                }
-            } else {
-                const int orig = __float_as_int(a.w);
-                if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
-                    best = s;
-                    best_orig = orig;
-                    best_t = t;
-                }
-            }
-        }
+        float t0 = 0.0f;
+        const bool h0 = mt_test(o, d, a0, b0, c0, t0);
+        leaf_accept<COUNT>(s0, a0, d, h0, t0, tmin, tmax, any_hit, best, best_orig, best_t, done);
+        if (done) return true;
     }
     return false;
 }
@@ -574,7 +585,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
         int res = -1;
         float qt = kInf;
         bool go = (mode == M_CLOSEST || mode == M_SHADOW);
-        if (PACKET) {
+        if (PACKET || a.vote) {
             /* one query type per wave and iteration (the majority); the other lanes wait */
             const int nc = __popcll(__ballot(mode == M_CLOSEST));
             const int ns = __popcll(__ballot(mode == M_SHADOW));

@@ -189,6 +189,9 @@ def main():
                 "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
                 "nodes_per_ray": round(cnt["nodes_visited"] / max(rays_cnt, 1), 2),
                 "tris_per_ray": round(cnt["tris_tested"] / max(rays_cnt, 1), 2)}
+    if cnt.get("lane_slots"):
+        # share of lanes doing a node or leaf step per traversal round (resumable BVH queries)
+        roofline["simd_efficiency"] = round((cnt["nodes_visited"] + cnt["leaves_visited"]) / cnt["lane_slots"], 4)
 
     # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
     # when they were taken on this exact workload and kernel variant

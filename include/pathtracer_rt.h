@@ -72,6 +72,9 @@ typedef struct rt_counters {
     uint64_t rays_shadow;
     uint64_t nodes_visited; /* BVH inner nodes fetched (counting launches only) */
     uint64_t tris_tested;   /* ray/triangle tests (counting launches only) */
+    uint64_t leaves_visited; /* BVH leaves entered (counting launches only) */
+    uint64_t lane_slots;     /* lanes x traversal-step rounds of the resumable (BVH) queries: SIMD
+                                efficiency = (nodes_visited + leaves_visited) / lane_slots */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */

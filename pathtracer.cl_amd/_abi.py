@@ -93,6 +93,8 @@ class RtCounters(ctypes.Structure):
         ("rays_shadow", ctypes.c_uint64),
         ("nodes_visited", ctypes.c_uint64),
         ("tris_tested", ctypes.c_uint64),
+        ("leaves_visited", ctypes.c_uint64),
+        ("lane_slots", ctypes.c_uint64),
     ]
 
 

@@ -89,7 +89,7 @@ struct rt_ctx {
     size_t flags_bytes = 0;
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
-    bool vote = false;
+    uint32_t fetch_k = 16;
     uint64_t mesh_serial = 0;
     size_t spill_entries = 0;
 
@@ -119,7 +119,7 @@ struct rt_ctx {
     unsigned long long *d_counters = nullptr;
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
-    rt_counters last = {0, 0, 0, 0};
+    rt_counters last = {0, 0, 0, 0, 0, 0};
     bool have_timing = false;
     int grid_cache[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
@@ -397,10 +397,10 @@ int rt_create(int device, rt_ctx **out)
         for (int j = 0; j < 4; ++j) c->view[i][j] = (i == j) ? 1.0f : 0.0f;
     c->rng.seed(1);
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0"; /* A/B knob */
-    if (const char *v = getenv("RT_VOTE")) c->vote = std::string(v) == "1";               /* A/B knob */
+    if (const char *v = getenv("RT_FETCH_K")) c->fetch_k = (uint32_t)std::max(1, std::min(64, atoi(v))); /* tuning knob */
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_HIP;
     }
@@ -692,7 +692,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         dout = c->d_stage;
         if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
     }
-    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT_N_COUNTERS * sizeof(unsigned long long), st));
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;
     int e = 0;
@@ -733,7 +733,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
-        a.vote = c->vote ? 1u : 0u;
+        a.fetch_k = c->fetch_k;
         a.tile_order = nullptr;
         if (c->schedule) {
             const int ro = tile_order(c, W, H, hl, stripe, nr, rk, st);
@@ -778,12 +778,14 @@ int rt_synchronize(rt_ctx *c)
     if (!c) return RT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    unsigned long long h[4];
+    unsigned long long h[RT_N_COUNTERS];
     HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
     c->last.rays_closest = h[0];
     c->last.rays_shadow = h[1];
     c->last.nodes_visited = h[2];
     c->last.tris_tested = h[3];
+    c->last.leaves_visited = h[4];
+    c->last.lane_slots = h[5];
     return RT_OK;
 }
 

@@ -19,6 +19,8 @@
 #define RT_BVH_MAX_DEPTH (RT_STACK_DEPTH + 1)
 #define RT_BLOCK 256
 #define RT_LEAF_MAX 8
+/* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots */
+#define RT_N_COUNTERS 6
 
 /* One BVH node = 4 x float4 = 64 B (both children's boxes in the parent):
      n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
@@ -70,11 +72,11 @@ struct RtTriLaunch {
     uint32_t sample_rate, max_depth, progressive;
     uint32_t stripe, n_ranks, rank;
     uint32_t *work_counter;
-    unsigned long long *counters; /* [4] */
+    unsigned long long *counters; /* [RT_N_COUNTERS] */
     int32_t *spill;      /* per-lane stack overflow (4-wide traversal), spill_cap entries per lane */
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
-    uint32_t vote;              /* 1: one query type per wave iteration (majority vote) */
+    uint32_t fetch_k;           /* resumable queries: completed lanes that end a stepping round */
 };
 
 struct RtSphLaunch {

@@ -79,6 +79,7 @@ __device__ __forceinline__ float t_slack(float t) { return t * 1.0009765625f + 1
 struct TravCounts {
     uint32_t nodes;
     uint32_t tests;
+    uint32_t leaves;
 };
 
 /* Leaf: the reference's triangle tests on slots [first, first+count).  The
@@ -154,6 +155,123 @@ __device__ __forceinline__ void cas(float &ta, int &ca, float &tb, int &cb)
     ca = c;
 }
 
+/* Resumable per-lane traversal of the binary or 4-wide tree: the whole query
+   state is this struct plus the lane's stack, so a query can be advanced one
+   node (or one leaf) at a time and suspended between steps. */
+struct TravState {
+    int node;      /* next node to visit (>= 0 inner, < 0 leaf) */
+    int best;      /* leaf-order slot of the current closest / occluding hit, -1 none */
+    int best_orig; /* its original triangle index (tie rule) */
+    float best_t;  /* closest hit so far (= tmax of an any-hit query) */
+    V3 inv, oi;    /* 1/d and o/d for the slab tests */
+};
+
+__device__ __forceinline__ void trav_begin(TravState &s, Stack &stk, V3 o, V3 d, float tmax)
+{
+    s.inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    s.oi = v3(o.x * s.inv.x, o.y * s.inv.y, o.z * s.inv.z);
+    s.node = 0;
+    s.best = -1;
+    s.best_orig = -1;
+    s.best_t = tmax;
+    stk.sp = 0;
+}
+
+/* One traversal step; returns true when the query is complete.  Closest hit:
+   the result equals the reference's linear loop (minimum t, ties to the highest
+   original index — rtcommon.h:39-52 with intersects_triangle's `t > tmax`
+   rejection).  Any hit: best >= 0 iff some triangle has tmin < t < tmax
+   (rtcommon.h:59-68). */
+template <int TRAV, bool COUNT>
+__device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                          TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
+                                          TravCounts &cnt)
+{
+    const float tmin_c = -1e-3f;
+    const V3 inv = s.inv, oi = s.oi;
+    int node = s.node;
+    if (node >= 0) {
+        if (COUNT) cnt.nodes++;
+        const float tmax_c = t_slack(s.best_t);
+        if (TRAV == RT_TRAV_BVH2) {
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
+            bool h0, h1;
+            const float t0 = slab(n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, inv, oi, tmin_c, tmax_c, h0);
+            const float t1 = slab(n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, inv, oi, tmin_c, tmax_c, h1);
+            const int c0 = __float_as_int(n3.x);
+            const int c1 = __float_as_int(n3.y);
+            if (h0 && h1) {
+                int nearc = c0, farc = c1;
+                if (t1 < t0) {
+                    nearc = c1;
+                    farc = c0;
+                }
+                stk.push(farc);
+                s.node = nearc;
+                return false;
+            }
+            if (h0 || h1) {
+                s.node = h0 ? c0 : c1;
+                return false;
+            }
+        } else {
+            /* 4-wide: near/far slab planes picked by the direction signs, so each
+               child costs 6 FMAs + max3/min3 and no min/max pairs. */
+            const int nxo = inv.x >= 0.0f ? 0 : 1, nyo = inv.y >= 0.0f ? 2 : 3, nzo = inv.z >= 0.0f ? 4 : 5;
+            const int fxo = 1 - nxo, fyo = 5 - nyo, fzo = 9 - nzo;
+            const float4 *nd = nodes + 8 * node;
+            const float4 nx = nd[nxo], fx = nd[fxo], ny = nd[nyo], fy = nd[fyo], nz = nd[nzo], fz = nd[fzo];
+            const float4 cc = nd[6];
+            float t[4];
+            int c[4];
+            const float nxs[4] = {nx.x, nx.y, nx.z, nx.w}, fxs[4] = {fx.x, fx.y, fx.z, fx.w};
+            const float nys[4] = {ny.x, ny.y, ny.z, ny.w}, fys[4] = {fy.x, fy.y, fy.z, fy.w};
+            const float nzs[4] = {nz.x, nz.y, nz.z, nz.w}, fzs[4] = {fz.x, fz.y, fz.z, fz.w};
+            const int cs[4] = {__float_as_int(cc.x), __float_as_int(cc.y), __float_as_int(cc.z),
+                               __float_as_int(cc.w)};
+            int nhit = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float tn = __builtin_fmaxf(
+                    __builtin_fmaxf(__builtin_fmaf(nxs[i], inv.x, -oi.x), __builtin_fmaf(nys[i], inv.y, -oi.y)),
+                    __builtin_fmaxf(__builtin_fmaf(nzs[i], inv.z, -oi.z), tmin_c));
+                const float tf = __builtin_fminf(
+                    __builtin_fminf(__builtin_fmaf(fxs[i], inv.x, -oi.x), __builtin_fmaf(fys[i], inv.y, -oi.y)),
+                    __builtin_fminf(__builtin_fmaf(fzs[i], inv.z, -oi.z), tmax_c));
+                const bool h = (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
+                t[i] = h ? tn : kInf;
+                c[i] = cs[i];
+                nhit += h ? 1 : 0;
+            }
+            if (nhit > 0) {
+                /* sort the (entry distance, child) pairs: misses (inf) sink to the end */
+                cas(t[0], c[0], t[1], c[1]);
+                cas(t[2], c[2], t[3], c[3]);
+                cas(t[0], c[0], t[2], c[2]);
+                cas(t[1], c[1], t[3], c[3]);
+                cas(t[1], c[1], t[2], c[2]);
+                if (nhit >= 4) stk.push(c[3]);
+                if (nhit >= 3) stk.push(c[2]);
+                if (nhit >= 2) stk.push(c[1]);
+                s.node = c[0];
+                return false;
+            }
+        }
+    } else {
+        const int enc = ~node;
+        if (COUNT) cnt.leaves++;
+        if (leaf_tests<COUNT>(tris, enc >> 3, (enc & 7) + 1, o, d, tmin, s.best_t, any_hit, s.best, s.best_orig,
+                              s.best_t, cnt))
+            return true;
+    }
+    if (stk.sp == 0) return true;
+    s.node = stk.pop();
+    return false;
+}
+
 /* One ray query.  Closest hit (any_hit = false): returns the leaf-order slot of
    the hit (or -1) with t in tmax; the result equals the reference's linear
    loop: minimum t, ties to the highest original index (rtcommon.h:39-52 with
@@ -198,111 +316,12 @@ __device__ __forceinline__ int traverse(const float4 *__restrict__ nodes, const 
         return best;
     }
 
-    const V3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
-    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-    const float tmin_c = -1e-3f;
-    stk.sp = 0;
-    int node = 0;
-    if (TRAV == RT_TRAV_BVH2) {
-        for (;;) {
-            if (node >= 0) {
-                const float4 n0 = nodes[4 * node + 0];
-                const float4 n1 = nodes[4 * node + 1];
-                const float4 n2 = nodes[4 * node + 2];
-                const float4 n3 = nodes[4 * node + 3];
-                if (COUNT) cnt.nodes++;
-                const float tmax_c = t_slack(best_t);
-                bool h0, h1;
-                const float t0 = slab(n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, inv, oi, tmin_c, tmax_c, h0);
-                const float t1 = slab(n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, inv, oi, tmin_c, tmax_c, h1);
-                const int c0 = __float_as_int(n3.x);
-                const int c1 = __float_as_int(n3.y);
-                if (h0 && h1) {
-                    int nearc = c0, farc = c1;
-                    if (t1 < t0) {
-                        nearc = c1;
-                        farc = c0;
-                    }
-                    stk.push(farc);
-                    node = nearc;
-                } else if (h0) {
-                    node = c0;
-                } else if (h1) {
-                    node = c1;
-                } else {
-                    if (stk.sp == 0) break;
-                    node = stk.pop();
-                }
-                continue;
-            }
-            const int enc = ~node;
-            if (leaf_tests<COUNT>(tris, enc >> 3, (enc & 7) + 1, o, d, tmin, tmax, any_hit, best, best_orig, best_t,
-                                  cnt))
-                break;
-            if (stk.sp == 0) break;
-            node = stk.pop();
-        }
-        if (!any_hit) tmax = best_t;
-        return best;
+    TravState st;
+    trav_begin(st, stk, o, d, tmax);
+    while (!trav_step<TRAV, COUNT>(nodes, tris, st, stk, o, d, tmin, any_hit, cnt)) {
     }
-
-    /* 4-wide: near/far slab planes picked once per ray by the direction signs, so
-       each child costs 6 FMAs + max3/min3 and no min/max pairs. */
-    const int nxo = inv.x >= 0.0f ? 0 : 1, nyo = inv.y >= 0.0f ? 2 : 3, nzo = inv.z >= 0.0f ? 4 : 5;
-    const int fxo = 1 - nxo, fyo = 5 - nyo, fzo = 9 - nzo;
-    for (;;) {
-        if (node >= 0) {
-            const float4 *nd = nodes + 8 * node;
-            const float4 nx = nd[nxo], fx = nd[fxo], ny = nd[nyo], fy = nd[fyo], nz = nd[nzo], fz = nd[fzo];
-            const float4 cc = nd[6];
-            if (COUNT) cnt.nodes++;
-            const float tmax_c = t_slack(best_t);
-            float t[4];
-            int c[4];
-            const float nxs[4] = {nx.x, nx.y, nx.z, nx.w}, fxs[4] = {fx.x, fx.y, fx.z, fx.w};
-            const float nys[4] = {ny.x, ny.y, ny.z, ny.w}, fys[4] = {fy.x, fy.y, fy.z, fy.w};
-            const float nzs[4] = {nz.x, nz.y, nz.z, nz.w}, fzs[4] = {fz.x, fz.y, fz.z, fz.w};
-            const int cs[4] = {__float_as_int(cc.x), __float_as_int(cc.y), __float_as_int(cc.z),
-                               __float_as_int(cc.w)};
-            int nhit = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float tn = __builtin_fmaxf(
-                    __builtin_fmaxf(__builtin_fmaf(nxs[i], inv.x, -oi.x), __builtin_fmaf(nys[i], inv.y, -oi.y)),
-                    __builtin_fmaxf(__builtin_fmaf(nzs[i], inv.z, -oi.z), tmin_c));
-                const float tf = __builtin_fminf(
-                    __builtin_fminf(__builtin_fmaf(fxs[i], inv.x, -oi.x), __builtin_fmaf(fys[i], inv.y, -oi.y)),
-                    __builtin_fminf(__builtin_fmaf(fzs[i], inv.z, -oi.z), tmax_c));
-                const bool h = (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
-                t[i] = h ? tn : kInf;
-                c[i] = cs[i];
-                nhit += h ? 1 : 0;
-            }
-            if (nhit == 0) {
-                if (stk.sp == 0) break;
-                node = stk.pop();
-                continue;
-            }
-            /* sort the (entry distance, child) pairs: misses (inf) sink to the end */
-            cas(t[0], c[0], t[1], c[1]);
-            cas(t[2], c[2], t[3], c[3]);
-            cas(t[0], c[0], t[2], c[2]);
-            cas(t[1], c[1], t[3], c[3]);
-            cas(t[1], c[1], t[2], c[2]);
-            if (nhit >= 4) stk.push(c[3]);
-            if (nhit >= 3) stk.push(c[2]);
-            if (nhit >= 2) stk.push(c[1]);
-            node = c[0];
-            continue;
-        }
-        const int enc = ~node;
-        if (leaf_tests<COUNT>(tris, enc >> 3, (enc & 7) + 1, o, d, tmin, tmax, any_hit, best, best_orig, best_t, cnt))
-            break;
-        if (stk.sp == 0) break;
-        node = stk.pop();
-    }
-    if (!any_hit) tmax = best_t;
-    return best;
+    if (!any_hit) tmax = st.best_t;
+    return st.best;
 }
 
 /* Wave-coherent (packet) traversal of the 4-wide tree.  All participating
@@ -436,22 +455,13 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
     return v;
 }
 
-__device__ __forceinline__ void flush_counters(unsigned long long *dst, unsigned long long a, unsigned long long b,
-                                               unsigned long long c, unsigned long long d, bool with_trav)
+__device__ __forceinline__ void flush_counters(unsigned long long *dst, const unsigned long long (&v)[RT_N_COUNTERS],
+                                               bool with_trav)
 {
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (with_trav) {
-        c = wave_sum(c);
-        d = wave_sum(d);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&dst[0], a);
-        atomicAdd(&dst[1], b);
-        if (with_trav) {
-            atomicAdd(&dst[2], c);
-            atomicAdd(&dst[3], d);
-        }
+    const int n = with_trav ? RT_N_COUNTERS : 2;
+    for (int i = 0; i < n; ++i) {
+        const unsigned long long w = wave_sum(v[i]);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&dst[i], w);
     }
 }
 
@@ -478,12 +488,24 @@ __device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uin
 
 constexpr int kMaxLights = 16;
 
-enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_PIXDONE = 4, M_DONE = 5 };
+enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 4 };
 
+/* Per-lane loop, one iteration:
+     D  lanes whose ray query completed advance their path (trace_path_tri) and
+        issue the next query, start the next sample, or write the pixel;
+     A  idle lanes take the next pixels from the queue;
+     B  camera ray of a new sample;
+     C  ray queries.  BVH kinds: queries are resumable — newly issued queries
+        start, then the wave steps every running query one node (or leaf) at a
+        time until `fetch_k` lanes have completed (or none is running), so lanes
+        whose query ended early go back to work instead of idling until the
+        wave's longest query ends.  LINEAR / PACKET: each query runs to
+        completion inside the iteration. */
 template <int TRAV, bool COUNT>
 __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
 {
     constexpr bool PACKET = TRAV == RT_TRAV_PACKET4;
+    constexpr bool RESUME = TRAV == RT_TRAV_BVH2 || TRAV == RT_TRAV_BVH4;
     __shared__ int s_stack[PACKET ? (RT_BLOCK / 64) * kWaveStack : RT_STACK_DEPTH * RT_BLOCK];
     __shared__ float s_light[kMaxLights * 8];
 
@@ -519,6 +541,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
     const float hw = ((float)a.W) / 2.0f;
     const float hh = ((float)a.H) / 2.0f;
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
+    const int fetch_k = (int)a.fetch_k;
 
     int mode = M_IDLE;
     uint32_t x = 0, yl = 0, y = 0, slot = 0;
@@ -531,9 +554,122 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
     V3 hp = ro, hn = ro, so = ro, sd = rd, direct = ro;
     float stmax = 0.0f;
     bool tri_hit = false;
-    unsigned long long n_closest = 0, n_shadow = 0, n_nodes = 0, n_tests = 0;
+    bool running = false; /* a resumable query is in flight */
+    bool fin = false;     /* the lane's query completed: res / qt hold its result */
+    int res = -1;
+    float qt = kInf;
+    TravState ts;
+    ts.node = 0;
+    ts.best = -1;
+    ts.best_orig = -1;
+    ts.best_t = kInf;
+    ts.inv = ro;
+    ts.oi = ro;
+    unsigned long long cnt[RT_N_COUNTERS] = {0, 0, 0, 0, 0, 0};
 
     for (;;) {
+        /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
+        if (fin) {
+            fin = false;
+            bool want_shadow = false, seg_done = false, sample_done = false;
+            if (mode == M_CLOSEST) {
+                ++cnt[0];
+                bool surface = true;
+                if (res >= 0) {
+                    const float4 e1 = tris[3 * res + 1];
+                    const float4 e2 = tris[3 * res + 2];
+                    hp = v3(ro.x + rd.x * qt, ro.y + rd.y * qt, ro.z + rd.z * qt);
+                    hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z)); /* unnormalised, rtcommon.h:389 */
+                    tri_hit = true;
+                } else {
+                    /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
+                    const float hd = intersect_box(ro, rd, RT_SMALL_F, bw, bh, bw);
+                    if (hd > RT_SMALL_F && hd < kInf) {
+                        hp = v3(ro.x + rd.x * hd, ro.y + rd.y * hd, ro.z + rd.z * hd);
+                        hn = box_normal(hp, bw, bh, bw);
+                        tri_hit = false;
+                    } else {
+                        surface = false;
+                        sample_done = true; /* path terminates (rtcommon.h:463-466) */
+                    }
+                }
+                if (surface) { /* sample_direct_illumination_tri, rtcommon.h:78-105 */
+                    so = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
+                    direct = v3(0.0f, 0.0f, 0.0f);
+                    light = 0;
+                    if (n_lights > 0) want_shadow = true;
+                    else seg_done = true;
+                }
+            } else {
+                ++cnt[1];
+                if (res < 0) { /* unoccluded: rtcommon.h:93-101 */
+                    const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
+                    if (cw > 0) {
+                        direct.x += s_light[light * 8 + 4] * cw;
+                        direct.y += s_light[light * 8 + 5] * cw;
+                        direct.z += s_light[light * 8 + 6] * cw;
+                    }
+                }
+                ++light;
+                if (light < n_lights) want_shadow = true;
+                else seg_done = true;
+            }
+            if (want_shadow) { /* one sample per light: frand r1 then r2 (rtcommon.h:92) */
+                const float r1 = frand(seed);
+                const float r2 = frand(seed);
+                const V3 lc = v3(s_light[light * 8 + 0], s_light[light * 8 + 1], s_light[light * 8 + 2]);
+                sd = sphere_light_dir(so, lc, s_light[light * 8 + 3], r1, r2, stmax);
+                mode = M_SHADOW;
+            }
+            if (seg_done) {
+                const float scale = 1.0f * RT_M_1_PI_F;
+                if (tri_hit) { /* rtcommon.h:411-421: no bounce off triangles */
+                    col_x += prop.x * direct.x * scale * 0.7f;
+                    col_y += prop.y * direct.y * scale * 0.7f;
+                    col_z += prop.z * direct.z * scale * 0.7f;
+                    sample_done = true;
+                } else { /* rtcommon.h:435-461: albedo 0.7, Lambert bounce (drawn even at the last depth) */
+                    prop.x *= 0.7f;
+                    prop.y *= 0.7f;
+                    prop.z *= 0.7f;
+                    col_x += prop.x * direct.x * scale;
+                    col_y += prop.y * direct.y * scale;
+                    col_z += prop.z * direct.z * scale;
+                    ro = hp;
+                    const float r1 = frand(seed);
+                    const float r2 = frand(seed);
+                    rd = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
+                    ++depth;
+                    if (depth > a.max_depth) sample_done = true;
+                    else mode = M_CLOSEST;
+                }
+            }
+            if (sample_done) {
+                acc_x += col_x;
+                acc_y += col_y;
+                acc_z += col_z;
+                ++sample;
+                mode = M_NEWSAMPLE;
+                if (sample >= spp) { /* raytracer.cl:234-242 */
+                    const float n = (float)spp;
+                    float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
+                    float4 *dst = out + ((size_t)yl * a.W + x);
+                    if (a.progressive > 0) {
+                        const float4 old = *dst;
+                        const float t = 1.0f / (float)a.progressive;
+                        p.x = old.x + (p.x - old.x) * t;
+                        p.y = old.y + (p.y - old.y) * t;
+                        p.z = old.z + (p.z - old.z) * t;
+                        p.w = old.w + (p.w - old.w) * t;
+                    }
+                    *dst = p;
+                    a.seeds[slot] = seed.x;
+                    a.seeds[plane + slot] = seed.y;
+                    mode = M_IDLE;
+                }
+            }
+        }
+
         /* ---- A: refill idle lanes from the pixel queue: one atomic per wave,
                 lanes ranked by a prefix popcount of the idle ballot ---- */
         const unsigned long long idle = __ballot(mode == M_IDLE);
@@ -560,7 +696,22 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                         seed.y = a.seeds[plane + slot];
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
-                        mode = (spp > 0) ? M_NEWSAMPLE : M_PIXDONE;
+                        if (spp > 0) {
+                            mode = M_NEWSAMPLE;
+                        } else { /* no samples: 0/0 pixels, seeds untouched (raytracer.cl:234-242) */
+                            const float n = 0.0f;
+                            float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
+                            float4 *dst = out + ((size_t)yl * a.W + x);
+                            if (a.progressive > 0) {
+                                const float4 old = *dst;
+                                const float t = 1.0f / (float)a.progressive;
+                                p.x = old.x + (p.x - old.x) * t;
+                                p.y = old.y + (p.y - old.y) * t;
+                                p.z = old.z + (p.z - old.z) * t;
+                                p.w = old.w + (p.w - old.w) * t;
+                            }
+                            *dst = p;
+                        }
                     }
                 }
             }
@@ -581,138 +732,74 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
             mode = M_CLOSEST;
         }
 
-        /* ---- C: this iteration's ray query ---- */
-        int res = -1;
-        float qt = kInf;
-        bool go = (mode == M_CLOSEST || mode == M_SHADOW);
-        if (PACKET || a.vote) {
-            /* one query type per wave and iteration (the majority); the other lanes wait */
-            const int nc = __popcll(__ballot(mode == M_CLOSEST));
-            const int ns = __popcll(__ballot(mode == M_SHADOW));
-            go = (ns > nc) ? (mode == M_SHADOW) : (mode == M_CLOSEST);
-            /* a trivially unoccluded shadow ray never waits */
-            go = go || (mode == M_SHADOW && !(stmax > RT_SMALL_F));
-        }
-        if (go) {
-            const bool shadow = (mode == M_SHADOW);
-            if (shadow) qt = stmax;
-            TravCounts tc = {0u, 0u};
-            /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
-               returns true): skip the traversal, same result */
-            if (!shadow || qt > RT_SMALL_F) {
-                if (PACKET)
-                    res = traverse_packet4<COUNT>(nodes, tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F, qt,
-                                                  shadow, s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
-                else
-                    res = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd,
-                                                RT_SMALL_F, qt, shadow, stk, tc);
-            }
-            if (COUNT) {
-                n_nodes += tc.nodes;
-                n_tests += tc.tests;
-            }
-        }
-
-        /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
-        bool want_shadow = false, seg_done = false, sample_done = false;
-        if (mode == M_CLOSEST && go) {
-            ++n_closest;
-            bool surface = true;
-            if (res >= 0) {
-                const float4 e1 = tris[3 * res + 1];
-                const float4 e2 = tris[3 * res + 2];
-                hp = v3(ro.x + rd.x * qt, ro.y + rd.y * qt, ro.z + rd.z * qt);
-                hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z)); /* unnormalised, rtcommon.h:389 */
-                tri_hit = true;
-            } else {
-                /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
-                const float hd = intersect_box(ro, rd, RT_SMALL_F, bw, bh, bw);
-                if (hd > RT_SMALL_F && hd < kInf) {
-                    hp = v3(ro.x + rd.x * hd, ro.y + rd.y * hd, ro.z + rd.z * hd);
-                    hn = box_normal(hp, bw, bh, bw);
-                    tri_hit = false;
-                } else {
-                    surface = false;
-                    sample_done = true; /* path terminates (rtcommon.h:463-466) */
+        /* ---- C: ray queries ---- */
+        const bool pending = (mode == M_CLOSEST || mode == M_SHADOW) && !running && !fin;
+        if (RESUME) {
+            if (pending) {
+                const bool shadow = (mode == M_SHADOW);
+                qt = shadow ? stmax : kInf;
+                res = -1;
+                /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
+                   returns true): no traversal, same result */
+                if (shadow && !(qt > RT_SMALL_F)) fin = true;
+                else {
+                    trav_begin(ts, stk, shadow ? so : ro, shadow ? sd : rd, qt);
+                    running = true;
                 }
             }
-            if (surface) { /* sample_direct_illumination_tri, rtcommon.h:78-105 */
-                so = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
-                direct = v3(0.0f, 0.0f, 0.0f);
-                light = 0;
-                if (n_lights > 0) want_shadow = true;
-                else seg_done = true;
+            for (;;) {
+                if (running) {
+                    const bool shadow = (mode == M_SHADOW);
+                    TravCounts tc = {0u, 0u, 0u};
+                    if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F,
+                                               shadow, tc)) {
+                        running = false;
+                        fin = true;
+                        res = ts.best;
+                        qt = ts.best_t;
+                    }
+                    if (COUNT) {
+                        cnt[2] += tc.nodes;
+                        cnt[3] += tc.tests;
+                        cnt[4] += tc.leaves;
+                    }
+                }
+                if (COUNT) ++cnt[5];
+                if (!__any(running)) break;
+                if (__popcll(__ballot(fin)) >= fetch_k) break;
             }
-        } else if (mode == M_SHADOW && go) {
-            ++n_shadow;
-            if (res < 0) { /* unoccluded: rtcommon.h:93-101 */
-                const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
-                if (cw > 0) {
-                    direct.x += s_light[light * 8 + 4] * cw;
-                    direct.y += s_light[light * 8 + 5] * cw;
-                    direct.z += s_light[light * 8 + 6] * cw;
+        } else if (pending) {
+            bool go = true;
+            if (PACKET) {
+                /* one query type per wave and iteration (the majority); the other lanes wait */
+                const int nc = __popcll(__ballot(mode == M_CLOSEST));
+                const int ns = __popcll(__ballot(mode == M_SHADOW));
+                go = (ns > nc) ? (mode == M_SHADOW) : (mode == M_CLOSEST);
+                /* a trivially unoccluded shadow ray never waits */
+                go = go || (mode == M_SHADOW && !(stmax > RT_SMALL_F));
+            }
+            if (go) {
+                const bool shadow = (mode == M_SHADOW);
+                qt = shadow ? stmax : kInf;
+                res = -1;
+                TravCounts tc = {0u, 0u, 0u};
+                if (!shadow || qt > RT_SMALL_F) {
+                    if (PACKET)
+                        res = traverse_packet4<COUNT>(nodes, tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F, qt,
+                                                      shadow, s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
+                    else
+                        res = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd,
+                                                    RT_SMALL_F, qt, shadow, stk, tc);
+                }
+                fin = true;
+                if (COUNT) {
+                    cnt[2] += tc.nodes;
+                    cnt[3] += tc.tests;
                 }
             }
-            ++light;
-            if (light < n_lights) want_shadow = true;
-            else seg_done = true;
-        }
-        if (want_shadow) { /* one sample per light: frand r1 then r2 (rtcommon.h:92) */
-            const float r1 = frand(seed);
-            const float r2 = frand(seed);
-            const V3 lc = v3(s_light[light * 8 + 0], s_light[light * 8 + 1], s_light[light * 8 + 2]);
-            sd = sphere_light_dir(so, lc, s_light[light * 8 + 3], r1, r2, stmax);
-            mode = M_SHADOW;
-        }
-        if (seg_done) {
-            const float scale = 1.0f * RT_M_1_PI_F;
-            if (tri_hit) { /* rtcommon.h:411-421: no bounce off triangles */
-                col_x += prop.x * direct.x * scale * 0.7f;
-                col_y += prop.y * direct.y * scale * 0.7f;
-                col_z += prop.z * direct.z * scale * 0.7f;
-                sample_done = true;
-            } else { /* rtcommon.h:435-461: albedo 0.7, Lambert bounce (drawn even at the last depth) */
-                prop.x *= 0.7f;
-                prop.y *= 0.7f;
-                prop.z *= 0.7f;
-                col_x += prop.x * direct.x * scale;
-                col_y += prop.y * direct.y * scale;
-                col_z += prop.z * direct.z * scale;
-                ro = hp;
-                const float r1 = frand(seed);
-                const float r2 = frand(seed);
-                rd = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
-                ++depth;
-                if (depth > a.max_depth) sample_done = true;
-                else mode = M_CLOSEST;
-            }
-        }
-        if (sample_done) {
-            acc_x += col_x;
-            acc_y += col_y;
-            acc_z += col_z;
-            ++sample;
-            mode = (sample < spp) ? M_NEWSAMPLE : M_PIXDONE;
-        }
-        if (mode == M_PIXDONE) { /* raytracer.cl:234-242 */
-            const float n = (float)spp;
-            float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
-            float4 *dst = out + ((size_t)yl * a.W + x);
-            if (a.progressive > 0) {
-                const float4 old = *dst;
-                const float t = 1.0f / (float)a.progressive;
-                p.x = old.x + (p.x - old.x) * t;
-                p.y = old.y + (p.y - old.y) * t;
-                p.z = old.z + (p.z - old.z) * t;
-                p.w = old.w + (p.w - old.w) * t;
-            }
-            *dst = p;
-            a.seeds[slot] = seed.x;
-            a.seeds[plane + slot] = seed.y;
-            mode = M_IDLE;
         }
     }
-    flush_counters(a.counters, n_closest, n_shadow, n_nodes, n_tests, COUNT);
+    flush_counters(a.counters, cnt, COUNT);
 }
 
 /* ======================================================================== */
@@ -891,7 +978,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
         a.seeds[slot] = seed.x;
         a.seeds[plane + slot] = seed.y;
     }
-    flush_counters(a.counters, n_closest, n_shadow, 0, 0, false);
+    const unsigned long long cnt[RT_N_COUNTERS] = {n_closest, n_shadow, 0, 0, 0, 0};
+    flush_counters(a.counters, cnt, false);
 }
 
 /* ======================================================================== */
@@ -908,7 +996,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     if (i >= n) return;
     const rt_ray r = rays[i];
     float t = r.tmax;
-    TravCounts tc = {0u, 0u};
+    TravCounts tc = {0u, 0u, 0u};
     Stack stk;
     stk.lds = s_stack + threadIdx.x;
     stk.spill = spill + (size_t)i * spill_cap;
@@ -949,7 +1037,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_probe(const float4 *__restrict__ n
     const V3 o = v3(cam.position.x, cam.position.y, cam.position.z);
     const V3 d = camera_dir(cam, ((float)x + 0.5f) - ((float)W) / 2.0f, ((float)y + 0.5f) - ((float)H) / 2.0f);
     float t = kInf;
-    TravCounts tc = {0u, 0u};
+    TravCounts tc = {0u, 0u, 0u};
     const int hit = traverse_packet4<false>(nodes, tris, o, d, RT_SMALL_F, t, false,
                                             s_wstack + (threadIdx.x >> 6) * kWaveStack, tc);
     if (valid) flags[(size_t)yl * W + x] = hit >= 0 ? 1 : 0;

@@ -32,8 +32,8 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-NODE_BYTES = {"bvh": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h
-TRI_BYTES = 48   # one triangle record (v0+orig, e1, e2 as float4), csrc/rt_internal.h
+NODE_BYTES = {"bvh": 56, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h
+TRI_BYTES = 40   # bytes read per triangle test: v0+orig (16), e1 (12), e2 (12) of the 48-B record, csrc/rt_internal.h
 PIXEL_BYTES = 16 + 8 + 8  # RGBA32F store + seed read + seed write per pixel
 
 
@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--sample-rate", type=int, default=None)
     ap.add_argument("--stripe", type=int, default=8)
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
-    ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh2", "linear", "packet"],
+    ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "bvh2", "linear", "packet"],
                     help="bvh: 4-wide BVH (default); bvh2: binary BVH; linear: the reference loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
@@ -235,7 +235,7 @@ def main():
         dist.destroy_process_group()
 
 
-TRAVERSAL_NAMES = {"bvh": "4-wide BVH", "bvh2": "binary BVH", "linear": "linear (reference)",
+TRAVERSAL_NAMES = {"bvh": "4-wide compressed BVH", "bvh4f": "4-wide BVH", "bvh2": "binary BVH", "linear": "linear (reference)",
                    "packet": "4-wide BVH, wave-coherent"}
 
 

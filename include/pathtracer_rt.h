@@ -46,10 +46,18 @@ enum {
 
 /* Triangle traversal: the reference's linear loop (rtcommon.h:39-68) or a BVH
    (identical results: closest hit = minimum t, ties to the highest index).
-   RT_TRAVERSAL_BVH is the 4-wide tree traversed per lane; RT_TRAVERSAL_BVH2 the
-   binary tree it is collapsed from; RT_TRAVERSAL_PACKET the 4-wide tree walked
-   wave-coherently (one node sequence per wave, scalar node fetches). */
-enum { RT_TRAVERSAL_BVH = 0, RT_TRAVERSAL_LINEAR = 1, RT_TRAVERSAL_BVH2 = 2, RT_TRAVERSAL_PACKET = 3 };
+   RT_TRAVERSAL_BVH is the 4-wide tree with compressed (8-bit quantised) 64-B
+   nodes traversed per lane; RT_TRAVERSAL_BVH4F the same tree with full-precision
+   128-B nodes; RT_TRAVERSAL_BVH2 the binary tree they are collapsed from;
+   RT_TRAVERSAL_PACKET the 4-wide tree walked wave-coherently (one node sequence
+   per wave, scalar node fetches). */
+enum {
+    RT_TRAVERSAL_BVH = 0,
+    RT_TRAVERSAL_LINEAR = 1,
+    RT_TRAVERSAL_BVH2 = 2,
+    RT_TRAVERSAL_PACKET = 3,
+    RT_TRAVERSAL_BVH4F = 4
+};
 
 /* rt_render flags */
 enum {

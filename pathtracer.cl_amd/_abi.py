@@ -37,6 +37,7 @@ RT_TRAVERSAL_BVH = 0
 RT_TRAVERSAL_LINEAR = 1
 RT_TRAVERSAL_BVH2 = 2
 RT_TRAVERSAL_PACKET = 3
+RT_TRAVERSAL_BVH4F = 4
 
 RT_OUT_DEVICE = 1
 

@@ -420,6 +420,68 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
         }
     }
 
+    /* Compressed copy of the 4-wide tree (64 B per node, see rt_internal.h):
+       child boxes quantised to 8 bits per plane on a per-node power-of-two grid,
+       rounded outward so every dequantised box contains the exact one. */
+    out.nodes4q.assign(16ull * out.n_nodes4, 0u);
+    for (uint32_t i = 0; i < out.n_nodes4; ++i) {
+        const float *n = out.nodes4.data() + 32ull * i;
+        uint32_t *q = out.nodes4q.data() + 16ull * i;
+        int32_t code[4];
+        std::memcpy(code, &n[24], 16);
+        uint32_t exps = 0;
+        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+        for (int ax = 0; ax < 3; ++ax) {
+            const float *lo = n + 8 * ax, *hi = n + 8 * ax + 4;
+            float omin = INFINITY, omax = -INFINITY;
+            for (int k = 0; k < 4; ++k)
+                if (code[k] != RT_EMPTY_CHILD) {
+                    omin = std::min(omin, lo[k]);
+                    omax = std::max(omax, hi[k]);
+                }
+            if (!(omin <= omax)) omin = omax = 0.0f; /* no children (cannot happen) */
+            const float origin = omin;
+            /* smallest grid step 2^e with 255 steps covering the extent (outward-rounded) */
+            int e = -64;
+            const double ext = (double)omax - (double)origin;
+            if (ext > 0) e = std::max(-64, (int)std::ceil(std::log2(ext / 255.0)));
+            for (;; ++e) {
+                const double step = std::ldexp(1.0, e);
+                bool ok = true;
+                uint32_t wl = 0, wh = 0;
+                for (int k = 0; k < 4; ++k) {
+                    int32_t l = 255, h = 0; /* empty slot: inverted box, never entered */
+                    if (code[k] != RT_EMPTY_CHILD) {
+                        l = (int32_t)std::floor(((double)lo[k] - origin) / step);
+                        h = (int32_t)std::ceil(((double)hi[k] - origin) / step);
+                        l = std::max(l, 0);
+                        if (h > 255) ok = false;
+                        /* containment in exact arithmetic */
+                        if ((double)origin + l * step > (double)lo[k] || (double)origin + h * step < (double)hi[k])
+                            ok = false;
+                    }
+                    wl |= (uint32_t)l << (8 * k);
+                    wh |= (uint32_t)(h & 255) << (8 * k);
+                }
+                if (ok) {
+                    qlo[ax] = wl;
+                    qhi[ax] = wh;
+                    break;
+                }
+            }
+            std::memcpy(&q[ax], &origin, 4);
+            exps |= (uint32_t)(e + 128) << (8 * ax);
+        }
+        q[3] = exps;
+        std::memcpy(&q[4], code, 16);
+        q[8] = qlo[0];
+        q[9] = qhi[0];
+        q[10] = qlo[1];
+        q[11] = qhi[1];
+        q[12] = qlo[2];
+        q[13] = qhi[2];
+    }
+
     /* Triangles in leaf order: (v0, orig), (e1 = v1 - v0), (e2 = v2 - v0). */
     out.tris.assign(12ull * n_tris, 0.0f);
     for (uint32_t s = 0; s < n_tris; ++s) {

@@ -81,6 +81,7 @@ struct rt_ctx {
     RtBvh bvh;
     float *d_nodes = nullptr;  /* binary tree */
     float *d_nodes4 = nullptr; /* 4-wide tree */
+    uint32_t *d_nodes4q = nullptr; /* 4-wide tree, compressed nodes */
     float *d_tris = nullptr;
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
@@ -271,17 +272,21 @@ int trav_kind(const rt_ctx *c)
     if (c->traversal == RT_TRAVERSAL_LINEAR) return RT_TRAV_LINEAR;
     if (c->traversal == RT_TRAVERSAL_BVH2) return RT_TRAV_BVH2;
     if (c->traversal == RT_TRAVERSAL_PACKET) return RT_TRAV_PACKET4;
-    return RT_TRAV_BVH4;
+    if (c->traversal == RT_TRAVERSAL_BVH4F) return RT_TRAV_BVH4;
+    return RT_TRAV_BVH4Q;
 }
 
 uint32_t spill_cap(const rt_ctx *c)
 {
-    return trav_kind(c) == RT_TRAV_BVH4 && c->bvh.stack4 > RT_STACK_DEPTH ? c->bvh.stack4 - RT_STACK_DEPTH : 0;
+    const int k = trav_kind(c);
+    return (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) && c->bvh.stack4 > RT_STACK_DEPTH ? c->bvh.stack4 - RT_STACK_DEPTH
+                                                                                        : 0;
 }
 
 const float *trav_nodes(const rt_ctx *c)
 {
     const int k = trav_kind(c);
+    if (k == RT_TRAV_BVH4Q) return reinterpret_cast<const float *>(c->d_nodes4q);
     return (k == RT_TRAV_BVH4 || k == RT_TRAV_PACKET4) ? c->d_nodes4 : c->d_nodes;
 }
 
@@ -417,6 +422,7 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_lights);
     free_dev(c->d_nodes);
     free_dev(c->d_nodes4);
+    free_dev(c->d_nodes4q);
     free_dev(c->d_spill);
     free_dev(c->d_order);
     free_dev(c->d_flags);
@@ -467,14 +473,18 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
     free_dev(c->d_nodes);
     free_dev(c->d_nodes4);
+    free_dev(c->d_nodes4q);
     free_dev(c->d_tris);
     c->d_nodes = c->d_nodes4 = c->d_tris = nullptr;
+    c->d_nodes4q = nullptr;
     c->n_tris = 0;
     HIPCHK(c, hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->d_nodes4, b.nodes4.size() * sizeof(float)));
+    HIPCHK(c, hipMalloc(&c->d_nodes4q, b.nodes4q.size() * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
     HIPCHK(c, hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_nodes4q, b.nodes4q.data(), b.nodes4q.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_tris, b.tris.data(), b.tris.size() * sizeof(float), hipMemcpyHostToDevice));
     c->n_tris = n_tris;
     c->mesh_serial++;
@@ -560,7 +570,7 @@ int rt_set_params(rt_ctx *c, uint32_t sample_rate, uint32_t max_depth)
 
 int rt_set_traversal(rt_ctx *c, int t)
 {
-    if (!c || t < RT_TRAVERSAL_BVH || t > RT_TRAVERSAL_PACKET) return RT_ERR_ARG;
+    if (!c || t < RT_TRAVERSAL_BVH || t > RT_TRAVERSAL_BVH4F) return RT_ERR_ARG;
     c->traversal = t;
     return RT_OK;
 }

@@ -39,6 +39,14 @@
    RT_EMPTY_CHILD marks an unused slot.  Collapsed from the binary SAH tree
    (largest-area child expanded first). */
 #define RT_EMPTY_CHILD 0x7fffffff
+/* Compressed 4-wide node = 16 dwords = 64 B (two per cache line), same tree:
+     d[0..2] = origin.xyz (float), d[3] = biased exponents (e + 128) of x, y, z in bytes 0..2,
+     d[4..7] = child[0..3] (as above),
+     d[8] = lo.x, d[9] = hi.x, d[10] = lo.y, d[11] = hi.y, d[12] = lo.z, d[13] = hi.z:
+            one byte per child (child k in byte k), plane = origin + q * 2^e,
+     d[14..15] = 0.
+   The quantised box contains the exact child box (floor / ceil); an unused slot
+   has lo = 255 > hi = 0. */
 
 struct RtBvh {
     std::vector<float> nodes; /* binary: 16 floats per node */
@@ -46,7 +54,8 @@ struct RtBvh {
     uint32_t n_nodes = 0;
     uint32_t n_leaves = 0;
     uint32_t depth = 0;
-    std::vector<float> nodes4; /* 4-wide: 32 floats per node */
+    std::vector<float> nodes4;     /* 4-wide: 32 floats per node */
+    std::vector<uint32_t> nodes4q; /* 4-wide, compressed: 16 dwords per node */
     uint32_t n_nodes4 = 0;
     uint32_t depth4 = 0;
     uint32_t stack4 = 0; /* worst-case traversal stack entries of the 4-wide tree */
@@ -93,7 +102,7 @@ struct RtSphLaunch {
 
 /* All return a hipError_t as int (0 = success). */
 /* traversal kinds (kernel template parameter) */
-enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH2 = 1, RT_TRAV_BVH4 = 2, RT_TRAV_PACKET4 = 3 };
+enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH2 = 1, RT_TRAV_BVH4 = 2, RT_TRAV_PACKET4 = 3, RT_TRAV_BVH4Q = 4 };
 
 int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream);
 int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);

@@ -217,6 +217,57 @@ __device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, cons
                 s.node = h0 ? c0 : c1;
                 return false;
             }
+        } else if (TRAV == RT_TRAV_BVH4Q) {
+            /* compressed 4-wide node (rt_internal.h): per axis, plane t =
+               q * (2^e / d) + (origin - o) / d; near/far planes picked by the
+               direction signs; 56 of the node's 64 B are fetched. */
+            const uint4 *nd = reinterpret_cast<const uint4 *>(nodes) + 4 * node;
+            const uint4 hd = nd[0];
+            const uint4 cc = nd[1];
+            const uint4 bxy = nd[2];
+            const uint2 bz = reinterpret_cast<const uint2 *>(nd)[6];
+            const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(hd.w & 255u) - 128);
+            const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((hd.w >> 8) & 255u) - 128);
+            const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((hd.w >> 16) & 255u) - 128);
+            const float bx = __builtin_fmaf(__uint_as_float(hd.x), inv.x, -oi.x);
+            const float by = __builtin_fmaf(__uint_as_float(hd.y), inv.y, -oi.y);
+            const float bzo = __builtin_fmaf(__uint_as_float(hd.z), inv.z, -oi.z);
+            const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+            const uint32_t nxw = px ? bxy.x : bxy.y, fxw = px ? bxy.y : bxy.x;
+            const uint32_t nyw = py ? bxy.z : bxy.w, fyw = py ? bxy.w : bxy.z;
+            const uint32_t nzw = pz ? bz.x : bz.y, fzw = pz ? bz.y : bz.x;
+            const int cs[4] = {(int)cc.x, (int)cc.y, (int)cc.z, (int)cc.w};
+            float t[4];
+            int c[4];
+            int nhit = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int sh = 8 * i;
+                const float tn = __builtin_fmaxf(
+                    __builtin_fmaxf(__builtin_fmaf((float)((nxw >> sh) & 255u), sx, bx),
+                                    __builtin_fmaf((float)((nyw >> sh) & 255u), sy, by)),
+                    __builtin_fmaxf(__builtin_fmaf((float)((nzw >> sh) & 255u), sz, bzo), tmin_c));
+                const float tf = __builtin_fminf(
+                    __builtin_fminf(__builtin_fmaf((float)((fxw >> sh) & 255u), sx, bx),
+                                    __builtin_fmaf((float)((fyw >> sh) & 255u), sy, by)),
+                    __builtin_fminf(__builtin_fmaf((float)((fzw >> sh) & 255u), sz, bzo), tmax_c));
+                const bool h = (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
+                t[i] = h ? tn : kInf;
+                c[i] = cs[i];
+                nhit += h ? 1 : 0;
+            }
+            if (nhit > 0) {
+                cas(t[0], c[0], t[1], c[1]);
+                cas(t[2], c[2], t[3], c[3]);
+                cas(t[0], c[0], t[2], c[2]);
+                cas(t[1], c[1], t[3], c[3]);
+                cas(t[1], c[1], t[2], c[2]);
+                if (nhit >= 4) stk.push(c[3]);
+                if (nhit >= 3) stk.push(c[2]);
+                if (nhit >= 2) stk.push(c[1]);
+                s.node = c[0];
+                return false;
+            }
         } else {
             /* 4-wide: near/far slab planes picked by the direction signs, so each
                child costs 6 FMAs + max3/min3 and no min/max pairs. */
@@ -505,7 +556,7 @@ template <int TRAV, bool COUNT>
 __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
 {
     constexpr bool PACKET = TRAV == RT_TRAV_PACKET4;
-    constexpr bool RESUME = TRAV == RT_TRAV_BVH2 || TRAV == RT_TRAV_BVH4;
+    constexpr bool RESUME = TRAV == RT_TRAV_BVH2 || TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
     __shared__ int s_stack[PACKET ? (RT_BLOCK / 64) * kWaveStack : RT_STACK_DEPTH * RT_BLOCK];
     __shared__ float s_light[kMaxLights * 8];
 
@@ -1066,6 +1117,7 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
     if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR);
     else if (trav == RT_TRAV_BVH2) RT_LAUNCH_TRIS(RT_TRAV_BVH2);
     else if (trav == RT_TRAV_PACKET4) RT_LAUNCH_TRIS(RT_TRAV_PACKET4);
+    else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q);
     else RT_LAUNCH_TRIS(RT_TRAV_BVH4);
 #undef RT_LAUNCH_TRIS
     return (int)hipGetLastError();
@@ -1097,6 +1149,9 @@ int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris,
     else if (trav == RT_TRAV_PACKET4)
         hipLaunchKernelGGL((k_trace_rays<RT_TRAV_PACKET4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit,
                            spill, spill_cap, out_idx, out_t);
+    else if (trav == RT_TRAV_BVH4Q)
+        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH4Q>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit,
+                           spill, spill_cap, out_idx, out_t);
     else
         hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
                            spill_cap, out_idx, out_t);
@@ -1114,6 +1169,8 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
     else if (trav == RT_TRAV_PACKET4)
         e = count ? occupancy(k_tris<RT_TRAV_PACKET4, true>, &per_cu)
                   : occupancy(k_tris<RT_TRAV_PACKET4, false>, &per_cu);
+    else if (trav == RT_TRAV_BVH4Q)
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4Q, false>, &per_cu);
     else
         e = count ? occupancy(k_tris<RT_TRAV_BVH4, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4, false>, &per_cu);
     if (e) return e;

@@ -20,7 +20,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-KERNEL = "k_tris<2, false>"
+KERNEL = "k_tris<4, false>"
 
 
 def counters(path: Path):

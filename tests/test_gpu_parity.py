@@ -42,7 +42,7 @@ def test_golden_spheres(name, tracer, pt, golden, golden_meta):
     rt.close()
 
 
-TRAVERSALS = ["bvh", "bvh2", "packet", "linear"]
+TRAVERSALS = ["bvh", "bvh4f", "bvh2", "packet", "linear"]
 
 
 @pytest.mark.parametrize("trav", TRAVERSALS)

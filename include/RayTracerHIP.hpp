@@ -108,6 +108,10 @@ public:
               "rayTrace");
     }
 
+    /* Blocking readback of the last frame into host memory (the non-sharing display
+       path, GlutCLWindow.cpp:214-225); n_floats = capacity of `host`. */
+    void read(float *host, size_t n_floats) { check(rt_read(ctx_, host, n_floats), "read"); }
+
     rt_counters counters() const
     {
         rt_counters c;

@@ -149,6 +149,11 @@ int rt_render(rt_ctx *ctx, float *out_rgba, uint32_t width, uint32_t height, uin
 int rt_render_async(rt_ctx *ctx, float *out_rgba, uint32_t width, uint32_t height, uint32_t progression,
                     int kernel, const rt_tile *tile, int flags, void *hip_stream);
 int rt_synchronize(rt_ctx *ctx);
+/* Blocking readback of the last render's framebuffer (W x rows x 4 floats) into host
+   memory: the non-sharing display path, enqueueReadBuffer(clPBOBuff, CL_TRUE, ...)
+   into the mapped PBO (GlutCLWindow.cpp:214-225).  Valid while the buffer passed to
+   that render (device framebuffers) is alive.  n_floats = capacity of `host`. */
+int rt_read(rt_ctx *ctx, float *host, size_t n_floats);
 /* Rows of `height` owned by `tile` (NULL: height). */
 uint32_t rt_tile_rows(uint32_t height, const rt_tile *tile);
 

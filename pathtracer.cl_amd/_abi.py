@@ -126,6 +126,7 @@ SIGNATURES = {
     "rt_render_async": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, ctypes.POINTER(RtTile), _i32, _vp]),
     "rt_synchronize": (_i32, [_vp]),
     "rt_tile_rows": (_u32, [_u32, ctypes.POINTER(RtTile)]),
+    "rt_read": (_i32, [_vp, _vp, _sz]),
     "rt_get_counters": (_i32, [_vp, ctypes.POINTER(RtCounters)]),
     "rt_set_counting": (_i32, [_vp, _i32]),
     "rt_last_kernel_ms": (_i32, [_vp, ctypes.POINTER(_f32)]),

@@ -122,6 +122,8 @@ struct rt_ctx {
     size_t stage_bytes = 0;
     rt_counters last = {0, 0, 0, 0, 0, 0};
     bool have_timing = false;
+    const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
+    size_t last_bytes = 0;
     int grid_cache[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
@@ -779,6 +781,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
     }
     if (e) return hip_fail(c, (hipError_t)e, "kernel launch");
     c->have_timing = true;
+    c->last_out = dout;
+    c->last_bytes = out_bytes;
     if (!(flags & RT_OUT_DEVICE)) HIPCHK(c, hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, st));
     return RT_OK;
 }
@@ -805,6 +809,17 @@ int rt_render(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int 
     const int r = rt_render_async(c, out, W, H, prog, kernel, tile, flags, nullptr);
     if (r != RT_OK) return r;
     return rt_synchronize(c); /* cmdQueue.finish(), RayTracerCL.cpp:292 */
+}
+
+int rt_read(rt_ctx *c, float *host, size_t n_floats)
+{
+    if (!c || !host) return RT_ERR_ARG;
+    if (!c->last_out) return fail(c, RT_ERR_STATE, "rt_read before any render");
+    if (n_floats * sizeof(float) < c->last_bytes) return fail(c, RT_ERR_ARG, "rt_read: host buffer too small");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(host, c->last_out, c->last_bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
 }
 
 int rt_get_counters(const rt_ctx *c, rt_counters *out)

@@ -204,6 +204,12 @@ class RayTracer:
             if sync:
                 self.synchronize()
 
+    def read(self, host: np.ndarray) -> None:
+        """Blocking readback of the last frame into `host` (GlutCLWindow.cpp:214-225)."""
+        if host.dtype != np.float32 or not host.flags["C_CONTIGUOUS"]:
+            raise ValueError("host buffer must be a contiguous float32 array")
+        self._check(self._lib.rt_read(self._h, _abi.ptr(host), host.size), "rt_read")
+
     def synchronize(self) -> None:
         self._check(self._lib.rt_synchronize(self._h), "rt_synchronize")
 

@@ -256,6 +256,12 @@ def test_device_framebuffer_matches_host(tracer, pt):
         for p in range(2):
             rt.rayTrace(out, W, H, p, kernel=2)
     np.testing.assert_array_equal(bits(host), bits(dev.cpu().numpy()))
+    # rt_read: the blocking readback of the last (device) frame
+    back = np.full(W * H * 4, -1.0, np.float32)
+    rt.read(back)
+    np.testing.assert_array_equal(bits(host), bits(back))
+    with pytest.raises(pt.RtError):
+        rt.read(np.zeros(16, np.float32))
 
 
 def test_dragon_full_size_properties(tracer, pt, oracle):

@@ -122,8 +122,29 @@ def main():
     rows = ptdist.max_tile_rows(H, args.stripe, n_ranks) if n_ranks > 1 else H
     out = torch.zeros(rows * W * 4, dtype=torch.float32, device=f"cuda:{device}")
 
+    Wp, Hp = sc.padded_dims(W, H)
+    # sphere config: progressive frames (progression 0, 1, 2, ...: row-shifted seeds); on a
+    # tile the seed rows that cross stripe boundaries move between ranks every frame
+    progressive = kernel != pt.RayTracer.KERNEL_TRIS
+    halo = ptdist.SeedHalo(H, Hp, args.stripe, n_ranks) if (progressive and n_ranks > 1) else None
+    frame_no = [0]
+
+    # halo buffers live on the GPU for RCCL; the gloo rehearsal moves them through host memory
+    halo_dev = f"cuda:{device}" if (dist and dist.get_backend() == "nccl") else "cpu"
+
+    def pack(rows):
+        buf = torch.empty((2, len(rows), Wp), dtype=torch.int32, device=halo_dev)
+        rt.packSeedRows(rows, buf)
+        return buf
+
     def step():
-        rt.rayTrace(out, W, H, 0, kernel=kernel, tile=tile)
+        p = frame_no[0] if progressive else 0
+        if halo is not None:
+            ptdist.exchange_seed_rows(halo.plan(p), pack, rt.unpackSeedRows, Wp, device=halo_dev)
+        rt.rayTrace(out, W, H, p, kernel=kernel, tile=tile, halo=halo is not None)
+        if halo is not None:
+            halo.commit(p)
+        frame_no[0] += 1
         c = rt.counters()
         if n_ranks > 1:
             ptdist.gather_frame(out, H, W, args.stripe)
@@ -132,7 +153,6 @@ def main():
     # first render creates the seed layout; snapshot it so the counting launch and the
     # first timed frame see the same seeds
     step()
-    Wp, Hp = sc.padded_dims(W, H)
     seeds0 = rt.getSeeds()
     # counting launch (untimed): traversal node / triangle-test counts for the roofline
     rt.setCounting(True)
@@ -243,7 +263,7 @@ def workload_name(cfg, n_tris, W, H, sr, traversal):
     if n_tris:
         return (f"raytrace_tris {cfg}-class synthetic mesh {n_tris} tris, {W}x{H}, sampleRate {sr} "
                 f"({sr * sr} spp, one launch), maxDepth 6, {TRAVERSAL_NAMES[traversal]} traversal")
-    return f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}"
+    return f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}, progressive frames (row-shifted seeds)"
 
 
 def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, verts, idx):

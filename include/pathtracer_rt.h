@@ -61,7 +61,9 @@ enum {
 
 /* rt_render flags */
 enum {
-    RT_OUT_DEVICE = 1 /* `out` is a device pointer on the context's GPU (else host memory) */
+    RT_OUT_DEVICE = 1, /* `out` is a device pointer on the context's GPU (else host memory) */
+    RT_SEEDS_HALO = 2  /* the caller keeps the seed rows this tile reads current (seed-row halo,
+                          below): permits progressive sphere frames on a tile */
 };
 
 /* Row-stripe tile of the frame owned by one rank (multi-GPU sharding).
@@ -136,6 +138,15 @@ int rt_set_seed_layout(rt_ctx *ctx, uint32_t wpad, uint32_t hpad);
 int rt_set_seeds(rt_ctx *ctx, const uint32_t *seeds, size_t count);
 int rt_get_seeds(const rt_ctx *ctx, uint32_t *out, size_t count);
 int rt_seed_layout(const rt_ctx *ctx, uint32_t *wpad, uint32_t *hpad);
+/* Seed-row halo for multi-GPU progressive sphere frames.  raytrace reads and writes
+   seed row (y + progressive) % Hpad for pixel row y (get_seed / put_seed,
+   raytracer.cl:20-30), so between frames one seed row per stripe boundary moves to
+   the neighbouring rank.  These copy whole rows (both planes) of the context's seed
+   layout to / from a packed buffer laid out [plane][i][x] (2 * n * Wpad words);
+   `buf` is a device pointer with RT_OUT_DEVICE in flags, else host memory.  The
+   rows to move are planned by pathtracer.cl_amd/dist.py (SeedHalo). */
+int rt_pack_seed_rows(rt_ctx *ctx, const uint32_t *rows, uint32_t n, uint32_t *buf, int flags);
+int rt_unpack_seed_rows(rt_ctx *ctx, const uint32_t *rows, uint32_t n, const uint32_t *buf, int flags);
 /* glibc rand() stream restated (tests compare it with libc's own rand()). */
 int rt_glibc_rand_fill(uint32_t seed, uint32_t *out, size_t count, uint32_t skip);
 

@@ -40,6 +40,7 @@ RT_TRAVERSAL_PACKET = 3
 RT_TRAVERSAL_BVH4F = 4
 
 RT_OUT_DEVICE = 1
+RT_SEEDS_HALO = 2
 
 # --- record layouts (rt_types.h) --------------------------------------------------------
 VEC3 = ("<f4", 3)
@@ -122,6 +123,8 @@ SIGNATURES = {
     "rt_get_seeds": (_i32, [_vp, _vp, _sz]),
     "rt_seed_layout": (_i32, [_vp, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
     "rt_glibc_rand_fill": (_i32, [_u32, _vp, _sz, _u32]),
+    "rt_pack_seed_rows": (_i32, [_vp, _vp, _u32, _vp, _i32]),
+    "rt_unpack_seed_rows": (_i32, [_vp, _vp, _u32, _vp, _i32]),
     "rt_render": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, ctypes.POINTER(RtTile), _i32]),
     "rt_render_async": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, ctypes.POINTER(RtTile), _i32, _vp]),
     "rt_synchronize": (_i32, [_vp]),

@@ -87,6 +87,9 @@ struct rt_ctx {
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
     uint8_t *d_flags = nullptr;  /* probe flags */
+    uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
+    uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
+    size_t halo_rows_cap = 0, halo_buf_cap = 0;
     size_t flags_bytes = 0;
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
@@ -428,6 +431,8 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_spill);
     free_dev(c->d_order);
     free_dev(c->d_flags);
+    free_dev(c->d_halo_rows);
+    free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
     free_dev(c->d_seeds);
     free_dev(c->d_work);
@@ -653,10 +658,10 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
     if (kernel < RT_KERNEL_SPHERES || kernel > RT_KERNEL_TRIS) return fail(c, RT_ERR_ARG, "unknown kernel");
     if (tile && tile->n_ranks > 1 && (tile->stripe_rows == 0 || tile->rank >= tile->n_ranks))
         return fail(c, RT_ERR_ARG, "bad tile");
-    if (tile && tile->n_ranks > 1 && kernel == RT_KERNEL_SPHERES && prog > 0)
+    if (tile && tile->n_ranks > 1 && kernel == RT_KERNEL_SPHERES && prog > 0 && !(flags & RT_SEEDS_HALO))
         return fail(c, RT_ERR_ARG,
-                    "row-shifted seeds (raytracer.cl:20-30) cross stripe boundaries: progressive sphere frames need "
-                    "the full frame on one device");
+                    "row-shifted seeds (raytracer.cl:20-30) cross stripe boundaries: progressive sphere frames on "
+                    "a tile need the seed-row halo (rt_pack_seed_rows / rt_unpack_seed_rows, flag RT_SEEDS_HALO)");
     if (kernel == RT_KERNEL_TRIS && c->n_tris == 0) return fail(c, RT_ERR_NO_MESH, "no mesh set");
     if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
     if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && c->bvh.depth > RT_STACK_DEPTH)
@@ -809,6 +814,54 @@ int rt_render(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int 
     const int r = rt_render_async(c, out, W, H, prog, kernel, tile, flags, nullptr);
     if (r != RT_OK) return r;
     return rt_synchronize(c); /* cmdQueue.finish(), RayTracerCL.cpp:292 */
+}
+
+static int seed_rows_io(rt_ctx *c, const uint32_t *rows, uint32_t n, uint32_t *buf, int flags, bool unpack)
+{
+    if (!c || (n && (!rows || !buf))) return RT_ERR_ARG;
+    if (!c->wpad) return fail(c, RT_ERR_STATE, "no seed layout");
+    for (uint32_t i = 0; i < n; ++i)
+        if (rows[i] >= c->hpad) return fail(c, RT_ERR_ARG, "seed row out of range");
+    if (!n) return RT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t words = 2ull * n * c->wpad;
+    if (c->halo_rows_cap < n) {
+        free_dev(c->d_halo_rows);
+        c->d_halo_rows = nullptr;
+        c->halo_rows_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_halo_rows, n * sizeof(uint32_t)));
+        c->halo_rows_cap = n;
+    }
+    uint32_t *dbuf = buf;
+    const bool on_device = (flags & RT_OUT_DEVICE) != 0;
+    if (!on_device) {
+        if (c->halo_buf_cap < words) {
+            free_dev(c->d_halo_buf);
+            c->d_halo_buf = nullptr;
+            c->halo_buf_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_halo_buf, words * sizeof(uint32_t)));
+            c->halo_buf_cap = words;
+        }
+        dbuf = c->d_halo_buf;
+        if (unpack) HIPCHK(c, hipMemcpyAsync(dbuf, buf, words * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_halo_rows, rows, n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+    const int e = rt_launch_seed_rows(c->d_seeds, c->wpad, c->hpad, c->d_halo_rows, n, dbuf, unpack, c->stream);
+    if (e) return hip_fail(c, (hipError_t)e, "seed-row kernel");
+    if (!on_device && !unpack)
+        HIPCHK(c, hipMemcpyAsync(buf, dbuf, words * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_pack_seed_rows(rt_ctx *c, const uint32_t *rows, uint32_t n, uint32_t *buf, int flags)
+{
+    return seed_rows_io(c, rows, n, buf, flags, false);
+}
+
+int rt_unpack_seed_rows(rt_ctx *c, const uint32_t *rows, uint32_t n, const uint32_t *buf, int flags)
+{
+    return seed_rows_io(c, rows, n, const_cast<uint32_t *>(buf), flags, true);
 }
 
 int rt_read(rt_ctx *c, float *host, size_t n_floats)

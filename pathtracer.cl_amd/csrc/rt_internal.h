@@ -112,6 +112,10 @@ int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris,
 /* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
 int rt_launch_probe(const float *nodes4, const float *tris, const rt_camera &cam, uint32_t W, uint32_t H, uint32_t Hl,
                     uint32_t stripe, uint32_t n_ranks, uint32_t rank, uint8_t *flags, void *stream);
+/* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed
+   buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
+int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,
+                        uint32_t *buf, bool unpack, void *stream);
 /* Persistent-grid size for the triangle kernel on this device. */
 int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks);
 

@@ -1094,10 +1094,37 @@ __global__ __launch_bounds__(RT_BLOCK) void k_probe(const float4 *__restrict__ n
     if (valid) flags[(size_t)yl * W + x] = hit >= 0 ? 1 : 0;
 }
 
+/* Seed-row halo pack / unpack (multi-GPU progressive sphere frames). */
+__global__ __launch_bounds__(RT_BLOCK) void k_seed_rows(uint32_t *__restrict__ seeds, uint32_t wpad, uint32_t hpad,
+                                                        const uint32_t *__restrict__ rows, uint32_t n,
+                                                        uint32_t *__restrict__ buf, int unpack)
+{
+    const size_t idx = (size_t)blockIdx.x * RT_BLOCK + threadIdx.x;
+    const size_t per_plane = (size_t)n * wpad;
+    if (idx >= 2 * per_plane) return;
+    const uint32_t p = (uint32_t)(idx / per_plane);
+    const uint32_t i = (uint32_t)((idx % per_plane) / wpad);
+    const uint32_t x = (uint32_t)(idx % wpad);
+    uint32_t *s = seeds + (size_t)p * wpad * hpad + (size_t)rows[i] * wpad + x;
+    if (unpack) *s = buf[idx];
+    else buf[idx] = *s;
+}
+
 } // namespace
 
 /* ======================================================================== */
 /* Launchers                                                                 */
+
+int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,
+                        uint32_t *buf, bool unpack, void *stream)
+{
+    const size_t total = 2ull * n * wpad;
+    if (!total) return 0;
+    dim3 grid((unsigned)((total + RT_BLOCK - 1) / RT_BLOCK)), block(RT_BLOCK);
+    hipLaunchKernelGGL(k_seed_rows, grid, block, 0, (hipStream_t)stream, seeds, wpad, hpad, rows, n, buf,
+                       unpack ? 1 : 0);
+    return (int)hipGetLastError();
+}
 
 template <typename K>
 static int occupancy(K kern, int *per_cu)

@@ -10,6 +10,12 @@ which over xGMI is one point-to-point transfer per sender.
 
 Progressive accumulation stays local (each rank mixes into its own rows), so the gather is
 only needed when the root wants to display/store the frame.
+
+The sphere kernel (raytrace) is the exception: pixel row y reads and writes seed row
+(y + progressive) % Hpad (get_seed / put_seed, raytracer.cl:20-30), so between progressive
+frames one seed row per stripe boundary migrates to the neighbouring rank.  `SeedHalo`
+plans those moves (it tracks the last writer of every seed row) and `exchange_seed_rows`
+performs them with point-to-point sends (RCCL over xGMI, 2 * Wpad * 4 B per row).
 """
 from __future__ import annotations
 
@@ -71,3 +77,62 @@ def gather_frame(local, height: int, width: int, stripe: int, group=None, root: 
     if rank != root:
         return None
     return assemble([g.reshape(rows_max, width, 4) for g in gathered], height, width, stripe)
+
+
+class SeedHalo:
+    """Seed-row bookkeeping for tiled progressive sphere frames.
+
+    Every rank holds the full seed planes; a rank's copy of a row is current only if it
+    wrote it last (or nobody has: the initial seeds are identical everywhere).  Before a
+    frame with row shift s, rank j needs rows (y + s) % Hpad for its pixel rows y < H;
+    `plan(s)` lists, per (src, dst) rank pair, the rows dst must receive from their last
+    writer src.  `commit(s)` records the frame's writes."""
+
+    def __init__(self, height: int, hpad: int, stripe: int, n_ranks: int):
+        if hpad < height:
+            raise ValueError("Hpad < H")
+        self.height, self.hpad, self.stripe, self.n_ranks = height, hpad, stripe, n_ranks
+        y = np.arange(height)
+        self.row_rank = (y // stripe) % n_ranks
+        self.writer = np.full(hpad, -1, np.int64)
+
+    def _rows(self, shift: int) -> np.ndarray:
+        return (np.arange(self.height) + int(shift)) % self.hpad
+
+    def plan(self, shift: int) -> dict:
+        r = self._rows(shift)
+        src = self.writer[r]
+        dst = self.row_rank
+        need = (src >= 0) & (src != dst)
+        out = {}
+        for s_, d_, row in zip(src[need], dst[need], r[need]):
+            out.setdefault((int(s_), int(d_)), []).append(int(row))
+        return {k: np.asarray(v, np.uint32) for k, v in sorted(out.items())}
+
+    def commit(self, shift: int) -> None:
+        self.writer[self._rows(shift)] = self.row_rank
+
+
+def exchange_seed_rows(plan: dict, pack, unpack, n_words_per_row: int, device=None, group=None) -> int:
+    """Carry out a SeedHalo plan on this rank: `pack(rows) -> tensor` ([2, n, Wpad] uint32)
+    for rows this rank sends, `unpack(rows, tensor)` for rows it receives, moved with
+    point-to-point sends (torch.distributed: RCCL for CUDA tensors, gloo on CPU).
+    Returns the number of rows this rank received."""
+    import torch
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    ops, recvs = [], []
+    for (src, dst), rows in plan.items():
+        if src == rank:
+            ops.append(dist.P2POp(dist.isend, pack(rows), dst, group))
+        elif dst == rank:
+            buf = torch.empty((2, len(rows), n_words_per_row), dtype=torch.int32, device=device)
+            ops.append(dist.P2POp(dist.irecv, buf, src, group))
+            recvs.append((rows, buf))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    for rows, buf in recvs:
+        unpack(rows, buf)
+    return sum(len(r) for r, _ in recvs)

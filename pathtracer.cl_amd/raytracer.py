@@ -162,6 +162,20 @@ class RayTracer:
             s = np.ascontiguousarray(seeds, np.uint32).reshape(-1)
             self._check(self._lib.rt_set_seeds(self._h, _abi.ptr(s), s.size), "rt_set_seeds")
 
+    def packSeedRows(self, rows, buf) -> None:
+        """Copy seed rows (both planes) into `buf` ([2, n, Wpad] uint32; numpy or torch CUDA)."""
+        r = np.ascontiguousarray(rows, np.uint32)
+        flags = _abi.RT_OUT_DEVICE if getattr(buf, "is_cuda", False) else 0
+        self._check(self._lib.rt_pack_seed_rows(self._h, _abi.ptr(r), r.size, _abi.ptr(buf), flags),
+                    "rt_pack_seed_rows")
+
+    def unpackSeedRows(self, rows, buf) -> None:
+        """Write seed rows (both planes) from `buf` ([2, n, Wpad] uint32; numpy or torch CUDA)."""
+        r = np.ascontiguousarray(rows, np.uint32)
+        flags = _abi.RT_OUT_DEVICE if getattr(buf, "is_cuda", False) else 0
+        self._check(self._lib.rt_unpack_seed_rows(self._h, _abi.ptr(r), r.size, _abi.ptr(buf), flags),
+                    "rt_unpack_seed_rows")
+
     def getSeeds(self) -> np.ndarray:
         w, h = ctypes.c_uint32(), ctypes.c_uint32()
         self._check(self._lib.rt_seed_layout(self._h, ctypes.byref(w), ctypes.byref(h)), "rt_seed_layout")
@@ -171,10 +185,12 @@ class RayTracer:
 
     # ---- render (RayTracerCL::rayTrace) ---------------------------------------------------
     def rayTrace(self, out, width: int, height: int, progression: int, kernel: int = _abi.RT_KERNEL_SPHERES,
-                 tile: tuple[int, int, int] | None = None, stream=None, sync: bool = True) -> None:
-        """Render into `out` (W*H*4 float32 — or tile rows*W*4 — numpy or torch CUDA tensor)."""
+                 tile: tuple[int, int, int] | None = None, stream=None, sync: bool = True, halo: bool = False) -> None:
+        """Render into `out` (W*H*4 float32 — or tile rows*W*4 — numpy or torch CUDA tensor).
+        halo=True: the caller keeps this tile's seed rows current (dist.SeedHalo), which
+        permits progressive sphere frames on a tile."""
         self._sync_scene()
-        flags = 0
+        flags = _abi.RT_SEEDS_HALO if halo else 0
         if not isinstance(out, np.ndarray):
             if getattr(out, "is_cuda", False):
                 flags |= _abi.RT_OUT_DEVICE

@@ -65,3 +65,89 @@ def test_gather_frame_gloo(world, stripe, tmp_path, oracle, pt):
     mp.spawn(_worker, args=(world, _free_port(), H, W, stripe, str(fp), str(rp)), nprocs=world, join=True)
     got = np.load(rp)
     np.testing.assert_array_equal(got.view(np.uint32), full.view(np.uint32))
+
+
+# ---- seed-row halo for tiled progressive sphere frames (raytracer.cl:20-30) ----------------
+
+def _halo_schedule():
+    """Progression sequence with a restart (camera move resets progression to 0)."""
+    return [0, 1, 2, 3, 4, 5, 0, 1, 2, 9, 10]
+
+
+def _write_value(row, frame_no):
+    return (row * 7919 + frame_no * 104729 + 1) & 0x7FFFFFFF
+
+
+@pytest.mark.parametrize("H,hpad,stripe,n", [(29, 32, 4, 2), (45, 48, 8, 3), (64, 64, 8, 4), (17, 24, 3, 2)])
+def test_seed_halo_plan_keeps_every_read_current(pt, H, hpad, stripe, n):
+    """Single-process model of N ranks: each rank reads seed rows (y+s)%Hpad of its pixel
+    rows, which must hold the latest value written by any rank, then writes them."""
+    import ptload
+
+    pdist = ptload.submodule("dist")
+    halo = pdist.SeedHalo(H, hpad, stripe, n)
+    truth = np.arange(hpad, dtype=np.int64) * 3 + 11  # initial seeds, replicated
+    local = [truth.copy() for _ in range(n)]
+    moved = 0
+    for f, s in enumerate(_halo_schedule()):
+        for (src, dst), rows in halo.plan(s).items():
+            local[dst][rows] = local[src][rows]
+            moved += len(rows)
+        for y in range(H):
+            r = (y + s) % hpad
+            k = halo.row_rank[y]
+            assert local[k][r] == truth[r], (f, s, y, r)
+            truth[r] = local[k][r] = _write_value(r, f)
+        halo.commit(s)
+    assert moved > 0
+
+
+def _halo_worker(rank, world, port, H, hpad, wpad, stripe, result_path):
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ptload
+
+    pdist = ptload.submodule("dist")
+    halo = pdist.SeedHalo(H, hpad, stripe, world)
+    seeds = np.zeros((2, hpad, wpad), np.int32)
+    seeds[0] = (np.arange(hpad)[:, None] * 5 + np.arange(wpad)[None, :]) & 0xFFFF
+    seeds[1] = seeds[0] ^ 0x5A5A
+    truth = seeds.copy()  # every rank replays all writes to know the expected state
+    ok = True
+    received = 0
+
+    def pack(rows):
+        return torch.from_numpy(np.ascontiguousarray(seeds[:, rows.astype(np.int64), :]))
+
+    def unpack(rows, buf):
+        seeds[:, rows.astype(np.int64), :] = buf.numpy()
+
+    for f, s in enumerate(_halo_schedule()):
+        received += pdist.exchange_seed_rows(halo.plan(s), pack, unpack, wpad)
+        for y in range(H):
+            r = (y + s) % hpad
+            if halo.row_rank[y] == rank:
+                ok &= bool(np.array_equal(seeds[:, r, :], truth[:, r, :]))
+                seeds[:, r, :] = _write_value(r, f) + np.arange(wpad)[None, :]
+            truth[:, r, :] = _write_value(r, f) + np.arange(wpad)[None, :]
+        halo.commit(s)
+    flags = torch.tensor([int(ok), received], dtype=torch.int64)
+    dist.all_reduce(flags[:1], op=dist.ReduceOp.MIN)
+    dist.all_reduce(flags[1:], op=dist.ReduceOp.SUM)
+    if rank == 0:
+        np.save(result_path, flags.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H,hpad,stripe", [(2, 29, 32, 4), (3, 45, 48, 8)])
+def test_seed_halo_exchange_gloo(world, H, hpad, stripe, tmp_path):
+    rp = tmp_path / "flags.npy"
+    mp.spawn(_halo_worker, args=(world, _free_port(), H, hpad, 32, stripe, str(rp)), nprocs=world, join=True)
+    ok, received = np.load(rp)
+    assert ok == 1 and received > 0

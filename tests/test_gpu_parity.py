@@ -236,6 +236,68 @@ def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt):
         np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full))
 
 
+@pytest.mark.parametrize("n_ranks,stripe,H", [(2, 8, 53), (3, 4, 45)])
+def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt):
+    """raytrace (row-shifted seeds) on row-stripe tiles over progressive frames, with the
+    seed-row halo moved between contexts through device buffers (rt_pack/unpack_seed_rows,
+    the path dist.exchange_seed_rows drives over RCCL): every frame reassembles bit-exactly
+    to the single-device frame, and every seed row equals the single-device seeds on its
+    last writer.  Includes a restart (progression back to 0)."""
+    import torch
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    sc = pt.scenes
+    W, sr = 72, 1
+    Wp, Hp = sc.padded_dims(W, H)
+    seeds = sc.default_seeds(Wp, Hp)
+    cam = sc.camera_spherical(W, **sc.MAIN_CAMERA)
+
+    def make():
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.main_scene())
+        rt.setCamera(cam)
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setSeeds(Wp, Hp, seeds)
+        return rt
+
+    ref = make()
+    ranks = [make() for _ in range(n_ranks)]
+    halo = dist.SeedHalo(H, Hp, stripe, n_ranks)
+    full = np.zeros(W * H * 4, np.float32)
+    rows = [dist.tile_rows(H, stripe, n_ranks, r) for r in range(n_ranks)]
+    tiles = [torch.zeros(len(rows[r]) * W * 4, dtype=torch.float32, device="cuda:0") for r in range(n_ranks)]
+    moved = 0
+    try:
+        for p in [0, 1, 2, 3, 4, 0, 1, 2]:
+            ref.rayTrace(full, W, H, p, kernel=0)
+            for (src, dst), rws in halo.plan(p).items():
+                buf = torch.empty((2, len(rws), Wp), dtype=torch.int32, device="cuda:0")
+                ranks[src].packSeedRows(rws, buf)
+                ranks[dst].unpackSeedRows(rws, buf)
+                moved += len(rws)
+            for r in range(n_ranks):
+                ranks[r].rayTrace(tiles[r], W, H, p, kernel=0, tile=(stripe, n_ranks, r), halo=True)
+            halo.commit(p)
+            frame = dist.assemble([t.cpu().numpy().reshape(-1, W, 4) for t in tiles], H, W, stripe)
+            np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full), err_msg=f"progression {p}")
+        ref_seeds = ref.getSeeds().reshape(2, Hp, Wp)
+        got = [rk.getSeeds().reshape(2, Hp, Wp) for rk in ranks]
+        for row in range(Hp):
+            w = halo.writer[row]
+            if w >= 0:
+                np.testing.assert_array_equal(got[w][:, row], ref_seeds[:, row])
+        assert moved > 0
+        # without the halo flag a progressive sphere tile is refused
+        with pytest.raises(pt.RtError):
+            ranks[0].rayTrace(tiles[0], W, H, 1, kernel=0, tile=(stripe, n_ranks, 0))
+    finally:
+        ref.close()
+        for rk in ranks:
+            rk.close()
+
+
 def test_device_framebuffer_matches_host(tracer, pt):
     import torch
 

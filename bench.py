@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
     ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "bvh2", "linear", "packet"],
                     help="bvh: 4-wide BVH (default); bvh2: binary BVH; linear: the reference loop")
+    ap.add_argument("--ply", default=None, help="render this PLY mesh (normalised, SURVEY §8d) instead of "
+                    "the synthetic mesh of the config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
@@ -109,7 +111,16 @@ def main():
     args.linear = args.traversal == "linear"
     rt.setTraversal(args.traversal)
     mesh_info = {}
-    if n_tris:
+    if args.ply and kernel == pt.RayTracer.KERNEL_TRIS:
+        t0 = time.time()
+        verts, idx = sc.load_ply(args.ply)
+        t1 = time.time()
+        n_tris = len(idx)
+        cfg = f"PLY {Path(args.ply).name}"
+        rt.setMesh(verts, idx)
+        mesh_info = rt.meshInfo()
+        mesh_info["load_seconds"] = round(t1 - t0, 3)
+    elif n_tris:
         t0 = time.time()
         verts, idx = sc.make_mesh(n_tris)
         t1 = time.time()
@@ -260,6 +271,9 @@ TRAVERSAL_NAMES = {"bvh": "4-wide compressed BVH", "bvh4f": "4-wide BVH", "bvh2"
 
 
 def workload_name(cfg, n_tris, W, H, sr, traversal):
+    if n_tris and cfg.startswith("PLY "):
+        return (f"raytrace_tris {cfg[4:]} ({n_tris} tris, normalised), {W}x{H}, sampleRate {sr} "
+                f"({sr * sr} spp, one launch), maxDepth 6, {TRAVERSAL_NAMES[traversal]} traversal")
     if n_tris:
         return (f"raytrace_tris {cfg}-class synthetic mesh {n_tris} tris, {W}x{H}, sampleRate {sr} "
                 f"({sr * sr} spp, one launch), maxDepth 6, {TRAVERSAL_NAMES[traversal]} traversal")

@@ -186,6 +186,22 @@ int rt_trace_rays(rt_ctx *ctx, const rt_ray *rays, uint32_t n, int any_hit, int3
 uint32_t rt_mesh_vertex_count(uint32_t n_tris);
 int rt_make_mesh(uint32_t n_tris, float cx, float cy, float cz, float r, float *verts_xyz, int32_t *idx);
 
+/* ---- PLY meshes: PLYLoader (clrt/PLYLoader.cpp:4-90) over ply.c (ply.c:2457-2720).
+   ascii / binary_little_endian / binary_big_endian; vertex x, y, z as float32, face
+   `vertex_indices` lists (polygons fan-triangulated, < 3 vertices dropped, indices
+   range-checked — the reference copies only 2-vertex faces, PLYLoader.cpp:74); other
+   properties and elements skipped.  open decodes the file and reports the counts;
+   read copies into caller buffers (3*n_verts floats, 3*n_tris ints). ---- */
+typedef struct rt_ply rt_ply;
+int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_tris);
+int rt_ply_read(const rt_ply *ply, float *verts_xyz, int32_t *idx);
+uint32_t rt_ply_dropped_faces(const rt_ply *ply);
+int rt_ply_close(rt_ply *ply);
+const char *rt_ply_last_error(void); /* message of the last failed rt_ply_open (this thread's process) */
+/* Scale uniformly to `max_extent` on the longest axis, centre x and z on 0 and rest the
+   lowest point on y = floor_y (extent 3 on the box floor y = -5). */
+int rt_normalize_mesh(float *verts_xyz, uint32_t n_verts, float max_extent, float floor_y);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,6 +136,12 @@ SIGNATURES = {
     "rt_trace_rays": (_i32, [_vp, _vp, _u32, _i32, _vp, _vp]),
     "rt_mesh_vertex_count": (_u32, [_u32]),
     "rt_make_mesh": (_i32, [_u32, _f32, _f32, _f32, _f32, _vp, _vp]),
+    "rt_ply_open": (_i32, [ctypes.c_char_p, ctypes.POINTER(_vp), ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    "rt_ply_read": (_i32, [_vp, _vp, _vp]),
+    "rt_ply_dropped_faces": (_u32, [_vp]),
+    "rt_ply_close": (_i32, [_vp]),
+    "rt_ply_last_error": (ctypes.c_char_p, []),
+    "rt_normalize_mesh": (_i32, [_vp, _u32, _f32, _f32]),
 }
 
 _LIB = None

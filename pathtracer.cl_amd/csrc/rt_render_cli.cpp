@@ -6,7 +6,7 @@
  * (W*H*4 little-endian floats) and/or a PFM.
  *
  *   rt_render [--scene main|ply] [--width W] [--height H] [--frames F]
- *             [--sample-rate S] [--depth D] [--mesh N_TRIS] [--linear]
+ *             [--sample-rate S] [--depth D] [--mesh N_TRIS | --ply FILE] [--linear]
  *             [--raw out.f32] [--pfm out.pfm] [--device K]
  */
 #include <hip/hip_runtime.h>
@@ -79,7 +79,8 @@ void add_scene(RayTracerHIP &rt, bool ply)
 int usage()
 {
     std::fprintf(stderr, "usage: rt_render [--scene main|ply] [--width W] [--height H] [--frames F] "
-                         "[--sample-rate S] [--depth D] [--mesh N] [--linear] [--raw f] [--pfm f] [--device K]\n");
+                         "[--sample-rate S] [--depth D] [--mesh N | --ply FILE] [--linear] [--raw f] [--pfm f] "
+                         "[--device K]\n");
     return 2;
 }
 
@@ -87,7 +88,7 @@ int usage()
 
 int main(int argc, char **argv)
 {
-    std::string scene = "main", raw, pfm;
+    std::string scene = "main", raw, pfm, ply_path;
     unsigned W = 512, H = 512, frames = 1, sr = 1, depth = 6, n_tris = 0;
     int device = 0;
     bool linear = false;
@@ -107,12 +108,13 @@ int main(int argc, char **argv)
         else if (a == "--sample-rate") sr = (unsigned)std::atoi(v);
         else if (a == "--depth") depth = (unsigned)std::atoi(v);
         else if (a == "--mesh") n_tris = (unsigned)std::atoi(v);
+        else if (a == "--ply") ply_path = v;
         else if (a == "--raw") raw = v;
         else if (a == "--pfm") pfm = v;
         else if (a == "--device") device = std::atoi(v);
         else return usage();
     }
-    const bool ply = scene == "ply" || n_tris > 0;
+    const bool ply = scene == "ply" || n_tris > 0 || !ply_path.empty();
     try {
         RayTracerHIP rt(device);
         add_scene(rt, ply);
@@ -122,7 +124,22 @@ int main(int argc, char **argv)
         if (ply) rt.setCameraSpherical(target, 40.0f, 105.0f, 5.0f); /* plymain.cpp:115-117 */
         else rt.setCameraSpherical(target, 14.0f, 118.0f, 5.0f);     /* main.cpp:127-128 */
         int kernel = RT_KERNEL_SPHERES;
-        if (n_tris) {
+        if (!ply_path.empty()) { /* plymain.cpp:121, with the mesh actually handed to the tracer */
+            rt_ply *mesh = nullptr;
+            uint32_t nv = 0, nt = 0;
+            if (rt_ply_open(ply_path.c_str(), &mesh, &nv, &nt) != RT_OK) {
+                std::fprintf(stderr, "rt_render: %s\n", rt_ply_last_error());
+                return 1;
+            }
+            std::vector<float> v(3ull * nv);
+            std::vector<int> idx(3ull * nt);
+            const int rr = rt_ply_read(mesh, v.data(), idx.data());
+            rt_ply_close(mesh);
+            if (rr != RT_OK || rt_normalize_mesh(v.data(), nv, 3.0f, -5.0f) != RT_OK) return 1;
+            rt.setMesh(v.data(), nv, idx.data(), nt);
+            rt.setTraversal(linear ? RT_TRAVERSAL_LINEAR : RT_TRAVERSAL_BVH);
+            kernel = RT_KERNEL_TRIS;
+        } else if (n_tris) {
             std::vector<float> v(3ull * rt_mesh_vertex_count(n_tris));
             std::vector<int> idx(3ull * n_tris);
             if (rt_make_mesh(n_tris, 0.0f, -2.2f, 0.0f, 2.5f, v.data(), idx.data()) != RT_OK) return 1;

@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
     ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "bvh2", "linear", "packet"],
                     help="bvh: 4-wide BVH (default); bvh2: binary BVH; linear: the reference loop")
+    ap.add_argument("--builder", default="host", choices=["host", "gpu"],
+                    help="BVH builder: host binned SAH (default) or the GPU LBVH build")
     ap.add_argument("--ply", default=None, help="render this PLY mesh (normalised, SURVEY §8d) instead of "
                     "the synthetic mesh of the config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -110,6 +112,7 @@ def main():
         args.traversal = "linear"
     args.linear = args.traversal == "linear"
     rt.setTraversal(args.traversal)
+    rt.setBuilder(args.builder)
     mesh_info = {}
     if args.ply and kernel == pt.RayTracer.KERNEL_TRIS:
         t0 = time.time()
@@ -227,7 +230,7 @@ def main():
     # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
     # when they were taken on this exact workload and kernel variant
     tp = ROOT / "profiles" / "pmc_traffic.json"
-    workload = workload_name(cfg, n_tris, W, H, sr, args.traversal)
+    workload = workload_name(cfg, n_tris, W, H, sr, args.traversal, args.builder)
     if tp.exists() and kernel == pt.RayTracer.KERNEL_TRIS and not args.linear and n_ranks == 1:
         t = json.loads(tp.read_text())
         if t.get("workload") == workload:
@@ -270,7 +273,12 @@ TRAVERSAL_NAMES = {"bvh": "4-wide compressed BVH", "bvh4f": "4-wide BVH", "bvh2"
                    "packet": "4-wide BVH, wave-coherent"}
 
 
-def workload_name(cfg, n_tris, W, H, sr, traversal):
+def workload_name(cfg, n_tris, W, H, sr, traversal, builder="host"):
+    name = _workload_name(cfg, n_tris, W, H, sr, traversal)
+    return name + (" (GPU-built BVH)" if (builder == "gpu" and n_tris) else "")
+
+
+def _workload_name(cfg, n_tris, W, H, sr, traversal):
     if n_tris and cfg.startswith("PLY "):
         return (f"raytrace_tris {cfg[4:]} ({n_tris} tris, normalised), {W}x{H}, sampleRate {sr} "
                 f"({sr * sr} spp, one launch), maxDepth 6, {TRAVERSAL_NAMES[traversal]} traversal")

@@ -107,7 +107,14 @@ typedef struct rt_mesh_stats {
     uint32_t n_nodes4, depth4; /* 4-wide tree */
     uint32_t stack4;           /* worst-case traversal stack of the 4-wide tree */
     double build_seconds;
+    uint32_t builder; /* RT_BUILD_HOST or RT_BUILD_GPU */
 } rt_mesh_stats;
+/* BVH builder used by the next rt_set_mesh: the host binned-SAH build (default: the best
+   trees) or the GPU build (LBVH over Morton codes, collapsed on the device: seconds-to-
+   milliseconds for large meshes, somewhat slower traversal; no binary-tree layout, so
+   RT_TRAVERSAL_BVH2 is refused on its meshes).  Results are identical either way. */
+enum { RT_BUILD_HOST = 0, RT_BUILD_GPU = 1 };
+int rt_set_builder(rt_ctx *ctx, int builder);
 int rt_mesh_info(const rt_ctx *ctx, rt_mesh_stats *out);
 
 /* ---- camera: RayTracer::setCameraMatrix / setCameraSpherical / setFoVAngle

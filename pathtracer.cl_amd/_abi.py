@@ -39,6 +39,9 @@ RT_TRAVERSAL_BVH2 = 2
 RT_TRAVERSAL_PACKET = 3
 RT_TRAVERSAL_BVH4F = 4
 
+RT_BUILD_HOST = 0
+RT_BUILD_GPU = 1
+
 RT_OUT_DEVICE = 1
 RT_SEEDS_HALO = 2
 
@@ -86,7 +89,7 @@ class RtTile(ctypes.Structure):
 class RtMeshStats(ctypes.Structure):
     _fields_ = [("n_tris", ctypes.c_uint32), ("n_nodes2", ctypes.c_uint32), ("depth2", ctypes.c_uint32),
                 ("n_nodes4", ctypes.c_uint32), ("depth4", ctypes.c_uint32), ("stack4", ctypes.c_uint32),
-                ("build_seconds", ctypes.c_double)]
+                ("build_seconds", ctypes.c_double), ("builder", ctypes.c_uint32)]
 
 
 class RtCounters(ctypes.Structure):
@@ -117,6 +120,7 @@ SIGNATURES = {
     "rt_camera_spherical": (_i32, [_f32, _f32, _f32, _f32, _f32, _f32, _f32, _u32, _vp]),
     "rt_set_params": (_i32, [_vp, _u32, _u32]),
     "rt_set_traversal": (_i32, [_vp, _i32]),
+    "rt_set_builder": (_i32, [_vp, _i32]),
     "rt_set_ndrange": (_i32, [_vp, _u32]),
     "rt_set_seed_layout": (_i32, [_vp, _u32, _u32]),
     "rt_set_seeds": (_i32, [_vp, _vp, _sz]),

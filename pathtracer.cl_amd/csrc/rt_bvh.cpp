@@ -208,10 +208,8 @@ int32_t leaf_code(uint32_t first, uint32_t count) { return ~(int32_t)((first << 
 
 } // namespace
 
-bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtBvh &out,
-                  std::string &err)
+bool rt_validate_mesh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, std::string &err)
 {
-    const auto t0 = std::chrono::steady_clock::now();
     if (!verts || !idx || n_tris == 0 || n_verts == 0) {
         err = "empty mesh";
         return false;
@@ -232,6 +230,14 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
             return false;
         }
     }
+    return true;
+}
+
+bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtBvh &out,
+                  std::string &err)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!rt_validate_mesh(verts, n_verts, idx, n_tris, err)) return false;
 
     Builder b;
     b.verts = verts;

@@ -94,6 +94,8 @@ struct rt_ctx {
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
     uint32_t fetch_k = 16;
+    int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
+    int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
     size_t spill_entries = 0;
 
@@ -474,10 +476,38 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
 {
     if (!c || !verts || !idx || !n_verts || !n_tris) return fail(c, RT_ERR_ARG, "empty mesh");
     HIPCHK(c, hipSetDevice(c->device));
-    RtBvh b;
     std::string err;
+    if (c->builder == RT_BUILD_GPU) {
+        if (!rt_validate_mesh(verts, n_verts, idx, n_tris, err)) return fail(c, RT_ERR_ARG, err);
+        free_dev(c->d_nodes);
+        free_dev(c->d_nodes4);
+        free_dev(c->d_nodes4q);
+        free_dev(c->d_tris);
+        c->d_nodes = c->d_nodes4 = c->d_tris = nullptr;
+        c->d_nodes4q = nullptr;
+        c->n_tris = 0;
+        RtGpuBvh g;
+        const int e = rt_build_bvh_gpu(verts, n_verts, idx, n_tris, g, err, c->stream);
+        c->d_nodes4 = g.nodes4;
+        c->d_nodes4q = g.nodes4q;
+        c->d_tris = g.tris;
+        if (e) return fail(c, RT_ERR_HIP, "GPU BVH build: " + err);
+        c->n_tris = n_tris;
+        c->mesh_serial++;
+        c->bvh.n_nodes = 0; /* no binary layout */
+        c->bvh.n_leaves = 0;
+        c->bvh.depth = 0;
+        c->bvh.n_nodes4 = g.n_nodes4;
+        c->bvh.depth4 = g.depth4;
+        c->bvh.stack4 = g.stack4;
+        c->bvh.build_seconds = g.build_seconds;
+        c->mesh_builder = RT_BUILD_GPU;
+        return RT_OK;
+    }
+    RtBvh b;
     if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
+    c->mesh_builder = RT_BUILD_HOST;
     free_dev(c->d_nodes);
     free_dev(c->d_nodes4);
     free_dev(c->d_nodes4q);
@@ -515,6 +545,7 @@ int rt_mesh_info(const rt_ctx *c, rt_mesh_stats *out)
     out->n_nodes4 = c->bvh.n_nodes4;
     out->depth4 = c->bvh.depth4;
     out->stack4 = c->bvh.stack4;
+    out->builder = (uint32_t)c->mesh_builder;
     out->build_seconds = c->bvh.build_seconds;
     return RT_OK;
 }
@@ -572,6 +603,13 @@ int rt_set_params(rt_ctx *c, uint32_t sample_rate, uint32_t max_depth)
     if (sample_rate > 4096) return fail(c, RT_ERR_ARG, "sample rate too large");
     c->sample_rate = sample_rate;
     c->max_depth = max_depth;
+    return RT_OK;
+}
+
+int rt_set_builder(rt_ctx *c, int builder)
+{
+    if (!c || (builder != RT_BUILD_HOST && builder != RT_BUILD_GPU)) return RT_ERR_ARG;
+    c->builder = builder;
     return RT_OK;
 }
 
@@ -664,6 +702,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                     "a tile need the seed-row halo (rt_pack_seed_rows / rt_unpack_seed_rows, flag RT_SEEDS_HALO)");
     if (kernel == RT_KERNEL_TRIS && c->n_tris == 0) return fail(c, RT_ERR_NO_MESH, "no mesh set");
     if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
+    if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && !c->d_nodes)
+        return fail(c, RT_ERR_STATE, "the GPU builder produces no binary tree: use a 4-wide traversal");
     if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && c->bvh.depth > RT_STACK_DEPTH)
         return fail(c, RT_ERR_LIMIT, "binary BVH deeper than the traversal stack");
     if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_PACKET && c->bvh.stack4 > 64)

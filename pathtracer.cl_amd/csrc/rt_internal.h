@@ -67,6 +67,21 @@ struct RtBvh {
 bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtBvh &out,
                   std::string &err);
 
+/* GPU build (rt_build_gpu.hip): LBVH over 63-bit Morton codes collapsed to the 4-wide
+   layouts; device buffers owned by the caller afterwards (hipFree).  No binary-tree
+   layout is produced.  Returns a hipError_t as int (or -1), err set. */
+struct RtGpuBvh {
+    float *nodes4 = nullptr;     /* 32 floats per node */
+    uint32_t *nodes4q = nullptr; /* 16 dwords per node */
+    float *tris = nullptr;       /* 12 floats per triangle, leaf order */
+    uint32_t n_nodes4 = 0, depth4 = 0, stack4 = 0;
+    double build_seconds = 0.0;
+};
+int rt_build_bvh_gpu(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtGpuBvh &out,
+                     std::string &err, void *stream);
+/* Input checks shared by both builders (finite coordinates, indices in range, size limit). */
+bool rt_validate_mesh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, std::string &err);
+
 /* ---- kernel launchers (rt_kernels.hip) ---- */
 struct RtTriLaunch {
     float *out;

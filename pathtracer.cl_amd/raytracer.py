@@ -108,6 +108,11 @@ class RayTracer:
              "packet": _abi.RT_TRAVERSAL_PACKET, "bvh4f": _abi.RT_TRAVERSAL_BVH4F}[linear]
         self._check(self._lib.rt_set_traversal(self._h, t), "rt_set_traversal")
 
+    def setBuilder(self, builder: str) -> None:
+        """BVH builder for the next setMesh: "host" (binned SAH, default) or "gpu" (LBVH on the device)."""
+        b = {"host": _abi.RT_BUILD_HOST, "gpu": _abi.RT_BUILD_GPU}[builder]
+        self._check(self._lib.rt_set_builder(self._h, b), "rt_set_builder")
+
     def setNDRange(self, nd_y: int) -> None:
         """Work-group height of the reference launch (fixes the padded seed height)."""
         self._check(self._lib.rt_set_ndrange(self._h, int(nd_y)), "rt_set_ndrange")

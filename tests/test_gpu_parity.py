@@ -443,3 +443,82 @@ def test_ply_mesh_cli_and_oracle(tracer, pt, oracle, tmp_path):
     oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, 1, 6, 0, seeds, v, i)
     np.testing.assert_array_equal(bits(got_py), bits(exp))
     np.testing.assert_array_equal(bits(got_cli), bits(exp))
+
+
+# ---- GPU BVH builder (csrc/rt_build_gpu.hip) ----------------------------------------------
+
+@pytest.mark.parametrize("trav", ["bvh", "bvh4f", "packet"])
+@pytest.mark.parametrize("name", TRI_CASES)
+def test_gpu_builder_golden_tris(name, trav, pt, golden, golden_meta):
+    """Frames from a GPU-built tree equal the reference kernel's (golden fixtures)."""
+    g, m = golden(name), golden_meta["cases"][name]
+    rt = pt.RayTracer(0)
+    rt.setBuilder("gpu")
+    _setup(rt, pt, g, m, kernel_tris=True)
+    assert rt.meshInfo()["builder"] == pt._abi.RT_BUILD_GPU
+    rt.setTraversal(trav)
+    out = np.zeros(m["W"] * m["H"] * 4, np.float32)
+    for p in range(m["frames"]):
+        rt.rayTrace(out, m["W"], m["H"], p, kernel=2)
+        np.testing.assert_array_equal(bits(out), bits(g["frames"][p]), err_msg=f"{name} frame {p}")
+    np.testing.assert_array_equal(rt.getSeeds(), g["seeds_out"])
+    rt.setTraversal("bvh2")
+    with pytest.raises(pt.RtError):
+        rt.rayTrace(out, m["W"], m["H"], 0, kernel=2)
+    rt.close()
+
+
+def _query_sets(pt, verts, n=16384, seed=5):
+    sc = pt.scenes
+    cam = sc.camera_spherical(320, **sc.PLY_CAMERA)
+    rays = sc.camera_rays(cam, 320, 180)
+    rng = np.random.default_rng(seed)
+    lo, hi = verts.min(0) - 1.0, verts.max(0) + 1.0
+    rr = np.zeros(n, pt._abi.RAY_DTYPE)
+    rr["o"] = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    rr["d"] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rr["tmin"] = np.float32(1e-4)
+    rr["tmax"] = np.float32(np.inf)
+    rs = rr.copy()
+    rs["tmax"] = rng.uniform(0.0, 8.0, n).astype(np.float32)
+    return rays, rr, rs
+
+
+@pytest.mark.parametrize("case", ["dragon", "tiny1", "tiny2", "tiny7", "duplicates"])
+def test_gpu_builder_equals_linear(case, pt):
+    """Closest-hit index + t and any-hit flags from the GPU-built tree equal the linear loop
+    (dragon class; 1/2/7-triangle meshes; many triangles with one centroid = equal Morton codes)."""
+    sc = pt.scenes
+    if case == "dragon":
+        verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    elif case.startswith("tiny"):
+        verts, idx = sc.make_mesh(200)
+        idx = idx[: int(case[4:])]
+    else:
+        rng = np.random.default_rng(2)
+        nt = 5000
+        # vertices a, -a and a point inside their box: every box centre (the Morton
+        # centroid) is the origin, so all codes are equal
+        a = rng.uniform(-2, 2, (nt, 3)).astype(np.float32)
+        c = (a * rng.uniform(-0.9, 0.9, (nt, 3))).astype(np.float32)
+        verts = np.stack([a, -a, c], axis=1).reshape(-1, 3)
+        idx = np.arange(nt * 3, dtype=np.int32).reshape(nt, 3)
+    rays, rr, rs = _query_sets(pt, verts)
+    res = {}
+    for builder, trav in [("host", "linear"), ("gpu", "bvh"), ("gpu", "bvh4f"), ("gpu", "packet")]:
+        rt = pt.RayTracer(0)
+        rt.setBuilder(builder)
+        rt.setMesh(verts, idx)
+        rt.setTraversal(trav)
+        res[(builder, trav)] = (rt.traceRays(rays), rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
+        if builder == "gpu":
+            info = rt.meshInfo()
+            assert info["builder"] == pt._abi.RT_BUILD_GPU and info["n_nodes4"] >= 1
+        rt.close()
+    ref = res[("host", "linear")]
+    for key, got in res.items():
+        for k in range(3):
+            np.testing.assert_array_equal(got[k][0], ref[k][0], err_msg=f"{case} {key} set {k}")
+            if k < 2:
+                np.testing.assert_array_equal(bits(got[k][1]), bits(ref[k][1]), err_msg=f"{case} {key} t {k}")

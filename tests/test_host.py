@@ -32,10 +32,13 @@ def test_library_exports_every_declared_symbol(pt):
 
 
 def test_library_is_gfx950_code_object(pt):
-    """The fat binary embeds a gfx950 (and only gfx950) device code object."""
+    """The fat binary embeds a gfx950 (and only gfx950) device code object.  (Bare arch names
+    such as "gfx942" do occur as host-side strings: rocPRIM's target-architecture table.)"""
+    import re as _re
+
     data = pt._abi.LIB_PATH.read_bytes()
-    assert b"amdgcn-amd-amdhsa--gfx950" in data
-    assert b"gfx942" not in data and b"gfx90a" not in data
+    targets = set(_re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", data))
+    assert targets == {b"gfx950"}
 
 
 def test_struct_layouts_match_reference(pt):

@@ -8,9 +8,12 @@
  *   rt_render [--scene main|ply] [--width W] [--height H] [--frames F]
  *             [--sample-rate S] [--depth D] [--mesh N_TRIS | --ply FILE] [--linear]
  *             [--raw out.f32] [--pfm out.pfm] [--device K]
+ *             [--events d,d,l,d,m:5:-3,s:64:32,d,...]   (interactive replay: ProgressiveViewHIP
+ *              display / arrow keys l r u n / drag motion / reshape, GlutCLWindow.cpp:136-301)
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -18,6 +21,7 @@
 #include <string>
 #include <vector>
 
+#include "ProgressiveViewHIP.hpp"
 #include "RayTracerHIP.hpp"
 
 namespace {
@@ -88,7 +92,7 @@ int usage()
 
 int main(int argc, char **argv)
 {
-    std::string scene = "main", raw, pfm, ply_path;
+    std::string scene = "main", raw, pfm, ply_path, events;
     unsigned W = 512, H = 512, frames = 1, sr = 1, depth = 6, n_tris = 0;
     int device = 0;
     bool linear = false;
@@ -109,6 +113,7 @@ int main(int argc, char **argv)
         else if (a == "--depth") depth = (unsigned)std::atoi(v);
         else if (a == "--mesh") n_tris = (unsigned)std::atoi(v);
         else if (a == "--ply") ply_path = v;
+        else if (a == "--events") events = v;
         else if (a == "--raw") raw = v;
         else if (a == "--pfm") pfm = v;
         else if (a == "--device") device = std::atoi(v);
@@ -146,6 +151,37 @@ int main(int argc, char **argv)
             rt.setMesh(v.data(), (unsigned)(v.size() / 3), idx.data(), n_tris);
             rt.setTraversal(linear ? RT_TRAVERSAL_LINEAR : RT_TRAVERSAL_BVH);
             kernel = RT_KERNEL_TRIS;
+        }
+        if (!events.empty()) { /* interactive replay through the display state machine */
+            ProgressiveViewHIP view(rt, W, H, kernel);
+            size_t pos = 0;
+            while (pos <= events.size()) {
+                const size_t end = std::min(events.find(',', pos), events.size());
+                const std::string ev = events.substr(pos, end - pos);
+                pos = end + 1;
+                if (ev.empty()) continue;
+                if (ev == "d") view.display();
+                else if (ev == "l") view.specialKey(ProgressiveViewHIP::KEY_LEFT);
+                else if (ev == "r") view.specialKey(ProgressiveViewHIP::KEY_RIGHT);
+                else if (ev == "u") view.specialKey(ProgressiveViewHIP::KEY_UP);
+                else if (ev == "n") view.specialKey(ProgressiveViewHIP::KEY_DOWN);
+                else if (ev[0] == 'm' || ev[0] == 's') {
+                    int a1 = 0, a2 = 0;
+                    if (std::sscanf(ev.c_str() + 1, ":%d:%d", &a1, &a2) != 2) return usage();
+                    if (ev[0] == 'm') view.motion(a1, a2);
+                    else view.reshape((unsigned)a1, (unsigned)a2);
+                } else return usage();
+            }
+            std::printf("{\"progression\": %u, \"azimuth\": %.9g, \"elevation\": %.9g, \"width\": %u, "
+                        "\"height\": %u}\n",
+                        view.progression(), view.azimuth(), view.elevation(), view.width(), view.height());
+            if (!raw.empty()) {
+                FILE *f = std::fopen(raw.c_str(), "wb");
+                const std::vector<float> &px = view.pixels();
+                if (!f || std::fwrite(px.data(), 4, px.size(), f) != px.size()) return 1;
+                std::fclose(f);
+            }
+            return 0;
         }
         float *dbuf = nullptr;
         if (hipMalloc(&dbuf, (size_t)W * H * 16) != hipSuccess) return 1;

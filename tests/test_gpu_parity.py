@@ -522,3 +522,70 @@ def test_gpu_builder_equals_linear(case, pt):
             np.testing.assert_array_equal(got[k][0], ref[k][0], err_msg=f"{case} {key} set {k}")
             if k < 2:
                 np.testing.assert_array_equal(bits(got[k][1]), bits(ref[k][1]), err_msg=f"{case} {key} t {k}")
+
+
+def test_interactive_view_replay(tracer, pt, tmp_path):
+    """ProgressiveViewHIP (GlutCLWindow.cpp:136-301 without GL) driven through the C++ CLI by
+    display / arrow-key / drag / reshape events equals the same event sequence replayed on the
+    Python RayTracer with the window's state machine written out: progression resets on every
+    camera change and on reshape, orbit about (0,-4,0) from azimuth 105 / elevation 40."""
+    import subprocess
+
+    from conftest import ROOT
+
+    events = "d,d,d,l,d,d,m:7:-4,d,u,u,d,s:48:40,d,d,n,d,r,d,m:-400:90,d"
+    raw = tmp_path / "view.f32"
+    res = subprocess.run([str(ROOT / "pathtracer.cl_amd" / "rt_render"), "--scene", "main", "--width", "64",
+                          "--height", "48", "--events", events, "--raw", str(raw)], check=True, timeout=120,
+                         capture_output=True, text=True)
+    import json
+
+    state = json.loads(res.stdout.strip().splitlines()[-1])
+    got = np.fromfile(raw, np.float32)
+
+    sc = pt.scenes
+    f32 = np.float32
+    rt = pt.RayTracer(0)
+    rt.setSpheres(sc.main_scene())
+    rt.setSampleRate(1)
+    rt.setMaxPathDepth(6)
+    rt.setCameraSpherical((0.0, -4.0, 0.0), 14.0, 118.0, 5.0)  # main.cpp:127-128
+    az, el, dist = f32(105.0), f32(40.0), f32(5.0)
+    W, H, prog, realloc, buf = 64, 48, 0, True, None
+
+    def orbit():
+        rt.setCameraSpherical((0.0, -4.0, 0.0), float(el), float(az), float(dist))
+
+    for ev in events.split(","):
+        if ev == "d":
+            if realloc:
+                buf = np.zeros(W * H * 4, np.float32)
+                prog, realloc = 0, False
+                rt.rayTrace(buf, W, H, prog, kernel=0)
+            elif prog < 10000:
+                prog += 1
+                rt.rayTrace(buf, W, H, prog, kernel=0)
+        elif ev in "lrun":
+            if ev == "l":
+                az = np.fmod(f32(az + f32(3.0)), f32(360.0))
+            elif ev == "r":
+                az = np.fmod(f32(az - f32(3.0)), f32(360.0))
+            elif ev == "u":
+                el = min(f32(el + f32(3.0)), f32(90.0))
+            else:
+                el = max(f32(el - f32(3.0)), f32(10.0))
+            orbit()
+            prog = 0
+        elif ev[0] == "m":
+            dx, dy = map(int, ev[2:].split(":"))
+            az = np.fmod(f32(az + f32(dx)), f32(360.0))
+            el = max(min(f32(el + f32(dy)), f32(90.0)), f32(10.0))
+            orbit()
+            prog = 0
+        else:
+            W, H = map(int, ev[2:].split(":"))
+            realloc = True
+    rt.close()
+    assert (state["progression"], state["width"], state["height"]) == (prog, W, H)
+    assert np.float32(state["azimuth"]) == az and np.float32(state["elevation"]) == el
+    np.testing.assert_array_equal(bits(got), bits(buf))

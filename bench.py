@@ -32,8 +32,10 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-NODE_BYTES = {"bvh": 56, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h
-TRI_BYTES = 40   # bytes read per triangle test: v0+orig (16), e1 (12), e2 (12) of the 48-B record, csrc/rt_internal.h
+NODE_BYTES = {"bvh": 48, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
+# bytes read per triangle test: the whole 48-B record (one-record steps of the compressed traversal), else
+# v0+orig (16), e1 (12), e2 (12); csrc/rt_internal.h
+TRI_BYTES = {"bvh": 48, "bvh4f": 40, "bvh2": 40, "linear": 40, "packet": 48}
 PIXEL_BYTES = 16 + 8 + 8  # RGBA32F store + seed read + seed write per pixel
 
 
@@ -213,7 +215,7 @@ def main():
     rays_cnt = cnt["rays_closest"] + cnt["rays_shadow"]
     pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0)) if n_ranks > 1 else H)
     if kernel == pt.RayTracer.KERNEL_TRIS:
-        alg_bytes = cnt["nodes_visited"] * NODE_BYTES[args.traversal] + cnt["tris_tested"] * TRI_BYTES + pix * PIXEL_BYTES
+        alg_bytes = cnt["nodes_visited"] * NODE_BYTES[args.traversal] + cnt["tris_tested"] * TRI_BYTES[args.traversal] + pix * PIXEL_BYTES
     else:
         alg_bytes = pix * PIXEL_BYTES
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
@@ -226,6 +228,9 @@ def main():
     if cnt.get("lane_slots"):
         # share of lanes doing a node or leaf step per traversal round (resumable BVH queries)
         roofline["simd_efficiency"] = round((cnt["nodes_visited"] + cnt["leaves_visited"]) / cnt["lane_slots"], 4)
+    if cnt.get("clocks_total"):
+        # share of the waves' time spent in traversal rounds (counting launch, s_memtime)
+        roofline["traversal_time_frac"] = round(cnt["clocks_traversal"] / cnt["clocks_total"], 4)
 
     # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
     # when they were taken on this exact workload and kernel variant

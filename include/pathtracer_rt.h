@@ -85,6 +85,8 @@ typedef struct rt_counters {
     uint64_t leaves_visited; /* BVH leaves entered (counting launches only) */
     uint64_t lane_slots;     /* lanes x traversal-step rounds of the resumable (BVH) queries: SIMD
                                 efficiency = (nodes_visited + leaves_visited) / lane_slots */
+    uint64_t clocks_traversal; /* shader clocks waves spent in traversal rounds, summed over waves */
+    uint64_t clocks_total;     /* shader clocks of the waves' whole lifetimes, summed over waves */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */

@@ -100,6 +100,8 @@ class RtCounters(ctypes.Structure):
         ("tris_tested", ctypes.c_uint64),
         ("leaves_visited", ctypes.c_uint64),
         ("lane_slots", ctypes.c_uint64),
+        ("clocks_traversal", ctypes.c_uint64),
+        ("clocks_total", ctypes.c_uint64),
     ]
 
 

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "rt_internal.h"
+#include "rt_quant.h"
 
 #pragma clang fp contract(off)
 
@@ -224,7 +225,8 @@ __global__ void k_collapse(const Frontier *__restrict__ cur, const uint32_t *__r
                            uint32_t *__restrict__ max_stack, const int2 *__restrict__ child,
                            const int2 *__restrict__ range, const float *__restrict__ nbox,
                            const float *__restrict__ tbox, const uint32_t *__restrict__ perm, int n,
-                           float *__restrict__ nodes4)
+                           float *__restrict__ nodes4, uint32_t *__restrict__ n_tris_out,
+                           uint32_t *__restrict__ perm2)
 {
     const uint32_t e = blockIdx.x * kB + threadIdx.x;
     if (e >= *n_cur) return;
@@ -257,36 +259,49 @@ __global__ void k_collapse(const Frontier *__restrict__ cur, const uint32_t *__r
     }
     const int stk = f.stack + (nk > 0 ? nk - 1 : 0);
     atomicMax(max_stack, (uint32_t)stk);
+    /* inner children get consecutive node indices, leaf children consecutive
+       triangle slots (rt_quant.h), allocated as one block each */
+    int n_in = 0;
+    uint32_t n_leaf_tris = 0;
+    for (int k = 0; k < nk; ++k) {
+        const int c = kids[k];
+        if (c >= 0 && n >= 2 && expandable(c)) ++n_in;
+        else n_leaf_tris += (c < 0 && n >= 2) ? 1u : (n >= 2 && c >= 0 ? (uint32_t)size_of(c) : (uint32_t)n);
+    }
+    const uint32_t node_base = n_in ? atomicAdd(n_nodes, (uint32_t)n_in) : 0u;
+    const uint32_t tri_base = n_leaf_tris ? atomicAdd(n_tris_out, n_leaf_tris) : 0u;
+    uint32_t next_node = node_base, next_tri = tri_base;
     float *nd = nodes4 + 32ull * f.out;
     for (int k = 0; k < 4; ++k) {
         int32_t code = RT_EMPTY_CHILD;
         float b[6] = {0, 0, 0, 0, 0, 0};
         if (k < nk) {
             const int c = kids[k];
-            if (c < 0 && n >= 2) { /* a single triangle */
-                const int s = ~c;
-                for (int a = 0; a < 6; ++a) b[a] = tbox[6ull * perm[s] + a];
-                code = ~(int32_t)(((uint32_t)s << 3) | 0u);
-            } else if (c < 0 || n < 2 || !expandable(c)) { /* a small subtree: leaf over its slot range */
-                uint32_t first = 0, count = (uint32_t)n;
-                if (n >= 2 && c >= 0) {
-                    first = (uint32_t)range[c].x;
-                    count = (uint32_t)(range[c].y - range[c].x + 1);
-                    for (int a = 0; a < 6; ++a) b[a] = nbox[6ull * c + a];
-                } else { /* whole mesh of <= kLeafMax triangles */
-                    if (n >= 2) {
-                        for (int a = 0; a < 6; ++a) b[a] = nbox[a];
-                    } else {
-                        for (int a = 0; a < 6; ++a) b[a] = tbox[6ull * perm[0] + a];
-                    }
-                }
-                code = ~(int32_t)((first << 3) | (count - 1));
-            } else {
+            if (c >= 0 && n >= 2 && expandable(c)) {
                 for (int a = 0; a < 6; ++a) b[a] = nbox[6ull * c + a];
-                const uint32_t id = atomicAdd(n_nodes, 1u);
+                const uint32_t id = next_node++;
                 code = (int32_t)id;
                 const uint32_t q = atomicAdd(n_next, 1u);
                 next[q] = Frontier{c, (int)id, stk};
+            } else {
+                /* a leaf: one triangle (binary leaf), a small subtree's slot range, or
+                   the whole mesh of <= kLeafMax triangles */
+                uint32_t first_old = 0, count = (uint32_t)n;
+                if (c < 0 && n >= 2) {
+                    first_old = (uint32_t)(~c);
+                    count = 1;
+                    for (int a = 0; a < 6; ++a) b[a] = tbox[6ull * perm[first_old] + a];
+                } else if (n >= 2) {
+                    first_old = (uint32_t)range[c].x;
+                    count = (uint32_t)(range[c].y - range[c].x + 1);
+                    for (int a = 0; a < 6; ++a) b[a] = nbox[6ull * c + a];
+                } else {
+                    for (int a = 0; a < 6; ++a) b[a] = tbox[6ull * perm[0] + a];
+                }
+                const uint32_t first = next_tri;
+                next_tri += count;
+                for (uint32_t q = 0; q < count; ++q) perm2[first + q] = first_old + q;
+                code = ~(int32_t)((first << 3) | (count - 1));
             }
         }
         nd[0 + k] = b[0];
@@ -300,73 +315,24 @@ __global__ void k_collapse(const Frontier *__restrict__ cur, const uint32_t *__r
     }
 }
 
-/* 6a. quantisation (the rule of rt_bvh.cpp, in binary64) */
-__global__ void k_quantize(const float *__restrict__ nodes4, uint32_t n_nodes, uint32_t *__restrict__ q4)
+/* 6a. compressed nodes (rt_quant.h, the host builder's encoder); flag = 1 if any
+   node cannot be encoded (the traversal then uses the full-precision nodes) */
+__global__ void k_quantize(const float *__restrict__ nodes4, uint32_t n_nodes, uint32_t *__restrict__ q4,
+                           uint32_t *__restrict__ fail)
 {
     const uint32_t i = blockIdx.x * kB + threadIdx.x;
     if (i >= n_nodes) return;
-    const float *n = nodes4 + 32ull * i;
-    uint32_t *q = q4 + 16ull * i;
-    int32_t code[4];
-    for (int k = 0; k < 4; ++k) code[k] = __float_as_int(n[24 + k]);
-    uint32_t exps = 0, qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-    for (int ax = 0; ax < 3; ++ax) {
-        const float *lo = n + 8 * ax, *hi = n + 8 * ax + 4;
-        float omin = INFINITY, omax = -INFINITY;
-        for (int k = 0; k < 4; ++k)
-            if (code[k] != RT_EMPTY_CHILD) {
-                omin = fminf(omin, lo[k]);
-                omax = fmaxf(omax, hi[k]);
-            }
-        if (!(omin <= omax)) omin = omax = 0.0f;
-        const float origin = omin;
-        int e = -64;
-        const double ext = (double)omax - (double)origin;
-        if (ext > 0) e = max(-64, (int)ceil(log2(ext / 255.0)));
-        for (;; ++e) {
-            const double step = ldexp(1.0, e);
-            bool ok = true;
-            uint32_t wl = 0, wh = 0;
-            for (int k = 0; k < 4; ++k) {
-                int32_t l = 255, h = 0;
-                if (code[k] != RT_EMPTY_CHILD) {
-                    l = (int32_t)floor(((double)lo[k] - origin) / step);
-                    h = (int32_t)ceil(((double)hi[k] - origin) / step);
-                    l = max(l, 0);
-                    if (h > 255) ok = false;
-                    if ((double)origin + l * step > (double)lo[k] || (double)origin + h * step < (double)hi[k])
-                        ok = false;
-                }
-                wl |= (uint32_t)l << (8 * k);
-                wh |= (uint32_t)(h & 255) << (8 * k);
-            }
-            if (ok) {
-                qlo[ax] = wl;
-                qhi[ax] = wh;
-                break;
-            }
-        }
-        q[ax] = __float_as_uint(origin);
-        exps |= (uint32_t)(e + 128) << (8 * ax);
-    }
-    q[3] = exps;
-    for (int k = 0; k < 4; ++k) q[4 + k] = (uint32_t)code[k];
-    q[8] = qlo[0];
-    q[9] = qhi[0];
-    q[10] = qlo[1];
-    q[11] = qhi[1];
-    q[12] = qlo[2];
-    q[13] = qhi[2];
-    q[14] = q[15] = 0u;
+    if (!rt_quantize_node4(nodes4 + 32ull * i, q4 + 12ull * i)) atomicOr(fail, 1u);
 }
 
 /* 6b. triangle records in slot order: (v0, orig), (v1 - v0), (v2 - v0) (rtcommon.h:20-37) */
 __global__ void k_tri_records(const float *__restrict__ verts, const int32_t *__restrict__ idx,
-                              const uint32_t *__restrict__ perm, uint32_t n, float *__restrict__ tris)
+                              const uint32_t *__restrict__ perm, const uint32_t *__restrict__ perm2, uint32_t n,
+                              float *__restrict__ tris)
 {
     const uint32_t s = blockIdx.x * kB + threadIdx.x;
     if (s >= n) return;
-    const uint32_t t = perm[s];
+    const uint32_t t = perm[perm2[s]];
     const float *a = verts + 3ull * (uint32_t)idx[3ull * t];
     const float *p1 = verts + 3ull * (uint32_t)idx[3ull * t + 1];
     const float *p2 = verts + 3ull * (uint32_t)idx[3ull * t + 2];
@@ -414,7 +380,7 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
     hipStream_t st = (hipStream_t)stream;
     const int n = (int)n_tris;
     DevBuf d_verts, d_idx, d_tbox, d_cent, d_bounds, d_keys, d_keys2, d_vals, d_perm, d_child, d_range, d_pin,
-        d_pleaf, d_nbox, d_flags, d_front[2], d_counts, d_tmp;
+        d_pleaf, d_nbox, d_flags, d_front[2], d_counts, d_tmp, d_perm2;
     GCHK(hipMalloc(&d_verts.p, 12ull * n_verts));
     GCHK(hipMalloc(&d_idx.p, 12ull * n_tris));
     GCHK(hipMemcpyAsync(d_verts.p, verts_h, 12ull * n_verts, hipMemcpyHostToDevice, st));
@@ -470,7 +436,9 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
     GCHK(hipMalloc(&d_front[0].p, sizeof(Frontier) * cap4));
     GCHK(hipMalloc(&d_front[1].p, sizeof(Frontier) * cap4));
     GCHK(hipMalloc(&d_counts.p, 8 * sizeof(uint32_t)));
-    /* counts: [0] frontier A size, [1] frontier B size, [2] nodes, [3] max stack */
+    GCHK(hipMalloc(&d_perm2.p, 4ull * n_tris));
+    /* counts: [0] frontier A size, [1] frontier B size, [2] nodes, [3] max stack,
+       [4] triangle slots handed out, [5] quantisation failure flag */
     const Frontier root = {n >= 2 ? 0 : ~0, 0, 0};
     GCHK(hipMemcpyAsync(d_front[0].p, &root, sizeof(root), hipMemcpyHostToDevice, st));
     const uint32_t init_counts[8] = {1u, 0u, 1u, 0u, 0u, 0u, 0u, 0u};
@@ -484,7 +452,8 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
         hipLaunchKernelGGL(k_collapse, dim3(blocks_for(level_size)), dim3(kB), 0, st,
                            (const Frontier *)d_front[cur].p, cnt + cur, (Frontier *)d_front[1 - cur].p,
                            cnt + (1 - cur), cnt + 2, cnt + 3, (const int2 *)d_child.p, (const int2 *)d_range.p,
-                           (const float *)d_nbox.p, (const float *)d_tbox.p, (const uint32_t *)d_perm.p, n, nodes4);
+                           (const float *)d_nbox.p, (const float *)d_tbox.p, (const uint32_t *)d_perm.p, n, nodes4,
+                           cnt + 4, (uint32_t *)d_perm2.p);
         GCHK(hipGetLastError());
         GCHK(hipMemcpyAsync(&level_size, cnt + (1 - cur), sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         GCHK(hipStreamSynchronize(st));
@@ -501,19 +470,30 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
     out.depth4 = depth;
     out.stack4 = counts[3];
 
+    if (counts[4] != n_tris) {
+        err = "GPU BVH collapse lost triangles";
+        return -1;
+    }
     uint32_t *q4 = nullptr;
-    GCHK(hipMalloc(&q4, 64ull * out.n_nodes4));
+    GCHK(hipMalloc(&q4, 48ull * out.n_nodes4));
     out.nodes4q = q4;
     hipLaunchKernelGGL(k_quantize, dim3(blocks_for(out.n_nodes4)), dim3(kB), 0, st, (const float *)nodes4,
-                       out.n_nodes4, q4);
+                       out.n_nodes4, q4, cnt + 5);
     GCHK(hipGetLastError());
     float *tris = nullptr;
     GCHK(hipMalloc(&tris, 48ull * n_tris));
     out.tris = tris;
     hipLaunchKernelGGL(k_tri_records, dim3(blocks_for(n_tris)), dim3(kB), 0, st, (const float *)d_verts.p,
-                       (const int32_t *)d_idx.p, (const uint32_t *)d_perm.p, n_tris, tris);
+                       (const int32_t *)d_idx.p, (const uint32_t *)d_perm.p, (const uint32_t *)d_perm2.p, n_tris,
+                       tris);
     GCHK(hipGetLastError());
+    uint32_t qfail = 0;
+    GCHK(hipMemcpyAsync(&qfail, cnt + 5, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     GCHK(hipStreamSynchronize(st));
+    if (qfail) { /* not encodable: full-precision nodes only */
+        (void)hipFree(q4);
+        out.nodes4q = nullptr;
+    }
     out.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return 0;
 }

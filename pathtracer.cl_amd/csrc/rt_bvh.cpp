@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "rt_internal.h"
+#include "rt_quant.h"
 
 namespace {
 
@@ -426,67 +427,81 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
         }
     }
 
-    /* Compressed copy of the 4-wide tree (64 B per node, see rt_internal.h):
-       child boxes quantised to 8 bits per plane on a per-node power-of-two grid,
-       rounded outward so every dequantised box contains the exact one. */
-    out.nodes4q.assign(16ull * out.n_nodes4, 0u);
-    for (uint32_t i = 0; i < out.n_nodes4; ++i) {
-        const float *n = out.nodes4.data() + 32ull * i;
-        uint32_t *q = out.nodes4q.data() + 16ull * i;
-        int32_t code[4];
-        std::memcpy(code, &n[24], 16);
-        uint32_t exps = 0;
-        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-        for (int ax = 0; ax < 3; ++ax) {
-            const float *lo = n + 8 * ax, *hi = n + 8 * ax + 4;
-            float omin = INFINITY, omax = -INFINITY;
-            for (int k = 0; k < 4; ++k)
-                if (code[k] != RT_EMPTY_CHILD) {
-                    omin = std::min(omin, lo[k]);
-                    omax = std::max(omax, hi[k]);
-                }
-            if (!(omin <= omax)) omin = omax = 0.0f; /* no children (cannot happen) */
-            const float origin = omin;
-            /* smallest grid step 2^e with 255 steps covering the extent (outward-rounded) */
-            int e = -64;
-            const double ext = (double)omax - (double)origin;
-            if (ext > 0) e = std::max(-64, (int)std::ceil(std::log2(ext / 255.0)));
-            for (;; ++e) {
-                const double step = std::ldexp(1.0, e);
-                bool ok = true;
-                uint32_t wl = 0, wh = 0;
-                for (int k = 0; k < 4; ++k) {
-                    int32_t l = 255, h = 0; /* empty slot: inverted box, never entered */
-                    if (code[k] != RT_EMPTY_CHILD) {
-                        l = (int32_t)std::floor(((double)lo[k] - origin) / step);
-                        h = (int32_t)std::ceil(((double)hi[k] - origin) / step);
-                        l = std::max(l, 0);
-                        if (h > 255) ok = false;
-                        /* containment in exact arithmetic */
-                        if ((double)origin + l * step > (double)lo[k] || (double)origin + h * step < (double)hi[k])
-                            ok = false;
-                    }
-                    wl |= (uint32_t)l << (8 * k);
-                    wh |= (uint32_t)(h & 255) << (8 * k);
-                }
-                if (ok) {
-                    qlo[ax] = wl;
-                    qhi[ax] = wh;
-                    break;
+    /* Renumber the 4-wide tree breadth-first with each node's inner children
+       consecutive, and re-lay the triangles so each node's leaf children cover
+       consecutive slots in child order (rt_quant.h); every leaf keeps its triangles
+       contiguous, so the binary tree's leaf codes are remapped, not rebuilt. */
+    {
+        const uint32_t n4 = out.n_nodes4;
+        std::vector<int32_t> new_id(n4, -1), order4;
+        order4.reserve(n4);
+        new_id[0] = 0;
+        order4.push_back(0);
+        for (size_t h = 0; h < order4.size(); ++h) {
+            const float *n = out.nodes4.data() + 32ull * order4[h];
+            for (int k = 0; k < 4; ++k) {
+                int32_t c;
+                std::memcpy(&c, &n[24 + k], 4);
+                if (c != RT_EMPTY_CHILD && c >= 0) {
+                    new_id[c] = (int32_t)order4.size();
+                    order4.push_back(c);
                 }
             }
-            std::memcpy(&q[ax], &origin, 4);
-            exps |= (uint32_t)(e + 128) << (8 * ax);
         }
-        q[3] = exps;
-        std::memcpy(&q[4], code, 16);
-        q[8] = qlo[0];
-        q[9] = qhi[0];
-        q[10] = qlo[1];
-        q[11] = qhi[1];
-        q[12] = qlo[2];
-        q[13] = qhi[2];
+        std::vector<uint32_t> new_first(n_tris, 0u), new_perm(n_tris, 0u);
+        uint32_t cursor = 0;
+        for (size_t h = 0; h < order4.size(); ++h) {
+            const float *n = out.nodes4.data() + 32ull * order4[h];
+            for (int k = 0; k < 4; ++k) {
+                int32_t c;
+                std::memcpy(&c, &n[24 + k], 4);
+                if (c == RT_EMPTY_CHILD || c >= 0) continue;
+                const uint32_t first = (uint32_t)(~c) >> 3, count = ((uint32_t)(~c) & 7u) + 1u;
+                new_first[first] = cursor;
+                for (uint32_t q = 0; q < count; ++q) new_perm[cursor + q] = b.perm[first + q];
+                cursor += count;
+            }
+        }
+        auto remap = [&](float *slot) {
+            int32_t c;
+            std::memcpy(&c, slot, 4);
+            if (c == RT_EMPTY_CHILD) return;
+            if (c >= 0) return;
+            const uint32_t enc = (uint32_t)(~c);
+            c = leaf_code(new_first[enc >> 3], (enc & 7u) + 1u);
+            std::memcpy(slot, &c, 4);
+        };
+        std::vector<float> nodes4(out.nodes4.size());
+        for (uint32_t i = 0; i < n4; ++i) {
+            float *dst = nodes4.data() + 32ull * new_id[i];
+            std::memcpy(dst, out.nodes4.data() + 32ull * i, 32 * sizeof(float));
+            for (int k = 0; k < 4; ++k) {
+                int32_t c;
+                std::memcpy(&c, &dst[24 + k], 4);
+                if (c != RT_EMPTY_CHILD && c >= 0) {
+                    c = new_id[c];
+                    std::memcpy(&dst[24 + k], &c, 4);
+                } else {
+                    remap(&dst[24 + k]);
+                }
+            }
+        }
+        out.nodes4.swap(nodes4);
+        for (uint32_t i = 0; i < out.n_nodes; ++i) {
+            remap(&out.nodes[16ull * i + 12]);
+            remap(&out.nodes[16ull * i + 13]);
+        }
+        b.perm.swap(new_perm);
     }
+
+    /* Compressed copy of the 4-wide tree (48 B per node, rt_quant.h); dropped (the
+       traversal falls back to full-precision nodes) if a node cannot be encoded. */
+    out.nodes4q.assign(12ull * out.n_nodes4, 0u);
+    for (uint32_t i = 0; i < out.n_nodes4; ++i)
+        if (!rt_quantize_node4(out.nodes4.data() + 32ull * i, out.nodes4q.data() + 12ull * i)) {
+            out.nodes4q.clear();
+            break;
+        }
 
     /* Triangles in leaf order: (v0, orig), (e1 = v1 - v0), (e2 = v2 - v0). */
     out.tris.assign(12ull * n_tris, 0.0f);

@@ -125,7 +125,7 @@ struct rt_ctx {
     unsigned long long *d_counters = nullptr;
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
-    rt_counters last = {0, 0, 0, 0, 0, 0};
+    rt_counters last = {0, 0, 0, 0, 0, 0, 0, 0};
     bool have_timing = false;
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
@@ -279,7 +279,7 @@ int trav_kind(const rt_ctx *c)
     if (c->traversal == RT_TRAVERSAL_LINEAR) return RT_TRAV_LINEAR;
     if (c->traversal == RT_TRAVERSAL_BVH2) return RT_TRAV_BVH2;
     if (c->traversal == RT_TRAVERSAL_PACKET) return RT_TRAV_PACKET4;
-    if (c->traversal == RT_TRAVERSAL_BVH4F) return RT_TRAV_BVH4;
+    if (c->traversal == RT_TRAVERSAL_BVH4F || !c->d_nodes4q) return RT_TRAV_BVH4;
     return RT_TRAV_BVH4Q;
 }
 
@@ -517,11 +517,13 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     c->n_tris = 0;
     HIPCHK(c, hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->d_nodes4, b.nodes4.size() * sizeof(float)));
-    HIPCHK(c, hipMalloc(&c->d_nodes4q, b.nodes4q.size() * sizeof(uint32_t)));
+    if (!b.nodes4q.empty()) HIPCHK(c, hipMalloc(&c->d_nodes4q, b.nodes4q.size() * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
     HIPCHK(c, hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->d_nodes4q, b.nodes4q.data(), b.nodes4q.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (!b.nodes4q.empty())
+        HIPCHK(c, hipMemcpy(c->d_nodes4q, b.nodes4q.data(), b.nodes4q.size() * sizeof(uint32_t),
+                            hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_tris, b.tris.data(), b.tris.size() * sizeof(float), hipMemcpyHostToDevice));
     c->n_tris = n_tris;
     c->mesh_serial++;
@@ -845,6 +847,8 @@ int rt_synchronize(rt_ctx *c)
     c->last.tris_tested = h[3];
     c->last.leaves_visited = h[4];
     c->last.lane_slots = h[5];
+    c->last.clocks_traversal = h[6] / 64; /* summed over every lane of a wave */
+    c->last.clocks_total = h[7] / 64;
     return RT_OK;
 }
 

@@ -19,8 +19,9 @@
 #define RT_BVH_MAX_DEPTH (RT_STACK_DEPTH + 1)
 #define RT_BLOCK 256
 #define RT_LEAF_MAX 8
-/* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots */
-#define RT_N_COUNTERS 6
+/* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots,
+   traversal-loop clocks, kernel clocks (the last two: per lane, summed) */
+#define RT_N_COUNTERS 8
 
 /* One BVH node = 4 x float4 = 64 B (both children's boxes in the parent):
      n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
@@ -39,14 +40,9 @@
    RT_EMPTY_CHILD marks an unused slot.  Collapsed from the binary SAH tree
    (largest-area child expanded first). */
 #define RT_EMPTY_CHILD 0x7fffffff
-/* Compressed 4-wide node = 16 dwords = 64 B (two per cache line), same tree:
-     d[0..2] = origin.xyz (float), d[3] = biased exponents (e + 128) of x, y, z in bytes 0..2,
-     d[4..7] = child[0..3] (as above),
-     d[8] = lo.x, d[9] = hi.x, d[10] = lo.y, d[11] = hi.y, d[12] = lo.z, d[13] = hi.z:
-            one byte per child (child k in byte k), plane = origin + q * 2^e,
-     d[14..15] = 0.
-   The quantised box contains the exact child box (floor / ceil); an unused slot
-   has lo = 255 > hi = 0. */
+/* Compressed 4-wide node = 12 dwords = 48 B: see rt_quant.h.  The 4-wide trees are
+   numbered breadth-first with each node's inner children consecutive, and the
+   triangles laid out so each node's leaf children cover consecutive slots. */
 
 struct RtBvh {
     std::vector<float> nodes; /* binary: 16 floats per node */
@@ -55,7 +51,7 @@ struct RtBvh {
     uint32_t n_leaves = 0;
     uint32_t depth = 0;
     std::vector<float> nodes4;     /* 4-wide: 32 floats per node */
-    std::vector<uint32_t> nodes4q; /* 4-wide, compressed: 16 dwords per node */
+    std::vector<uint32_t> nodes4q; /* 4-wide, compressed: 12 dwords per node (empty: not encodable) */
     uint32_t n_nodes4 = 0;
     uint32_t depth4 = 0;
     uint32_t stack4 = 0; /* worst-case traversal stack entries of the 4-wide tree */
@@ -72,7 +68,7 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
    layout is produced.  Returns a hipError_t as int (or -1), err set. */
 struct RtGpuBvh {
     float *nodes4 = nullptr;     /* 32 floats per node */
-    uint32_t *nodes4q = nullptr; /* 16 dwords per node */
+    uint32_t *nodes4q = nullptr; /* 12 dwords per node (nullptr: not encodable) */
     float *tris = nullptr;       /* 12 floats per triangle, leaf order */
     uint32_t n_nodes4 = 0, depth4 = 0, stack4 = 0;
     double build_seconds = 0.0;

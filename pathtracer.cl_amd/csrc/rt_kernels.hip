@@ -18,6 +18,7 @@
 
 #include "rt_device.h"
 #include "rt_internal.h"
+#include "rt_quant.h"
 
 #pragma clang fp contract(off)
 
@@ -177,6 +178,98 @@ __device__ __forceinline__ void trav_begin(TravState &s, Stack &stk, V3 o, V3 d,
     stk.sp = 0;
 }
 
+/* One step of the compressed 4-wide traversal (rt_quant.h).  Every lane fetches
+   exactly one 48-B record per step — a node, or ONE triangle of its current leaf —
+   with the same three dwordx4 loads, so a wave-step costs one memory round trip
+   whatever mix of node and leaf lanes it holds (a leaf of k triangles takes k
+   steps; the leaf cursor is the leaf code itself: first slot and remaining count). */
+template <bool COUNT>
+__device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                            TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
+                                            TravCounts &cnt)
+{
+    const float tmin_c = -1e-3f;
+    const V3 inv = s.inv, oi = s.oi;
+    const int node = s.node;
+    const bool leaf = node < 0;
+    const uint32_t enc = (uint32_t)(~node);
+    const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (enc >> 3)
+                            : reinterpret_cast<const uint4 *>(nodes) + 3 * node;
+    const uint4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+    if (leaf) {
+        if (COUNT) {
+            cnt.tests++;
+            cnt.leaves++;
+        }
+        const float4 a = make_float4(__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z),
+                                     __uint_as_float(q0.w));
+        const float4 b = make_float4(__uint_as_float(q1.x), __uint_as_float(q1.y), __uint_as_float(q1.z), 0.0f);
+        const float4 c = make_float4(__uint_as_float(q2.x), __uint_as_float(q2.y), __uint_as_float(q2.z), 0.0f);
+        float t = 0.0f;
+        bool done = false;
+        const bool h = mt_test(o, d, a, b, c, t);
+        leaf_accept<COUNT>((int)(enc >> 3), a, d, h, t, tmin, s.best_t, any_hit, s.best, s.best_orig, s.best_t, done);
+        if (done) return true;
+        if (enc & 7u) { /* next triangle of this leaf */
+            s.node = ~(int)((((enc >> 3) + 1u) << 3) | ((enc & 7u) - 1u));
+            return false;
+        }
+    } else {
+        if (COUNT) cnt.nodes++;
+        const float tmax_c = t_slack(s.best_t);
+        const uint32_t w = q0.w;
+        const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
+        const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
+        const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
+        const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
+        const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
+        const float bzo = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
+        const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+        const uint32_t nxw = px ? q1.x : q1.y, fxw = px ? q1.y : q1.x;
+        const uint32_t nyw = py ? q1.z : q1.w, fyw = py ? q1.w : q1.z;
+        const uint32_t nzw = pz ? q2.x : q2.y, fzw = pz ? q2.y : q2.x;
+        float t[4];
+        int c[4];
+        int nhit = 0;
+        int leaf_off = 0; /* triangles of the leaf children before child i */
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int sh = 8 * i;
+            const float tn = __builtin_fmaxf(
+                __builtin_fmaxf(__builtin_fmaf((float)((nxw >> sh) & 255u), sx, bx),
+                                __builtin_fmaf((float)((nyw >> sh) & 255u), sy, by)),
+                __builtin_fmaxf(__builtin_fmaf((float)((nzw >> sh) & 255u), sz, bzo), tmin_c));
+            const float tf = __builtin_fminf(
+                __builtin_fminf(__builtin_fmaf((float)((fxw >> sh) & 255u), sx, bx),
+                                __builtin_fmaf((float)((fyw >> sh) & 255u), sy, by)),
+                __builtin_fminf(__builtin_fmaf((float)((fzw >> sh) & 255u), sz, bzo), tmax_c));
+            const bool h = tn <= tf; /* an unused slot's inverted box never passes */
+            const uint32_t m = (w >> (16 + 4 * i)) & 15u;
+            const bool lf = (m & 8u) != 0;
+            const int k = (int)(m & 7u); /* leaf: count - 1; inner: rank */
+            c[i] = lf ? ~((((int)q2.w + leaf_off) << 3) | k) : (int)q2.z + k;
+            leaf_off += lf ? k + 1 : 0;
+            t[i] = h ? tn : kInf;
+            nhit += h ? 1 : 0;
+        }
+        if (nhit > 0) {
+            cas(t[0], c[0], t[1], c[1]);
+            cas(t[2], c[2], t[3], c[3]);
+            cas(t[0], c[0], t[2], c[2]);
+            cas(t[1], c[1], t[3], c[3]);
+            cas(t[1], c[1], t[2], c[2]);
+            if (nhit >= 4) stk.push(c[3]);
+            if (nhit >= 3) stk.push(c[2]);
+            if (nhit >= 2) stk.push(c[1]);
+            s.node = c[0];
+            return false;
+        }
+    }
+    if (stk.sp == 0) return true;
+    s.node = stk.pop();
+    return false;
+}
+
 /* One traversal step; returns true when the query is complete.  Closest hit:
    the result equals the reference's linear loop (minimum t, ties to the highest
    original index — rtcommon.h:39-52 with intersects_triangle's `t > tmax`
@@ -187,6 +280,7 @@ __device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, cons
                                           TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
                                           TravCounts &cnt)
 {
+    if (TRAV == RT_TRAV_BVH4Q) return trav_step_q<COUNT>(nodes, tris, s, stk, o, d, tmin, any_hit, cnt);
     const float tmin_c = -1e-3f;
     const V3 inv = s.inv, oi = s.oi;
     int node = s.node;
@@ -215,57 +309,6 @@ __device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, cons
             }
             if (h0 || h1) {
                 s.node = h0 ? c0 : c1;
-                return false;
-            }
-        } else if (TRAV == RT_TRAV_BVH4Q) {
-            /* compressed 4-wide node (rt_internal.h): per axis, plane t =
-               q * (2^e / d) + (origin - o) / d; near/far planes picked by the
-               direction signs; 56 of the node's 64 B are fetched. */
-            const uint4 *nd = reinterpret_cast<const uint4 *>(nodes) + 4 * node;
-            const uint4 hd = nd[0];
-            const uint4 cc = nd[1];
-            const uint4 bxy = nd[2];
-            const uint2 bz = reinterpret_cast<const uint2 *>(nd)[6];
-            const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(hd.w & 255u) - 128);
-            const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((hd.w >> 8) & 255u) - 128);
-            const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((hd.w >> 16) & 255u) - 128);
-            const float bx = __builtin_fmaf(__uint_as_float(hd.x), inv.x, -oi.x);
-            const float by = __builtin_fmaf(__uint_as_float(hd.y), inv.y, -oi.y);
-            const float bzo = __builtin_fmaf(__uint_as_float(hd.z), inv.z, -oi.z);
-            const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-            const uint32_t nxw = px ? bxy.x : bxy.y, fxw = px ? bxy.y : bxy.x;
-            const uint32_t nyw = py ? bxy.z : bxy.w, fyw = py ? bxy.w : bxy.z;
-            const uint32_t nzw = pz ? bz.x : bz.y, fzw = pz ? bz.y : bz.x;
-            const int cs[4] = {(int)cc.x, (int)cc.y, (int)cc.z, (int)cc.w};
-            float t[4];
-            int c[4];
-            int nhit = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int sh = 8 * i;
-                const float tn = __builtin_fmaxf(
-                    __builtin_fmaxf(__builtin_fmaf((float)((nxw >> sh) & 255u), sx, bx),
-                                    __builtin_fmaf((float)((nyw >> sh) & 255u), sy, by)),
-                    __builtin_fmaxf(__builtin_fmaf((float)((nzw >> sh) & 255u), sz, bzo), tmin_c));
-                const float tf = __builtin_fminf(
-                    __builtin_fminf(__builtin_fmaf((float)((fxw >> sh) & 255u), sx, bx),
-                                    __builtin_fmaf((float)((fyw >> sh) & 255u), sy, by)),
-                    __builtin_fminf(__builtin_fmaf((float)((fzw >> sh) & 255u), sz, bzo), tmax_c));
-                const bool h = (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
-                t[i] = h ? tn : kInf;
-                c[i] = cs[i];
-                nhit += h ? 1 : 0;
-            }
-            if (nhit > 0) {
-                cas(t[0], c[0], t[1], c[1]);
-                cas(t[2], c[2], t[3], c[3]);
-                cas(t[0], c[0], t[2], c[2]);
-                cas(t[1], c[1], t[3], c[3]);
-                cas(t[1], c[1], t[2], c[2]);
-                if (nhit >= 4) stk.push(c[3]);
-                if (nhit >= 3) stk.push(c[2]);
-                if (nhit >= 2) stk.push(c[1]);
-                s.node = c[0];
                 return false;
             }
         } else {
@@ -500,6 +543,14 @@ __device__ __forceinline__ int traverse_packet4(const float4 *__restrict__ nodes
     return best;
 }
 
+/* shader-clock timestamp (s_memtime), counting launches only */
+__device__ __forceinline__ unsigned long long wave_clock()
+{
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -616,7 +667,8 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
     ts.best_t = kInf;
     ts.inv = ro;
     ts.oi = ro;
-    unsigned long long cnt[RT_N_COUNTERS] = {0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[RT_N_COUNTERS] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long t_k0 = COUNT ? wave_clock() : 0ull;
 
     for (;;) {
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
@@ -798,6 +850,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                     running = true;
                 }
             }
+            const unsigned long long t_c0 = COUNT ? wave_clock() : 0ull;
             for (;;) {
                 if (running) {
                     const bool shadow = (mode == M_SHADOW);
@@ -819,6 +872,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                 if (!__any(running)) break;
                 if (__popcll(__ballot(fin)) >= fetch_k) break;
             }
+            if (COUNT) cnt[6] += wave_clock() - t_c0;
         } else if (pending) {
             bool go = true;
             if (PACKET) {
@@ -850,6 +904,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
             }
         }
     }
+    if (COUNT) cnt[7] = wave_clock() - t_k0;
     flush_counters(a.counters, cnt, COUNT);
 }
 
@@ -1029,7 +1084,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
         a.seeds[slot] = seed.x;
         a.seeds[plane + slot] = seed.y;
     }
-    const unsigned long long cnt[RT_N_COUNTERS] = {n_closest, n_shadow, 0, 0, 0, 0};
+    const unsigned long long cnt[RT_N_COUNTERS] = {n_closest, n_shadow, 0, 0, 0, 0, 0, 0};
     flush_counters(a.counters, cnt, false);
 }
 

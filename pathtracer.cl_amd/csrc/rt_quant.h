@@ -1,0 +1,122 @@
+/*
+ * rt_quant.h — the compressed 4-wide node (48 B), built identically by the host SAH
+ * builder (rt_bvh.cpp) and the GPU builder (rt_build_gpu.hip) from a full-precision
+ * 4-wide node whose inner children are numbered consecutively and whose leaf children
+ * cover consecutive triangle slots, in child order.
+ *
+ * Layout (12 dwords, fetched as 3 x dwordx4):
+ *   d[0..2]  origin.xyz (float): the minimum corner of the children's boxes
+ *   d[3]     bits 0-4 / 5-9 / 10-14: per-axis grid exponent e + 24 (e in [-24, 7]);
+ *            bits 16-31: 4 bits per child k at 16 + 4k:
+ *              bit 3 set: leaf, bits 0-2 = triangle count - 1;
+ *              bit 3 clear: inner node, bits 0-1 = rank among the inner children
+ *   d[4..9]  8-bit planes lo.x, hi.x, lo.y, hi.y, lo.z, hi.z (child k in byte k);
+ *            plane = origin + q * 2^e, rounded outward (floor / ceil, checked in binary64)
+ *            so the box contains the exact child box; an unused slot is the inverted
+ *            box lo = 255 > hi = 0, which no ray enters
+ *   d[10]    index of the first inner child (inner child of rank r = d[10] + r)
+ *   d[11]    first triangle slot of the leaf children (a leaf starts after the
+ *            triangles of the leaf children before it)
+ */
+#ifndef RT_QUANT_H
+#define RT_QUANT_H
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "rt_internal.h"
+
+#define RT_QEXP_MIN (-24)
+#define RT_QEXP_MAX 7
+
+#if defined(__HIPCC__)
+#define RT_QHD __host__ __device__
+#else
+#define RT_QHD
+#endif
+
+/* f: 32 floats of a full-precision 4-wide node (rt_internal.h); q: 12 dwords out.
+   Returns false if a child's layout breaks the contiguity rules or an axis needs a grid
+   step beyond 2^RT_QEXP_MAX (extent > 255 * 128). */
+RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
+{
+    int32_t code[4];
+    for (int k = 0; k < 4; ++k) memcpy(&code[k], &f[24 + k], 4);
+    uint32_t exps = 0, meta = 0;
+    uint32_t planes[6] = {0, 0, 0, 0, 0, 0};
+    int32_t inner_base = 0, tri_base = 0;
+    int n_inner = 0, n_leaf_tris = 0;
+    bool seen_empty = false;
+    for (int k = 0; k < 4; ++k) {
+        const int32_t c = code[k];
+        if (c == RT_EMPTY_CHILD) {
+            seen_empty = true;
+            continue;
+        }
+        if (seen_empty) return false; /* unused slots must trail */
+        if (c >= 0) {
+            if (n_inner == 0) inner_base = c;
+            else if (c != inner_base + n_inner) return false;
+            meta |= (uint32_t)n_inner << (16 + 4 * k);
+            ++n_inner;
+        } else {
+            const int32_t enc = ~c;
+            const int32_t first = enc >> 3, count = (enc & 7) + 1;
+            if (n_leaf_tris == 0) tri_base = first;
+            else if (first != tri_base + n_leaf_tris) return false;
+            meta |= (uint32_t)(8 | (count - 1)) << (16 + 4 * k);
+            n_leaf_tris += count;
+        }
+    }
+    for (int ax = 0; ax < 3; ++ax) {
+        const float *lo = f + 8 * ax, *hi = f + 8 * ax + 4;
+        float omin = INFINITY, omax = -INFINITY;
+        for (int k = 0; k < 4; ++k)
+            if (code[k] != RT_EMPTY_CHILD) {
+                omin = fminf(omin, lo[k]);
+                omax = fmaxf(omax, hi[k]);
+            }
+        if (!(omin <= omax)) omin = omax = 0.0f;
+        const float origin = omin;
+        int e = RT_QEXP_MIN;
+        const double ext = (double)omax - (double)origin;
+        if (ext > 0) {
+            const int want = (int)ceil(log2(ext / 255.0));
+            e = want > RT_QEXP_MIN ? want : RT_QEXP_MIN;
+        }
+        for (;; ++e) {
+            if (e > RT_QEXP_MAX) return false;
+            const double step = ldexp(1.0, e);
+            bool ok = true;
+            uint32_t wl = 0, wh = 0;
+            for (int k = 0; k < 4; ++k) {
+                int32_t l = 255, h = 0;
+                if (code[k] != RT_EMPTY_CHILD) {
+                    l = (int32_t)floor(((double)lo[k] - origin) / step);
+                    h = (int32_t)ceil(((double)hi[k] - origin) / step);
+                    if (l < 0) l = 0;
+                    if (h > 255) ok = false;
+                    if ((double)origin + l * step > (double)lo[k] || (double)origin + h * step < (double)hi[k])
+                        ok = false;
+                }
+                wl |= (uint32_t)l << (8 * k);
+                wh |= (uint32_t)(h & 255) << (8 * k);
+            }
+            if (ok) {
+                planes[2 * ax] = wl;
+                planes[2 * ax + 1] = wh;
+                break;
+            }
+        }
+        memcpy(&q[ax], &origin, 4);
+        exps |= (uint32_t)(e - RT_QEXP_MIN) << (5 * ax);
+    }
+    q[3] = exps | meta;
+    for (int i = 0; i < 6; ++i) q[4 + i] = planes[i];
+    q[10] = (uint32_t)inner_base;
+    q[11] = (uint32_t)tri_base;
+    return true;
+}
+
+#endif /* RT_QUANT_H */

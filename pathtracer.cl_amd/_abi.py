@@ -158,7 +158,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = Path(path) if path else LIB_PATH
+    # RTMI_LIB: an alternative in-tree build of the same library (A/B experiments)
+    p = Path(path) if path else Path(os.environ.get("RTMI_LIB", LIB_PATH))
     if not p.exists():
         raise RuntimeError(
             f"{p} not found: the HIP library is required (build with `python __graft_entry__.py` "

@@ -192,6 +192,9 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     const V3 inv = s.inv, oi = s.oi;
     const int node = s.node;
     const bool leaf = node < 0;
+    /* wave-uniform: every lane's pushes and pops of this step stay in the LDS part
+       of the stack (almost always), so they need no per-lane LDS/spill selection */
+    const bool lds_only = !__any(stk.sp + 3 > RT_STACK_DEPTH);
     const uint32_t enc = (uint32_t)(~node);
     const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (enc >> 3)
                             : reinterpret_cast<const uint4 *>(nodes) + 3 * node;
@@ -258,15 +261,28 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
             cas(t[0], c[0], t[2], c[2]);
             cas(t[1], c[1], t[3], c[3]);
             cas(t[1], c[1], t[2], c[2]);
-            if (nhit >= 4) stk.push(c[3]);
-            if (nhit >= 3) stk.push(c[2]);
-            if (nhit >= 2) stk.push(c[1]);
+            if (lds_only) {
+                /* the nhit - 1 farther hits, farthest first, written unconditionally at
+                   sp, sp+1, sp+2 (slots above the new top hold junk) */
+                const int v0 = nhit >= 4 ? c[3] : (nhit == 3 ? c[2] : c[1]);
+                const int v1 = nhit >= 4 ? c[2] : c[1];
+                int *top = stk.lds + stk.sp * RT_BLOCK;
+                top[0] = v0;
+                top[RT_BLOCK] = v1;
+                top[2 * RT_BLOCK] = c[1];
+                stk.sp += nhit - 1;
+            } else {
+                if (nhit >= 4) stk.push(c[3]);
+                if (nhit >= 3) stk.push(c[2]);
+                if (nhit >= 2) stk.push(c[1]);
+            }
             s.node = c[0];
             return false;
         }
     }
     if (stk.sp == 0) return true;
-    s.node = stk.pop();
+    if (lds_only) s.node = stk.lds[--stk.sp * RT_BLOCK];
+    else s.node = stk.pop();
     return false;
 }
 

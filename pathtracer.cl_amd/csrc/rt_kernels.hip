@@ -662,27 +662,27 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
     const int fetch_k = (int)a.fetch_k;
 
     int mode = M_IDLE;
-    uint32_t x = 0, yl = 0, y = 0, slot = 0;
+    uint32_t x = 0, yl = 0; /* pixel column and local row (global row / seed slot derived) */
     Seed seed = {0u, 0u};
     float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f; /* pixel sum over samples (raytracer.cl:228-230) */
     float col_x = 0.0f, col_y = 0.0f, col_z = 0.0f; /* this path's radiance (trace_path_tri's pixelColor) */
     V3 prop = v3(1.0f, 1.0f, 1.0f);
     uint32_t sample = 0, depth = 0, light = 0;
-    V3 ro = v3(0.0f, 0.0f, 0.0f), rd = v3(0.0f, 0.0f, 1.0f);
-    V3 hp = ro, hn = ro, so = ro, sd = rd, direct = ro;
+    /* the query ray: a path segment (closest hit) or a shadow ray from the offset hit
+       point (any hit) — one register set for both, the phases never overlap */
+    V3 qo = v3(0.0f, 0.0f, 0.0f), qd = v3(0.0f, 0.0f, 1.0f);
+    V3 hp = qo, hn = qo, direct = qo;
     float stmax = 0.0f;
     bool tri_hit = false;
     bool running = false; /* a resumable query is in flight */
-    bool fin = false;     /* the lane's query completed: res / qt hold its result */
-    int res = -1;
-    float qt = kInf;
+    bool fin = false;     /* the lane's query completed: ts.best / ts.best_t hold its result */
     TravState ts;
     ts.node = 0;
     ts.best = -1;
     ts.best_orig = -1;
     ts.best_t = kInf;
-    ts.inv = ro;
-    ts.oi = ro;
+    ts.inv = qo;
+    ts.oi = qo;
     unsigned long long cnt[RT_N_COUNTERS] = {0, 0, 0, 0, 0, 0, 0, 0};
     const unsigned long long t_k0 = COUNT ? wave_clock() : 0ull;
 
@@ -694,17 +694,18 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
             if (mode == M_CLOSEST) {
                 ++cnt[0];
                 bool surface = true;
-                if (res >= 0) {
-                    const float4 e1 = tris[3 * res + 1];
-                    const float4 e2 = tris[3 * res + 2];
-                    hp = v3(ro.x + rd.x * qt, ro.y + rd.y * qt, ro.z + rd.z * qt);
+                if (ts.best >= 0) {
+                    const float qt = ts.best_t;
+                    const float4 e1 = tris[3 * ts.best + 1];
+                    const float4 e2 = tris[3 * ts.best + 2];
+                    hp = v3(qo.x + qd.x * qt, qo.y + qd.y * qt, qo.z + qd.z * qt);
                     hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z)); /* unnormalised, rtcommon.h:389 */
                     tri_hit = true;
                 } else {
                     /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
-                    const float hd = intersect_box(ro, rd, RT_SMALL_F, bw, bh, bw);
+                    const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
                     if (hd > RT_SMALL_F && hd < kInf) {
-                        hp = v3(ro.x + rd.x * hd, ro.y + rd.y * hd, ro.z + rd.z * hd);
+                        hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
                         hn = box_normal(hp, bw, bh, bw);
                         tri_hit = false;
                     } else {
@@ -713,7 +714,8 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                     }
                 }
                 if (surface) { /* sample_direct_illumination_tri, rtcommon.h:78-105 */
-                    so = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
+                    /* the shadow-ray origin (so) becomes the query origin */
+                    qo = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
                     direct = v3(0.0f, 0.0f, 0.0f);
                     light = 0;
                     if (n_lights > 0) want_shadow = true;
@@ -721,8 +723,8 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                 }
             } else {
                 ++cnt[1];
-                if (res < 0) { /* unoccluded: rtcommon.h:93-101 */
-                    const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
+                if (ts.best < 0) { /* unoccluded: rtcommon.h:93-101 */
+                    const float cw = qd.x * hn.x + qd.y * hn.y + qd.z * hn.z;
                     if (cw > 0) {
                         direct.x += s_light[light * 8 + 4] * cw;
                         direct.y += s_light[light * 8 + 5] * cw;
@@ -737,7 +739,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                 const float r1 = frand(seed);
                 const float r2 = frand(seed);
                 const V3 lc = v3(s_light[light * 8 + 0], s_light[light * 8 + 1], s_light[light * 8 + 2]);
-                sd = sphere_light_dir(so, lc, s_light[light * 8 + 3], r1, r2, stmax);
+                qd = sphere_light_dir(qo, lc, s_light[light * 8 + 3], r1, r2, stmax);
                 mode = M_SHADOW;
             }
             if (seg_done) {
@@ -754,10 +756,10 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                     col_x += prop.x * direct.x * scale;
                     col_y += prop.y * direct.y * scale;
                     col_z += prop.z * direct.z * scale;
-                    ro = hp;
+                    qo = hp;
                     const float r1 = frand(seed);
                     const float r2 = frand(seed);
-                    rd = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
+                    qd = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
                     ++depth;
                     if (depth > a.max_depth) sample_done = true;
                     else mode = M_CLOSEST;
@@ -782,6 +784,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                         p.w = old.w + (p.w - old.w) * t;
                     }
                     *dst = p;
+                    const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
                     mode = M_IDLE;
@@ -809,8 +812,8 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                     x = (tile % tiles_x) * 8u + (in & 7u);
                     yl = (tile / tiles_x) * 8u + (in >> 3);
                     if (x < a.W && yl < a.Hl) {
-                        y = global_row(yl, a.stripe, a.n_ranks, a.rank);
-                        slot = y * a.Wpad + x; /* raytracer.cl:207-209: unshifted seed slot */
+                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                        /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
                         acc_x = acc_y = acc_z = 0.0f;
@@ -842,9 +845,10 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
         if (mode == M_NEWSAMPLE) {
             const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
             const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
+            const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
             const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
-            ro = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
-            rd = camera_dir(a.cam, fa - hw, fb - hh);
+            qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+            qd = camera_dir(a.cam, fa - hw, fb - hh);
             prop = v3(1.0f, 1.0f, 1.0f);
             col_x = col_y = col_z = 0.0f;
             depth = 0;
@@ -856,13 +860,14 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
         if (RESUME) {
             if (pending) {
                 const bool shadow = (mode == M_SHADOW);
-                qt = shadow ? stmax : kInf;
-                res = -1;
+                const float qt = shadow ? stmax : kInf;
                 /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
                    returns true): no traversal, same result */
-                if (shadow && !(qt > RT_SMALL_F)) fin = true;
-                else {
-                    trav_begin(ts, stk, shadow ? so : ro, shadow ? sd : rd, qt);
+                if (shadow && !(qt > RT_SMALL_F)) {
+                    ts.best = -1;
+                    fin = true;
+                } else {
+                    trav_begin(ts, stk, qo, qd, qt);
                     running = true;
                 }
             }
@@ -871,12 +876,9 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                 if (running) {
                     const bool shadow = (mode == M_SHADOW);
                     TravCounts tc = {0u, 0u, 0u};
-                    if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F,
-                                               shadow, tc)) {
+                    if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, shadow, tc)) {
                         running = false;
                         fin = true;
-                        res = ts.best;
-                        qt = ts.best_t;
                     }
                     if (COUNT) {
                         cnt[2] += tc.nodes;
@@ -901,16 +903,16 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
             }
             if (go) {
                 const bool shadow = (mode == M_SHADOW);
-                qt = shadow ? stmax : kInf;
-                res = -1;
+                ts.best_t = shadow ? stmax : kInf;
+                ts.best = -1;
                 TravCounts tc = {0u, 0u, 0u};
-                if (!shadow || qt > RT_SMALL_F) {
+                if (!shadow || ts.best_t > RT_SMALL_F) {
                     if (PACKET)
-                        res = traverse_packet4<COUNT>(nodes, tris, shadow ? so : ro, shadow ? sd : rd, RT_SMALL_F, qt,
-                                                      shadow, s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
+                        ts.best = traverse_packet4<COUNT>(nodes, tris, qo, qd, RT_SMALL_F, ts.best_t, shadow,
+                                                          s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
                     else
-                        res = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, shadow ? so : ro, shadow ? sd : rd,
-                                                    RT_SMALL_F, qt, shadow, stk, tc);
+                        ts.best = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, qo, qd, RT_SMALL_F, ts.best_t, shadow,
+                                                        stk, tc);
                 }
                 fin = true;
                 if (COUNT) {

@@ -735,13 +735,7 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                 if (light < n_lights) want_shadow = true;
                 else seg_done = true;
             }
-            if (want_shadow) { /* one sample per light: frand r1 then r2 (rtcommon.h:92) */
-                const float r1 = frand(seed);
-                const float r2 = frand(seed);
-                const V3 lc = v3(s_light[light * 8 + 0], s_light[light * 8 + 1], s_light[light * 8 + 2]);
-                qd = sphere_light_dir(qo, lc, s_light[light * 8 + 3], r1, r2, stmax);
-                mode = M_SHADOW;
-            }
+            bool bounce = false;
             if (seg_done) {
                 const float scale = 1.0f * RT_M_1_PI_F;
                 if (tri_hit) { /* rtcommon.h:411-421: no bounce off triangles */
@@ -757,9 +751,45 @@ __global__ __launch_bounds__(RT_BLOCK, 4) void k_tris(RtTriLaunch a)
                     col_y += prop.y * direct.y * scale;
                     col_z += prop.z * direct.z * scale;
                     qo = hp;
-                    const float r1 = frand(seed);
-                    const float r2 = frand(seed);
-                    qd = shading_to_world(cos_sample_hemisphere(r1, r2), hn);
+                    bounce = true;
+                }
+            }
+            /* Next direction, light sample or Lambert bounce, through ONE code path: both
+               draw r1 then r2 (rtcommon.h:92, :459), build (cos(phi) st, sin(phi) st, ct)
+               with phi = 2 pi r2 and st = sqrt(1 - ct^2), and rotate it about an axis
+               (shading_to_world) — sphereEmissiveRadiance (materials.h:232-271) about the
+               direction to the light with ct = 1 + r1 (cos_max - 1), cos_sample_hemisphere
+               (materials.h:21-35) about the normal with ct = sqrt(1 - r1).  Only ct and the
+               axis differ, so lanes of both kinds share the sin/cos and the frame. */
+            if (want_shadow || bounce) {
+                const float r1 = frand(seed);
+                const float r2 = frand(seed);
+                V3 axis = hn;
+                float ct = 0.0f;
+                V3 lc = hn;
+                float lr = 0.0f;
+                if (want_shadow) {
+                    lc = v3(s_light[light * 8 + 0], s_light[light * 8 + 1], s_light[light * 8 + 2]);
+                    lr = s_light[light * 8 + 3];
+                    V3 dir = v3(lc.x - qo.x, lc.y - qo.y, lc.z - qo.z);
+                    const float inv = rt_rsqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
+                    dir.x *= inv;
+                    dir.y *= inv;
+                    dir.z *= inv;
+                    const float sin_max = lr * inv;
+                    const float cos_max = rt_sqrtf(1.0f - sin_max * sin_max);
+                    ct = 1.0f + r1 * (cos_max - 1.0f);
+                    axis = dir;
+                } else {
+                    ct = rt_sqrtf(1.0f - r1);
+                }
+                const float st = rt_sqrtf(1.0f - ct * ct);
+                const float phi = RT_M_2PI_F * r2;
+                qd = shading_to_world(v3(rt_cosf(phi) * st, rt_sinf(phi) * st, ct), axis);
+                if (want_shadow) {
+                    stmax = intersect_sphere(qo, qd, RT_SMALL_F, lc, lr) - RT_SMALL_F;
+                    mode = M_SHADOW;
+                } else {
                     ++depth;
                     if (depth > a.max_depth) sample_done = true;
                     else mode = M_CLOSEST;

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -63,6 +64,28 @@ struct TmpNode {
     int left = -1, right = -1; /* TmpNode indices, or -1 for a leaf */
     uint32_t first = 0, count = 0;
 };
+
+constexpr int kMaxBins = 64;
+
+/* SAH parameters: bins per axis and the cost of one node step relative to one
+   triangle test (RT_SAH_BINS / RT_SAH_TRAV override them for experiments). */
+int sah_bins()
+{
+    static const int b = [] {
+        const char *v = getenv("RT_SAH_BINS");
+        const int x = v ? atoi(v) : 32;
+        return std::min(std::max(x, 4), kMaxBins);
+    }();
+    return b;
+}
+float sah_trav()
+{
+    static const float c = [] {
+        const char *v = getenv("RT_SAH_TRAV");
+        return v ? (float)atof(v) : 1.0f;
+    }();
+    return c;
+}
 
 struct Builder {
     const float *verts;
@@ -112,13 +135,13 @@ struct Builder {
         const bool must_median =
             (int)depth + balanced_levels(count) >= RT_BVH_MAX_DEPTH - 1 || ext[axis] <= 0.0f;
         if (!must_median) {
-            constexpr int B = 16;
+            const int B = sah_bins();
             float best_cost = INFINITY;
             int best_axis = -1, best_bin = -1;
             for (int k = 0; k < 3; ++k) {
                 if (!(ext[k] > 0.0f)) continue;
-                Box bb[B];
-                uint32_t bn[B];
+                Box bb[kMaxBins];
+                uint32_t bn[kMaxBins];
                 for (int b = 0; b < B; ++b) {
                     bb[b].reset();
                     bn[b] = 0;
@@ -131,8 +154,8 @@ struct Builder {
                     bb[b].grow(tbox[t]);
                     bn[b]++;
                 }
-                float left_area[B];
-                uint32_t left_n[B];
+                float left_area[kMaxBins];
+                uint32_t left_n[kMaxBins];
                 Box acc;
                 acc.reset();
                 uint32_t n = 0;
@@ -158,9 +181,9 @@ struct Builder {
                 }
             }
             const float parent_area = nb.area();
-            /* SAH: traversal cost 1, triangle cost 1 (relative to the parent) */
+            /* SAH: traversal cost sah_trav(), triangle cost 1 (relative to the parent) */
             const float leaf_cost = (float)count;
-            const float split_cost = 1.0f + (parent_area > 0.0f ? best_cost / parent_area : INFINITY);
+            const float split_cost = sah_trav() + (parent_area > 0.0f ? best_cost / parent_area : INFINITY);
             if (count <= RT_LEAF_MAX && !(split_cost < leaf_cost)) return 0;
             if (best_axis >= 0) {
                 const float scale = (float)B / ext[best_axis];

@@ -15,7 +15,7 @@
 
 /* Traversal stack entries per lane (LDS).  rt_bvh.cpp bounds the tree depth so
    that push-far-child traversal never needs more (checked before launch). */
-#define RT_STACK_DEPTH 32
+#define RT_STACK_DEPTH 24
 #define RT_BVH_MAX_DEPTH (RT_STACK_DEPTH + 1)
 #define RT_BLOCK 256
 #define RT_LEAF_MAX 8

@@ -13,7 +13,7 @@
  * Binned SAH (16 bins over centroid bounds) with a depth budget: when the
  * remaining levels would only just fit a balanced tree under
  * RT_BVH_MAX_DEPTH, the split falls back to an object median, so inner depth
- * never exceeds RT_STACK_DEPTH (the LDS traversal stack).
+ * never exceeds RT_BVH_MAX_DEPTH - 1.
  */
 #include <algorithm>
 #include <chrono>
@@ -547,7 +547,7 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
         o[10] = p2[2] - a[2];
     }
     out.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (out.depth > RT_STACK_DEPTH) {
+    if (out.depth >= RT_BVH_MAX_DEPTH) {
         err = "BVH deeper than the traversal stack";
         return false;
     }

@@ -285,9 +285,13 @@ int trav_kind(const rt_ctx *c)
 
 uint32_t spill_cap(const rt_ctx *c)
 {
+    /* worst-case stack: the 4-wide tree's stack4; the binary tree pushes at most one
+       entry per level below the root */
     const int k = trav_kind(c);
-    return (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) && c->bvh.stack4 > RT_STACK_DEPTH ? c->bvh.stack4 - RT_STACK_DEPTH
-                                                                                        : 0;
+    uint32_t need = 0;
+    if (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) need = c->bvh.stack4;
+    else if (k == RT_TRAV_BVH2) need = c->bvh.depth;
+    return need > RT_STACK_DEPTH ? need - RT_STACK_DEPTH : 0;
 }
 
 const float *trav_nodes(const rt_ctx *c)
@@ -706,8 +710,6 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
     if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
     if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && !c->d_nodes)
         return fail(c, RT_ERR_STATE, "the GPU builder produces no binary tree: use a 4-wide traversal");
-    if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && c->bvh.depth > RT_STACK_DEPTH)
-        return fail(c, RT_ERR_LIMIT, "binary BVH deeper than the traversal stack");
     if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_PACKET && c->bvh.stack4 > 64)
         return fail(c, RT_ERR_LIMIT, "4-wide BVH stack exceeds the per-wave stack (64)");
     HIPCHK(c, hipSetDevice(c->device));

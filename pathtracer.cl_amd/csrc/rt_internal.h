@@ -13,10 +13,12 @@
 
 #include "rt_types.h"
 
-/* Traversal stack entries per lane (LDS).  rt_bvh.cpp bounds the tree depth so
-   that push-far-child traversal never needs more (checked before launch). */
+/* Traversal stack entries per lane kept in LDS (24 x 256 lanes x 4 B = 24 KB per
+   block: 5 blocks per CU); deeper entries go to a per-lane global spill tail sized
+   from the tree (rt_host.cpp spill_cap). */
 #define RT_STACK_DEPTH 24
-#define RT_BVH_MAX_DEPTH (RT_STACK_DEPTH + 1)
+/* Inner depth bound of the binary tree (median splits below it). */
+#define RT_BVH_MAX_DEPTH 33
 #define RT_BLOCK 256
 #define RT_LEAF_MAX 8
 /* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots,

@@ -130,18 +130,23 @@ __device__ __forceinline__ bool leaf_tests(const float4 *__restrict__ tris, int 
    4-wide tree whose worst-case stack exceeds RT_STACK_DEPTH. */
 struct Stack {
     int *lds;
-    int32_t *spill;
+    int32_t *spill_block; /* the block's spill area (uniform): lane l owns [l * cap, (l + 1) * cap) */
+    uint32_t cap;
     int sp;
+    __device__ __forceinline__ int32_t *spill_slot(int i) const
+    {
+        return spill_block + threadIdx.x * cap + (uint32_t)(i - RT_STACK_DEPTH);
+    }
     __device__ __forceinline__ void push(int v)
     {
         if (sp < RT_STACK_DEPTH) lds[sp * RT_BLOCK] = v;
-        else spill[sp - RT_STACK_DEPTH] = v;
+        else *spill_slot(sp) = v;
         ++sp;
     }
     __device__ __forceinline__ int pop()
     {
         --sp;
-        return (sp < RT_STACK_DEPTH) ? lds[sp * RT_BLOCK] : spill[sp - RT_STACK_DEPTH];
+        return (sp < RT_STACK_DEPTH) ? lds[sp * RT_BLOCK] : *spill_slot(sp);
     }
 };
 
@@ -559,6 +564,12 @@ __device__ __forceinline__ int traverse_packet4(const float4 *__restrict__ nodes
     return best;
 }
 
+/* a launch-uniform float held in an SGPR */
+__device__ __forceinline__ float uniform_f(float v)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 /* shader-clock timestamp (s_memtime), counting launches only */
 __device__ __forceinline__ unsigned long long wave_clock()
 {
@@ -645,7 +656,8 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
 
     Stack stk;
     stk.lds = s_stack + threadIdx.x;
-    stk.spill = a.spill + (size_t)(blockIdx.x * RT_BLOCK + threadIdx.x) * a.spill_cap;
+    stk.spill_block = a.spill + (size_t)blockIdx.x * RT_BLOCK * a.spill_cap;
+    stk.cap = a.spill_cap;
     stk.sp = 0;
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
@@ -656,8 +668,11 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
     const uint32_t tiles_x = (a.W + 7u) >> 3;
     const uint32_t tiles_y = (a.Hl + 7u) >> 3;
     const uint32_t n_items = tiles_x * tiles_y * 64u;
-    const float hw = ((float)a.W) / 2.0f;
-    const float hh = ((float)a.H) / 2.0f;
+    /* launch-uniform values pinned to SGPRs (readfirstlane), so they neither occupy nor
+       spill vector registers */
+    const float hw = uniform_f(((float)a.W) / 2.0f);
+    const float hh = uniform_f(((float)a.H) / 2.0f);
+    const float mix_t = uniform_f(a.progressive > 0 ? 1.0f / (float)a.progressive : 0.0f);
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
     const int fetch_k = (int)a.fetch_k;
 
@@ -807,7 +822,7 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                     float4 *dst = out + ((size_t)yl * a.W + x);
                     if (a.progressive > 0) {
                         const float4 old = *dst;
-                        const float t = 1.0f / (float)a.progressive;
+                        const float t = mix_t;
                         p.x = old.x + (p.x - old.x) * t;
                         p.y = old.y + (p.y - old.y) * t;
                         p.z = old.z + (p.z - old.z) * t;
@@ -831,7 +846,9 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
             if (lane == leader) base = atomicAdd(a.work_counter, (uint32_t)__popcll(idle));
             base = __shfl(base, leader);
             if (mode == M_IDLE) {
-                const uint32_t item = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+                /* rank among the idle lanes below this one (mbcnt: no per-lane mask register) */
+                const uint32_t item = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 if (item >= n_items) {
                     mode = M_DONE;
                 } else {
@@ -856,7 +873,7 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                             float4 *dst = out + ((size_t)yl * a.W + x);
                             if (a.progressive > 0) {
                                 const float4 old = *dst;
-                                const float t = 1.0f / (float)a.progressive;
+                                const float t = mix_t;
                                 p.x = old.x + (p.x - old.x) * t;
                                 p.y = old.y + (p.y - old.y) * t;
                                 p.z = old.z + (p.z - old.z) * t;
@@ -1153,7 +1170,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     TravCounts tc = {0u, 0u, 0u};
     Stack stk;
     stk.lds = s_stack + threadIdx.x;
-    stk.spill = spill + (size_t)i * spill_cap;
+    stk.spill_block = spill + (size_t)blockIdx.x * RT_BLOCK * spill_cap;
+    stk.cap = spill_cap;
     stk.sp = 0;
     int s;
     if (TRAV == RT_TRAV_PACKET4)

@@ -920,20 +920,24 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
             }
             const unsigned long long t_c0 = COUNT ? wave_clock() : 0ull;
             for (;;) {
-                if (running) {
-                    const bool shadow = (mode == M_SHADOW);
-                    TravCounts tc = {0u, 0u, 0u};
-                    if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, shadow, tc)) {
-                        running = false;
-                        fin = true;
+                /* four steps per exit check (fewer wave-level ballots and branches) */
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (running) {
+                        const bool shadow = (mode == M_SHADOW);
+                        TravCounts tc = {0u, 0u, 0u};
+                        if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, shadow, tc)) {
+                            running = false;
+                            fin = true;
+                        }
+                        if (COUNT) {
+                            cnt[2] += tc.nodes;
+                            cnt[3] += tc.tests;
+                            cnt[4] += tc.leaves;
+                        }
                     }
-                    if (COUNT) {
-                        cnt[2] += tc.nodes;
-                        cnt[3] += tc.tests;
-                        cnt[4] += tc.leaves;
-                    }
+                    if (COUNT) ++cnt[5];
                 }
-                if (COUNT) ++cnt[5];
                 if (!__any(running)) break;
                 if (__popcll(__ballot(fin)) >= fetch_k) break;
             }

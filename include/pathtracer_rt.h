@@ -87,6 +87,9 @@ typedef struct rt_counters {
                                 efficiency = (nodes_visited + leaves_visited) / lane_slots */
     uint64_t clocks_traversal; /* shader clocks waves spent in traversal rounds, summed over waves */
     uint64_t clocks_total;     /* shader clocks of the waves' whole lifetimes, summed over waves */
+    uint64_t pixel_clocks_max; /* the costliest pixel: shader clocks from its refill to its write */
+    uint64_t pixel_rays_max;   /* the most queries any one pixel needed */
+    uint64_t pixel_steps_max;  /* the most traversal steps any one pixel needed */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */

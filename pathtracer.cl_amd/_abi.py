@@ -102,6 +102,9 @@ class RtCounters(ctypes.Structure):
         ("lane_slots", ctypes.c_uint64),
         ("clocks_traversal", ctypes.c_uint64),
         ("clocks_total", ctypes.c_uint64),
+        ("pixel_clocks_max", ctypes.c_uint64),
+        ("pixel_rays_max", ctypes.c_uint64),
+        ("pixel_steps_max", ctypes.c_uint64),
     ]
 
 

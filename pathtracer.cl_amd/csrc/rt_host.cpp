@@ -125,7 +125,7 @@ struct rt_ctx {
     unsigned long long *d_counters = nullptr;
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
-    rt_counters last = {0, 0, 0, 0, 0, 0, 0, 0};
+    rt_counters last = {};
     bool have_timing = false;
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
@@ -851,6 +851,9 @@ int rt_synchronize(rt_ctx *c)
     c->last.lane_slots = h[5];
     c->last.clocks_traversal = h[6] / 64; /* summed over every lane of a wave */
     c->last.clocks_total = h[7] / 64;
+    c->last.pixel_clocks_max = h[8];
+    c->last.pixel_rays_max = h[9];
+    c->last.pixel_steps_max = h[10];
     return RT_OK;
 }
 

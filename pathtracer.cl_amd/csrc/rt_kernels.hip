@@ -587,11 +587,13 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 __device__ __forceinline__ void flush_counters(unsigned long long *dst, const unsigned long long (&v)[RT_N_COUNTERS],
                                                bool with_trav)
 {
-    const int n = with_trav ? RT_N_COUNTERS : 2;
+    const int n = with_trav ? RT_N_SUM_COUNTERS : 2;
     for (int i = 0; i < n; ++i) {
         const unsigned long long w = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0) atomicAdd(&dst[i], w);
     }
+    if (with_trav) /* per-pixel maxima */
+        for (int i = RT_N_SUM_COUNTERS; i < RT_N_COUNTERS; ++i) atomicMax(&dst[i], v[i]);
 }
 
 /* raytracer.cl:81-85: normalize(view + right*a + up*b), float4 lanes incl. w,
@@ -698,8 +700,10 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
     ts.best_t = kInf;
     ts.inv = qo;
     ts.oi = qo;
-    unsigned long long cnt[RT_N_COUNTERS] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[RT_N_COUNTERS] = {};
     const unsigned long long t_k0 = COUNT ? wave_clock() : 0ull;
+    /* counting launches: this pixel's start clock, queries and traversal steps */
+    unsigned long long pix_t0 = 0, pix_q = 0, pix_steps = 0;
 
     for (;;) {
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
@@ -708,6 +712,7 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
             bool want_shadow = false, seg_done = false, sample_done = false;
             if (mode == M_CLOSEST) {
                 ++cnt[0];
+                if (COUNT) ++pix_q;
                 bool surface = true;
                 if (ts.best >= 0) {
                     const float qt = ts.best_t;
@@ -738,6 +743,7 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                 }
             } else {
                 ++cnt[1];
+                if (COUNT) ++pix_q;
                 if (ts.best < 0) { /* unoccluded: rtcommon.h:93-101 */
                     const float cw = qd.x * hn.x + qd.y * hn.y + qd.z * hn.z;
                     if (cw > 0) {
@@ -833,6 +839,12 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
                     mode = M_IDLE;
+                    if (COUNT) {
+                        const unsigned long long dt = wave_clock() - pix_t0;
+                        cnt[8] = dt > cnt[8] ? dt : cnt[8];
+                        cnt[9] = pix_q > cnt[9] ? pix_q : cnt[9];
+                        cnt[10] = pix_steps > cnt[10] ? pix_steps : cnt[10];
+                    }
                 }
             }
         }
@@ -863,6 +875,10 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
+                        if (COUNT) {
+                            pix_t0 = wave_clock();
+                            pix_q = pix_steps = 0;
+                        }
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
                         if (spp > 0) {
@@ -934,6 +950,7 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                             cnt[2] += tc.nodes;
                             cnt[3] += tc.tests;
                             cnt[4] += tc.leaves;
+                            pix_steps += tc.nodes + tc.leaves;
                         }
                     }
                     if (COUNT) ++cnt[5];
@@ -1153,7 +1170,9 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
         a.seeds[slot] = seed.x;
         a.seeds[plane + slot] = seed.y;
     }
-    const unsigned long long cnt[RT_N_COUNTERS] = {n_closest, n_shadow, 0, 0, 0, 0, 0, 0};
+    unsigned long long cnt[RT_N_COUNTERS] = {};
+    cnt[0] = n_closest;
+    cnt[1] = n_shadow;
     flush_counters(a.counters, cnt, false);
 }
 

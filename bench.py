@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--sample-rate", type=int, default=None)
     ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
+                    help="N > 1: strong = one frame split into row-stripe tiles across ranks; weak = one full "
+                         "frame per rank (turntable views 3 degrees apart), frames gathered to rank 0. auto: weak "
+                         "for the dragon config (its 256-spp pixels are serial chains: DESIGN.md), else strong")
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
     ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "bvh2", "linear", "packet"],
                     help="bvh: 4-wide BVH (default); bvh2: binary BVH; linear: the reference loop")
@@ -102,11 +106,19 @@ def main():
     H = args.height or H
     sr = args.sample_rate or sr
 
+    scaling = args.scaling
+    if scaling == "auto":
+        scaling = "weak" if (cfg == "dragon" and world > 1) else "strong"
+    frames_per_rank = world > 1 and scaling == "weak"
+
     rt = pt.RayTracer(device)
     S = sc.ply_scene() if kernel == pt.RayTracer.KERNEL_TRIS else sc.main_scene()
     rt.setSpheres(S)
     cam_setup = sc.PLY_CAMERA if kernel == pt.RayTracer.KERNEL_TRIS else sc.MAIN_CAMERA
-    rt.setCameraSpherical(cam_setup["target"], cam_setup["elevation"], cam_setup["azimuth"], cam_setup["distance"])
+    # weak scaling: rank r renders the view r arrow-key steps (3 degrees, GlutCLWindow.cpp:228-262)
+    # around the turntable; rank 0's frame is the single-GPU frame
+    azimuth = cam_setup["azimuth"] + (3.0 * rank if frames_per_rank else 0.0)
+    rt.setCameraSpherical(cam_setup["target"], cam_setup["elevation"], azimuth, cam_setup["distance"])
     rt.setFoVAngle(sc.DEFAULT_FOV)
     rt.setSampleRate(sr)
     rt.setMaxPathDepth(6)
@@ -133,7 +145,7 @@ def main():
         mesh_info = rt.meshInfo()
         mesh_info["gen_seconds"] = round(t1 - t0, 3)
 
-    n_ranks = world
+    n_ranks = 1 if frames_per_rank else world  # ranks sharing one frame
     tile = (args.stripe, n_ranks, rank) if n_ranks > 1 else None
     rows = ptdist.max_tile_rows(H, args.stripe, n_ranks) if n_ranks > 1 else H
     out = torch.zeros(rows * W * 4, dtype=torch.float32, device=f"cuda:{device}")
@@ -164,6 +176,8 @@ def main():
         c = rt.counters()
         if n_ranks > 1:
             ptdist.gather_frame(out, H, W, args.stripe)
+        elif frames_per_rank:
+            ptdist.gather_frames(out)
         return c["rays_closest"] + c["rays_shadow"]
 
     # first render creates the seed layout; snapshot it so the counting launch and the
@@ -256,16 +270,19 @@ def main():
         "steps": steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
-        "frames_per_sec": round(steps / elapsed, 4),
+        "frames_per_sec": round(steps * (world if frames_per_rank else 1) / elapsed, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if frames_per_rank else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
         "config": {"workload": workload,
                    "W": W, "H": H, "spp": sr * sr, "n_tris": n_tris,
-                   "parallelism": f"row-stripes({args.stripe})x{world}" + ((" + rccl gather" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl" else " + gloo gather") if world > 1 else ""),
-                   "rays_per_frame": int(rays / steps), "mesh": mesh_info},
+                   "parallelism": ((f"frames x{world} (one turntable view per rank)" if frames_per_rank
+                                    else f"row-stripes({args.stripe})x{world}")
+                                   + ((" + rccl gather" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl"
+                                       else " + gloo gather") if world > 1 else "")),
+                   "rays_per_frame": int(rays / steps / (world if frames_per_rank else 1)), "mesh": mesh_info},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

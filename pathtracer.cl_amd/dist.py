@@ -79,6 +79,22 @@ def gather_frame(local, height: int, width: int, stripe: int, group=None, root: 
     return assemble([g.reshape(rows_max, width, 4) for g in gathered], height, width, stripe)
 
 
+def gather_frames(local, group=None, root: int = 0):
+    """Frame-parallel mode: every rank rendered its own full frame; gather them to `root`
+    with one torch.distributed.gather (RCCL for CUDA tensors).  Returns the list of frames
+    (rank order) on root, else None."""
+    import torch
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        local = local.cpu()
+    gathered = [torch.empty_like(local) for _ in range(world)] if rank == root else None
+    dist.gather(local, gathered, dst=root, group=group)
+    return gathered
+
+
 class SeedHalo:
     """Seed-row bookkeeping for tiled progressive sphere frames.
 

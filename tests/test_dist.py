@@ -151,3 +151,32 @@ def test_seed_halo_exchange_gloo(world, H, hpad, stripe, tmp_path):
     mp.spawn(_halo_worker, args=(world, _free_port(), H, hpad, 32, stripe, str(rp)), nprocs=world, join=True)
     ok, received = np.load(rp)
     assert ok == 1 and received > 0
+
+
+def _frames_worker(rank, world, port, result_path):
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ptload
+
+    pdist = ptload.submodule("dist")
+    local = torch.full((6 * 5 * 4,), float(rank) + 0.5)
+    frames = pdist.gather_frames(local)
+    if rank == 0:
+        np.save(result_path, torch.stack(frames).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_frames_gloo(tmp_path):
+    """Frame-parallel (weak-scaling) mode: one full frame per rank, gathered in rank order."""
+    rp = tmp_path / "frames.npy"
+    mp.spawn(_frames_worker, args=(3, _free_port(), str(rp)), nprocs=3, join=True)
+    got = np.load(rp)
+    assert got.shape == (3, 120)
+    for r in range(3):
+        assert np.all(got[r] == r + 0.5)

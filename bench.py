@@ -32,7 +32,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-NODE_BYTES = {"bvh": 48, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
+NODE_BYTES = {"bvh": 64, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
 # bytes read per triangle test: the whole 48-B record (one-record steps of the compressed traversal), else
 # v0+orig (16), e1 (12), e2 (12); csrc/rt_internal.h
 TRI_BYTES = {"bvh": 48, "bvh4f": 40, "bvh2": 40, "linear": 40, "packet": 48}

@@ -322,7 +322,7 @@ __global__ void k_quantize(const float *__restrict__ nodes4, uint32_t n_nodes, u
 {
     const uint32_t i = blockIdx.x * kB + threadIdx.x;
     if (i >= n_nodes) return;
-    if (!rt_quantize_node4(nodes4 + 32ull * i, q4 + 12ull * i)) atomicOr(fail, 1u);
+    if (!rt_quantize_node4(nodes4 + 32ull * i, q4 + (uint64_t)RT_QNODE_DWORDS * i)) atomicOr(fail, 1u);
 }
 
 /* 6b. triangle records in slot order: (v0, orig), (v1 - v0), (v2 - v0) (rtcommon.h:20-37) */
@@ -475,7 +475,7 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
         return -1;
     }
     uint32_t *q4 = nullptr;
-    GCHK(hipMalloc(&q4, 48ull * out.n_nodes4));
+    GCHK(hipMalloc(&q4, 4ull * RT_QNODE_DWORDS * out.n_nodes4));
     out.nodes4q = q4;
     hipLaunchKernelGGL(k_quantize, dim3(blocks_for(out.n_nodes4)), dim3(kB), 0, st, (const float *)nodes4,
                        out.n_nodes4, q4, cnt + 5);

@@ -519,9 +519,9 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
 
     /* Compressed copy of the 4-wide tree (48 B per node, rt_quant.h); dropped (the
        traversal falls back to full-precision nodes) if a node cannot be encoded. */
-    out.nodes4q.assign(12ull * out.n_nodes4, 0u);
+    out.nodes4q.assign((uint64_t)RT_QNODE_DWORDS * out.n_nodes4, 0u);
     for (uint32_t i = 0; i < out.n_nodes4; ++i)
-        if (!rt_quantize_node4(out.nodes4.data() + 32ull * i, out.nodes4q.data() + 12ull * i)) {
+        if (!rt_quantize_node4(out.nodes4.data() + 32ull * i, out.nodes4q.data() + (uint64_t)RT_QNODE_DWORDS * i)) {
             out.nodes4q.clear();
             break;
         }

@@ -202,8 +202,10 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     const bool lds_only = !__any(stk.sp + 3 > RT_STACK_DEPTH);
     const uint32_t enc = (uint32_t)(~node);
     const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (enc >> 3)
-                            : reinterpret_cast<const uint4 *>(nodes) + 3 * node;
+                            : reinterpret_cast<const uint4 *>(nodes) + (RT_QNODE_DWORDS / 4) * node;
     const uint4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+    /* explicit links (64-B nodes): a leaf lane re-reads its record's first 16 B (same line) */
+    [[maybe_unused]] const uint4 q3 = (RT_QNODE_DWORDS == 16) ? rec[leaf ? 0 : 3] : q0;
     if (leaf) {
         if (COUNT) {
             cnt.tests++;
@@ -239,7 +241,9 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
         float t[4];
         int c[4];
         int nhit = 0;
+#if RT_QNODE_DWORDS != 16
         int leaf_off = 0; /* triangles of the leaf children before child i */
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int sh = 8 * i;
@@ -252,11 +256,15 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                                 __builtin_fmaf((float)((fyw >> sh) & 255u), sy, by)),
                 __builtin_fminf(__builtin_fmaf((float)((fzw >> sh) & 255u), sz, bzo), tmax_c));
             const bool h = tn <= tf; /* an unused slot's inverted box never passes */
+#if RT_QNODE_DWORDS == 16
+            c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
+#else
             const uint32_t m = (w >> (16 + 4 * i)) & 15u;
             const bool lf = (m & 8u) != 0;
             const int k = (int)(m & 7u); /* leaf: count - 1; inner: rank */
             c[i] = lf ? ~((((int)q2.w + leaf_off) << 3) | k) : (int)q2.z + k;
             leaf_off += lf ? k + 1 : 0;
+#endif
             t[i] = h ? tn : kInf;
             nhit += h ? 1 : 0;
         }

@@ -1,10 +1,10 @@
 /*
- * rt_quant.h — the compressed 4-wide node (48 B), built identically by the host SAH
+ * rt_quant.h — the compressed 4-wide node (64 B), built identically by the host SAH
  * builder (rt_bvh.cpp) and the GPU builder (rt_build_gpu.hip) from a full-precision
  * 4-wide node whose inner children are numbered consecutively and whose leaf children
  * cover consecutive triangle slots, in child order.
  *
- * Layout (12 dwords, fetched as 3 x dwordx4):
+ * Layout (16 dwords, fetched as 4 x dwordx4; two nodes per 128-B line):
  *   d[0..2]  origin.xyz (float): the minimum corner of the children's boxes
  *   d[3]     bits 0-4 / 5-9 / 10-14: per-axis grid exponent e + 24 (e in [-24, 7]);
  *            bits 16-31: 4 bits per child k at 16 + 4k:
@@ -17,6 +17,10 @@
  *   d[10]    index of the first inner child (inner child of rank r = d[10] + r)
  *   d[11]    first triangle slot of the leaf children (a leaf starts after the
  *            triangles of the leaf children before it)
+ *   d[12..15] the four child links written out (rt_internal.h encoding)
+ * With RT_QNODE_DWORDS 12 the node is the first 48 B only and the traversal decodes the
+ * links from d[3] / d[10] / d[11]; measured 4.9 % slower than reading them (the decode's
+ * per-child branches cost more than the fourth load), so 64 B is the default.
  */
 #ifndef RT_QUANT_H
 #define RT_QUANT_H
@@ -27,6 +31,9 @@
 
 #include "rt_internal.h"
 
+#ifndef RT_QNODE_DWORDS
+#define RT_QNODE_DWORDS 16 /* 12: 48-B nodes (links from the meta nibbles); 16: + explicit links */
+#endif
 #define RT_QEXP_MIN (-24)
 #define RT_QEXP_MAX 7
 
@@ -36,7 +43,7 @@
 #define RT_QHD
 #endif
 
-/* f: 32 floats of a full-precision 4-wide node (rt_internal.h); q: 12 dwords out.
+/* f: 32 floats of a full-precision 4-wide node (rt_internal.h); q: RT_QNODE_DWORDS out.
    Returns false if a child's layout breaks the contiguity rules or an axis needs a grid
    step beyond 2^RT_QEXP_MAX (extent > 255 * 128). */
 RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
@@ -116,6 +123,9 @@ RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
     for (int i = 0; i < 6; ++i) q[4 + i] = planes[i];
     q[10] = (uint32_t)inner_base;
     q[11] = (uint32_t)tri_base;
+#if RT_QNODE_DWORDS == 16
+    for (int k = 0; k < 4; ++k) q[12 + k] = (uint32_t)code[k]; /* explicit links (64-B variant) */
+#endif
     return true;
 }
 

@@ -589,3 +589,35 @@ def test_interactive_view_replay(tracer, pt, tmp_path):
     assert (state["progression"], state["width"], state["height"]) == (prog, W, H)
     assert np.float32(state["azimuth"]) == az and np.float32(state["elevation"]) == el
     np.testing.assert_array_equal(bits(got), bits(buf))
+
+
+def test_huge_coordinates_fall_back_to_full_precision_nodes(tracer, pt):
+    """A mesh whose extent exceeds the compressed grid (255 * 2^7) cannot be encoded in
+    48/64-B nodes: the default traversal falls back to the full-precision 4-wide nodes and
+    still equals the linear loop."""
+    sc = pt.scenes
+    verts, idx = sc.make_mesh(3000)
+    verts = (verts * np.float32(2.0e4)).astype(np.float32)  # extent ~1e5
+    rng = np.random.default_rng(4)
+    n = 4096
+    rr = np.zeros(n, pt._abi.RAY_DTYPE)
+    rr["o"] = rng.uniform(-1.5e5, 1.5e5, (n, 3)).astype(np.float32)
+    tgt = verts[rng.integers(0, len(verts), n)]
+    d = tgt - rr["o"]
+    rr["d"] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rr["tmin"] = np.float32(1e-4)
+    rr["tmax"] = np.float32(np.inf)
+    res = {}
+    for builder in ("host", "gpu"):
+        for trav in ("bvh", "linear"):
+            rt = pt.RayTracer(0)
+            rt.setBuilder(builder)
+            rt.setMesh(verts, idx)
+            rt.setTraversal(trav)
+            res[(builder, trav)] = rt.traceRays(rr)
+            rt.close()
+    ref = res[("host", "linear")]
+    assert (ref[0] >= 0).sum() > n // 4
+    for key, got in res.items():
+        np.testing.assert_array_equal(got[0], ref[0], err_msg=str(key))
+        np.testing.assert_array_equal(bits(got[1]), bits(ref[1]), err_msg=str(key))

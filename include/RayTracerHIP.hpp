@@ -93,6 +93,26 @@ public:
         check(rt_set_mesh(ctx_, verts_xyz, n_verts, idx, n_tris), "setMesh");
     }
     void setTraversal(int traversal) { check(rt_set_traversal(ctx_, traversal), "setTraversal"); }
+    /* BVH builder for the next setMesh: RT_BUILD_HOST (binned SAH) or RT_BUILD_GPU (LBVH). */
+    void setBuilder(int builder) { check(rt_set_builder(ctx_, builder), "setBuilder"); }
+
+    /* plymain.cpp's PLYLoader (PLYLoader.cpp:4-90) with the mesh actually handed over:
+       read a PLY file, optionally normalise it (extent 3, resting on y = -5, centred on
+       x = z = 0) and set it as the mesh. */
+    void setMeshFromPly(const char *path, bool normalize = true)
+    {
+        rt_ply *ply = nullptr;
+        uint32_t nv = 0, nt = 0;
+        if (rt_ply_open(path, &ply, &nv, &nt) != RT_OK)
+            throw std::runtime_error(std::string("setMeshFromPly: ") + rt_ply_last_error());
+        std::vector<float> v(3ull * nv);
+        std::vector<int32_t> idx(3ull * nt);
+        const int r = rt_ply_read(ply, v.data(), idx.data());
+        rt_ply_close(ply);
+        check(r, "setMeshFromPly: read");
+        if (normalize) check(rt_normalize_mesh(v.data(), nv, 3.0f, -5.0f), "setMeshFromPly: normalise");
+        setMesh(v.data(), nv, idx.data(), nt);
+    }
 
     /* ---- RayTracerCL::rayTrace(cl_mem*, W, H, progression) ----
        `buff` is W*H*4 floats; a device pointer when on_device, else host memory. */

@@ -130,18 +130,7 @@ int main(int argc, char **argv)
         else rt.setCameraSpherical(target, 14.0f, 118.0f, 5.0f);     /* main.cpp:127-128 */
         int kernel = RT_KERNEL_SPHERES;
         if (!ply_path.empty()) { /* plymain.cpp:121, with the mesh actually handed to the tracer */
-            rt_ply *mesh = nullptr;
-            uint32_t nv = 0, nt = 0;
-            if (rt_ply_open(ply_path.c_str(), &mesh, &nv, &nt) != RT_OK) {
-                std::fprintf(stderr, "rt_render: %s\n", rt_ply_last_error());
-                return 1;
-            }
-            std::vector<float> v(3ull * nv);
-            std::vector<int> idx(3ull * nt);
-            const int rr = rt_ply_read(mesh, v.data(), idx.data());
-            rt_ply_close(mesh);
-            if (rr != RT_OK || rt_normalize_mesh(v.data(), nv, 3.0f, -5.0f) != RT_OK) return 1;
-            rt.setMesh(v.data(), nv, idx.data(), nt);
+            rt.setMeshFromPly(ply_path.c_str());
             rt.setTraversal(linear ? RT_TRAVERSAL_LINEAR : RT_TRAVERSAL_BVH);
             kernel = RT_KERNEL_TRIS;
         } else if (n_tris) {

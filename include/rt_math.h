@@ -145,6 +145,33 @@ RT_HD float rt_cosf(float x)
     return (sign < 0) ? -y : y;
 }
 
+/* sin and cos of one argument with one shared reduction: bit-identical to rt_sinf(x)
+   and rt_cosf(x) (the same operations, evaluated once). */
+RT_HD void rt_sincosf(float x, float *s, float *c)
+{
+    float ax = rt_fabsf(x);
+    if (!(ax < 1.0e7f)) {
+        *s = x - x;
+        *c = x - x;
+        return;
+    }
+    int j;
+    float r = rt_trig_reduce(ax, &j);
+    int ssign = (x < 0.0f) ? -1 : 1, csign = 1;
+    if (j > 3) {
+        ssign = -ssign;
+        csign = -csign;
+        j -= 4;
+    }
+    if (j > 1) csign = -csign;
+    float z = r * r;
+    const float sp = rt_sin_poly(r, z), cp = rt_cos_poly(z);
+    const int swap = (j == 1 || j == 2);
+    const float sy = swap ? cp : sp, cy = swap ? sp : cp;
+    *s = (ssign < 0) ? -sy : sy;
+    *c = (csign < 0) ? -cy : cy;
+}
+
 /* ---- exp (Cephes expf.c structure) -------------------------------------- */
 RT_HD float rt_expf(float x)
 {

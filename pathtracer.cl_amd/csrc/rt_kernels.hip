@@ -814,7 +814,9 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                 }
                 const float st = rt_sqrtf(1.0f - ct * ct);
                 const float phi = RT_M_2PI_F * r2;
-                qd = shading_to_world(v3(rt_cosf(phi) * st, rt_sinf(phi) * st, ct), axis);
+                float sphi, cphi;
+                rt_sincosf(phi, &sphi, &cphi);
+                qd = shading_to_world(v3(cphi * st, sphi * st, ct), axis);
                 if (want_shadow) {
                     stmax = intersect_sphere(qo, qd, RT_SMALL_F, lc, lr) - RT_SMALL_F;
                     mode = M_SHADOW;

@@ -282,7 +282,11 @@ def main():
                                     else f"row-stripes({args.stripe})x{world}")
                                    + ((" + rccl gather" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl"
                                        else " + gloo gather") if world > 1 else "")),
-                   "rays_per_frame": int(rays / steps / (world if frames_per_rank else 1)), "mesh": mesh_info},
+                   "rays_per_frame": int(rays / steps / (world if frames_per_rank else 1)),
+                   # rays = the reference's queries (oracle-equal counts); shadow rays whose answer
+                   # cannot change the pixel are answered without a traversal
+                   "rays_traversed_per_frame": int(rays_cnt - cnt.get("rays_skipped", 0)),
+                   "mesh": mesh_info},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

@@ -90,6 +90,9 @@ typedef struct rt_counters {
     uint64_t pixel_clocks_max; /* the costliest pixel: shader clocks from its refill to its write */
     uint64_t pixel_rays_max;   /* the most queries any one pixel needed */
     uint64_t pixel_steps_max;  /* the most traversal steps any one pixel needed */
+    uint64_t rays_skipped;     /* shadow rays (counted in rays_shadow) answered without a
+                                  traversal because the answer cannot change the pixel:
+                                  tmax <= tmin, or cos(wi) <= 0 (rtcommon.h:93-95) */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */

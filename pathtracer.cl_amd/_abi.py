@@ -105,6 +105,7 @@ class RtCounters(ctypes.Structure):
         ("pixel_clocks_max", ctypes.c_uint64),
         ("pixel_rays_max", ctypes.c_uint64),
         ("pixel_steps_max", ctypes.c_uint64),
+        ("rays_skipped", ctypes.c_uint64),
     ]
 
 

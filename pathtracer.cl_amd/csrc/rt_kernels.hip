@@ -595,8 +595,8 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v)
 __device__ __forceinline__ void flush_counters(unsigned long long *dst, const unsigned long long (&v)[RT_N_COUNTERS],
                                                bool with_trav)
 {
-    const int n = with_trav ? RT_N_SUM_COUNTERS : 2;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < RT_N_SUM_COUNTERS; ++i) {
+        if (!with_trav && i >= 2 && i != RT_CNT_SKIPPED) continue;
         const unsigned long long w = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0) atomicAdd(&dst[i], w);
     }
@@ -851,9 +851,9 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
                     mode = M_IDLE;
                     if (COUNT) {
                         const unsigned long long dt = wave_clock() - pix_t0;
-                        cnt[8] = dt > cnt[8] ? dt : cnt[8];
-                        cnt[9] = pix_q > cnt[9] ? pix_q : cnt[9];
-                        cnt[10] = pix_steps > cnt[10] ? pix_steps : cnt[10];
+                        cnt[9] = dt > cnt[9] ? dt : cnt[9];
+                        cnt[10] = pix_q > cnt[10] ? pix_q : cnt[10];
+                        cnt[11] = pix_steps > cnt[11] ? pix_steps : cnt[11];
                     }
                 }
             }
@@ -934,11 +934,16 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
             if (pending) {
                 const bool shadow = (mode == M_SHADOW);
                 const float qt = shadow ? stmax : kInf;
-                /* a shadow ray with tmax <= tmin can hit nothing (visibility_test_tri
-                   returns true): no traversal, same result */
-                if (shadow && !(qt > RT_SMALL_F)) {
+                /* Shadow rays whose answer cannot change the pixel are not traversed:
+                   tmax <= tmin (the sample missed the light) can hit nothing
+                   (visibility_test_tri returns true), and with cos(wi) <= 0 the light's
+                   term is dropped whatever the visibility (rtcommon.h:93-95 tests
+                   cosWi > 0 after the visibility test; the ray is const there, and
+                   both draws were already made).  Same pixel, same seeds. */
+                if (shadow && (!(qt > RT_SMALL_F) || !(qd.x * hn.x + qd.y * hn.y + qd.z * hn.z > 0))) {
                     ts.best = -1;
                     fin = true;
+                    ++cnt[RT_CNT_SKIPPED];
                 } else {
                     trav_begin(ts, stk, qo, qd, qt);
                     running = true;
@@ -1009,7 +1014,8 @@ __global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
 /* (raytracer.cl:46-166, trace_path rtcommon.h:267-365).                     */
 
 __device__ V3 trace_path(PathRay &r, const rt_sphere *__restrict__ sph, uint32_t n, uint32_t max_depth, Seed &seed,
-                         unsigned long long &n_closest, unsigned long long &n_shadow)
+                         unsigned long long &n_closest, unsigned long long &n_shadow,
+                         unsigned long long &n_skipped)
 {
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
     V3 color = v3(0.0f, 0.0f, 0.0f);
@@ -1064,17 +1070,17 @@ __device__ V3 trace_path(PathRay &r, const rt_sphere *__restrict__ sph, uint32_t
                         float stmax;
                         const V3 sd = sphere_light_dir(so, lc, lr, r1, r2, stmax);
                         ++n_shadow;
-                        bool vis = true; /* visibility_test, rtcommon.h:128-138 */
-                        for (uint32_t j = 0; j < n; ++j) {
+                        /* the light term needs cos(wi) > 0 AND visibility (rtcommon.h:160-167);
+                           the const shadow ray is tested only when cos(wi) > 0 — same result */
+                        const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
+                        bool vis = cw > 0; /* visibility_test, rtcommon.h:128-138 */
+                        if (!vis) ++n_skipped;
+                        for (uint32_t j = 0; vis && j < n; ++j) {
                             const float dd = intersect_sphere(so, sd, RT_SMALL_F, v3f(sph[j].center), sph[j].radius);
-                            if (dd > RT_SMALL_F && dd < stmax) {
-                                vis = false;
-                                break;
-                            }
+                            if (dd > RT_SMALL_F && dd < stmax) vis = false;
                         }
                         if (vis) {
-                            const float cw = sd.x * hn.x + sd.y * hn.y + sd.z * hn.z;
-                            if (cw > 0) {
+                            {
                                 direct.x += sph[k].mat.emission.x * cw * inv_samples;
                                 direct.y += sph[k].mat.emission.y * cw * inv_samples;
                                 direct.z += sph[k].mat.emission.z * cw * inv_samples;
@@ -1119,7 +1125,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
     /* 16 x 16 pixel tile per block; a wave covers 16 x 4 pixels */
     const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u);
     const uint32_t yl = blockIdx.y * 16u + (threadIdx.x >> 4);
-    unsigned long long n_closest = 0, n_shadow = 0;
+    unsigned long long n_closest = 0, n_shadow = 0, n_skipped = 0;
     if (x < a.W && yl < a.Hl) {
         const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
         const uint32_t plane = a.Wpad * a.Hpad;
@@ -1139,7 +1145,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
             r.prop = v3(1.0f, 1.0f, 1.0f);
             r.ext = v3(0.0f, 0.0f, 0.0f);
             r.diffuse = 0;
-            const V3 c = trace_path(r, a.spheres, a.n_spheres, a.max_depth, seed, n_closest, n_shadow);
+            const V3 c = trace_path(r, a.spheres, a.n_spheres, a.max_depth, seed, n_closest, n_shadow, n_skipped);
             pc = make_float4(c.x, c.y, c.z, 0.0f);
         } else {
             const uint32_t sr = a.sample_rate;
@@ -1155,7 +1161,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
                     r.prop = v3(1.0f, 1.0f, 1.0f);
                     r.ext = v3(0.0f, 0.0f, 0.0f);
                     r.diffuse = 0;
-                    const V3 c = trace_path(r, a.spheres, a.n_spheres, a.max_depth, seed, n_closest, n_shadow);
+                    const V3 c = trace_path(r, a.spheres, a.n_spheres, a.max_depth, seed, n_closest, n_shadow, n_skipped);
                     pc.x += c.x;
                     pc.y += c.y;
                     pc.z += c.z;
@@ -1183,6 +1189,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
     unsigned long long cnt[RT_N_COUNTERS] = {};
     cnt[0] = n_closest;
     cnt[1] = n_shadow;
+    cnt[RT_CNT_SKIPPED] = n_skipped;
     flush_counters(a.counters, cnt, false);
 }
 

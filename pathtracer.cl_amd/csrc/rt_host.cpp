@@ -758,7 +758,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                    rk = tile ? tile->rank : 0u;
     int e = 0;
     if (kernel == RT_KERNEL_TRIS) {
-        RtTriLaunch a;
+        RtTriLaunch a{};
         a.out = dout;
         a.seeds = c->d_seeds;
         a.nodes = trav_nodes(c);

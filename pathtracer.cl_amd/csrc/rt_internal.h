@@ -20,6 +20,10 @@
 /* Inner depth bound of the binary tree (median splits below it). */
 #define RT_BVH_MAX_DEPTH 33
 #define RT_BLOCK 256
+/* waves per SIMD the triangle kernel is compiled for (register budget 512 / waves) */
+#ifndef RT_TRIS_WAVES
+#define RT_TRIS_WAVES 5
+#endif
 #define RT_LEAF_MAX 8
 /* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots,
    traversal-loop clocks, kernel clocks (the last two: per lane, summed), shadow rays

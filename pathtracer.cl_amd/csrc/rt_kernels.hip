@@ -641,7 +641,7 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         wave's longest query ends.  LINEAR / PACKET: each query runs to
         completion inside the iteration. */
 template <int TRAV, bool COUNT>
-__global__ __launch_bounds__(RT_BLOCK, 5) void k_tris(RtTriLaunch a)
+__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
     constexpr bool PACKET = TRAV == RT_TRAV_PACKET4;
     constexpr bool RESUME = TRAV == RT_TRAV_BVH2 || TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;

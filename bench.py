@@ -245,6 +245,7 @@ def main():
     if cnt.get("clocks_total"):
         # share of the waves' time spent in traversal rounds (counting launch, s_memtime)
         roofline["traversal_time_frac"] = round(cnt["clocks_traversal"] / cnt["clocks_total"], 4)
+        roofline["shade_time_frac"] = round(cnt.get("clocks_shade", 0) / cnt["clocks_total"], 4)
 
     # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
     # when they were taken on this exact workload and kernel variant

@@ -93,6 +93,7 @@ typedef struct rt_counters {
     uint64_t rays_skipped;     /* shadow rays (counted in rays_shadow) answered without a
                                   traversal because the answer cannot change the pixel:
                                   tmax <= tmin, or cos(wi) <= 0 (rtcommon.h:93-95) */
+    uint64_t clocks_shade;     /* shader clocks waves spent advancing paths (counting launches) */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */

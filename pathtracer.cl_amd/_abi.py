@@ -106,6 +106,7 @@ class RtCounters(ctypes.Structure):
         ("pixel_rays_max", ctypes.c_uint64),
         ("pixel_steps_max", ctypes.c_uint64),
         ("rays_skipped", ctypes.c_uint64),
+        ("clocks_shade", ctypes.c_uint64),
     ]
 
 

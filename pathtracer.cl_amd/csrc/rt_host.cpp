@@ -852,9 +852,10 @@ int rt_synchronize(rt_ctx *c)
     c->last.clocks_traversal = h[6] / 64; /* summed over every lane of a wave */
     c->last.clocks_total = h[7] / 64;
     c->last.rays_skipped = h[RT_CNT_SKIPPED];
-    c->last.pixel_clocks_max = h[9];
-    c->last.pixel_rays_max = h[10];
-    c->last.pixel_steps_max = h[11];
+    c->last.clocks_shade = h[RT_CNT_SHADE] / 64;
+    c->last.pixel_clocks_max = h[10];
+    c->last.pixel_rays_max = h[11];
+    c->last.pixel_steps_max = h[12];
     return RT_OK;
 }
 

@@ -27,11 +27,12 @@
 #define RT_LEAF_MAX 8
 /* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots,
    traversal-loop clocks, kernel clocks (the last two: per lane, summed), shadow rays
-   answered without a traversal — summed over lanes; then per-pixel maxima: clocks,
-   queries, traversal steps of the costliest pixel */
-#define RT_N_SUM_COUNTERS 9
-#define RT_N_COUNTERS 12
+   answered without a traversal, path-advance (shading) clocks — summed over lanes; then
+   per-pixel maxima: clocks, queries, traversal steps of the costliest pixel */
+#define RT_N_SUM_COUNTERS 10
+#define RT_N_COUNTERS 13
 #define RT_CNT_SKIPPED 8
+#define RT_CNT_SHADE 9
 
 /* One BVH node = 4 x float4 = 64 B (both children's boxes in the parent):
      n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)

@@ -21,6 +21,9 @@
 #define RT_BVH_MAX_DEPTH 33
 #define RT_BLOCK 256
 /* waves per SIMD the triangle kernel is compiled for (register budget 512 / waves) */
+#ifndef RT_FULL_LOADS
+#define RT_FULL_LOADS 1 /* traversal records as whole dwordx4 loads (rt_kernels.hip trav_step_q) */
+#endif
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif

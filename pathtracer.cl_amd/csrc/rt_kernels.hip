@@ -129,13 +129,24 @@ __device__ __forceinline__ bool leaf_tests(const float4 *__restrict__ tris, int 
 
 /* Per-lane traversal stack: [depth][lane] in LDS (stride RT_BLOCK dwords, bank
    conflict free) with an overflow tail in global memory for the rare rays of a
-   4-wide tree whose worst-case stack exceeds RT_STACK_DEPTH. */
+   4-wide tree whose worst-case stack exceeds RT_STACK_DEPTH.  The two parts are
+   typed by address space, so that a pop that may come from either stays a
+   ds_read plus a global load under lane masks — never a generic (flat) load, which
+   would occupy the vector-memory address path for every LDS pop. */
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) int lds_int;
+typedef __attribute__((address_space(1))) int32_t glob_int;
+#else
+typedef int lds_int;
+typedef int32_t glob_int;
+#endif
+
 struct Stack {
-    int *lds;
-    int32_t *spill_block; /* the block's spill area (uniform): lane l owns [l * cap, (l + 1) * cap) */
+    lds_int *lds;
+    glob_int *spill_block; /* the block's spill area (uniform): lane l owns [l * cap, (l + 1) * cap) */
     uint32_t cap;
     int sp;
-    __device__ __forceinline__ int32_t *spill_slot(int i) const
+    __device__ __forceinline__ glob_int *spill_slot(int i) const
     {
         return spill_block + threadIdx.x * cap + (uint32_t)(i - RT_STACK_DEPTH);
     }
@@ -148,7 +159,17 @@ struct Stack {
     __device__ __forceinline__ int pop()
     {
         --sp;
-        return (sp < RT_STACK_DEPTH) ? lds[sp * RT_BLOCK] : *spill_slot(sp);
+        int v;
+        if (sp < RT_STACK_DEPTH) v = lds[sp * RT_BLOCK];
+        else v = *spill_slot(sp);
+        return v;
+    }
+    __device__ __forceinline__ void init(int *lds_base, int32_t *spill_base, uint32_t spill_cap)
+    {
+        lds = (lds_int *)(lds_base + threadIdx.x);
+        spill_block = (glob_int *)(spill_base + (size_t)blockIdx.x * RT_BLOCK * spill_cap);
+        cap = spill_cap;
+        sp = 0;
     }
 };
 
@@ -205,9 +226,25 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     const uint32_t enc = (uint32_t)(~node);
     const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (enc >> 3)
                             : reinterpret_cast<const uint4 *>(nodes) + (RT_QNODE_DWORDS / 4) * node;
-    const uint4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
+#if RT_FULL_LOADS
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u *vrec = reinterpret_cast<const v4u *>(rec);
+    v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2];
     /* explicit links (64-B nodes): a leaf lane re-reads its record's first 16 B (same line) */
+    v4u w3 = (RT_QNODE_DWORDS == 16) ? vrec[leaf ? 0 : 3] : w0;
+    /* Every lane's record arrives as whole dwordx4 loads issued together: without this
+       the compiler narrows loads to the components each branch uses (x4 + x3 + x2 +
+       dword) and sinks the child links below the box test, i.e. 5-6 vector-memory
+       instructions per step instead of 4 (each costs the address path ~16 cycles per
+       wave whatever its width) and a second dependent round trip for node lanes. */
+    asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+    const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
+    const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);
+    [[maybe_unused]] const uint4 q3 = make_uint4(w3.x, w3.y, w3.z, w3.w);
+#else
+    const uint4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
     [[maybe_unused]] const uint4 q3 = (RT_QNODE_DWORDS == 16) ? rec[leaf ? 0 : 3] : q0;
+#endif
     if (leaf) {
         if (COUNT) {
             cnt.tests++;
@@ -281,7 +318,7 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                    sp, sp+1, sp+2 (slots above the new top hold junk) */
                 const int v0 = nhit >= 4 ? c[3] : (nhit == 3 ? c[2] : c[1]);
                 const int v1 = nhit >= 4 ? c[2] : c[1];
-                int *top = stk.lds + stk.sp * RT_BLOCK;
+                lds_int *top = stk.lds + stk.sp * RT_BLOCK;
                 top[0] = v0;
                 top[RT_BLOCK] = v1;
                 top[2 * RT_BLOCK] = c[1];
@@ -667,10 +704,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     __syncthreads();
 
     Stack stk;
-    stk.lds = s_stack + threadIdx.x;
-    stk.spill_block = a.spill + (size_t)blockIdx.x * RT_BLOCK * a.spill_cap;
-    stk.cap = a.spill_cap;
-    stk.sp = 0;
+    stk.init(s_stack, a.spill, a.spill_cap);
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
     float4 *__restrict__ out = reinterpret_cast<float4 *>(a.out);
@@ -1215,10 +1249,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     float t = r.tmax;
     TravCounts tc = {0u, 0u, 0u};
     Stack stk;
-    stk.lds = s_stack + threadIdx.x;
-    stk.spill_block = spill + (size_t)blockIdx.x * RT_BLOCK * spill_cap;
-    stk.cap = spill_cap;
-    stk.sp = 0;
+    stk.init(s_stack, spill, spill_cap);
     int s;
     if (TRAV == RT_TRAV_PACKET4)
         s = traverse_packet4<false>(nodes, tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0,

@@ -129,7 +129,8 @@ struct rt_ctx {
     bool have_timing = false;
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
-    int grid_cache[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    /* persistent-grid size per (traversal kind, counting): index trav * 2 + count */
+    int grid_cache[2 * (RT_TRAV_BVH4Q + 1)] = {};
 };
 
 namespace {
@@ -315,6 +316,8 @@ int ensure_spill(rt_ctx *c, size_t entries)
 int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
 {
     const int key = trav * 2 + (count ? 1 : 0);
+    if (key < 0 || key >= (int)(sizeof(c->grid_cache) / sizeof(c->grid_cache[0])))
+        return fail(c, RT_ERR_ARG, "unknown traversal kind");
     if (!c->grid_cache[key]) {
         int b = 0;
         const int e = rt_tris_grid_blocks(c->device, trav, count, &b);
@@ -796,12 +799,17 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.spill = c->d_spill;
         a.fetch_k = c->fetch_k;
         a.tile_order = nullptr;
+        a.pixel_flags = nullptr;
         if (c->schedule) {
             const int ro = tile_order(c, W, H, hl, stripe, nr, rk, st);
             if (ro != RT_OK) return ro;
             a.tile_order = c->d_order;
+            if (a.tile_order) a.pixel_flags = c->d_flags;
         }
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
+        if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
+            fprintf(stderr, "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p\n", (void *)c,
+                    trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order);
         HIPCHK(c, hipEventRecord(c->ev0, st));
         e = rt_launch_tris(a, trav, c->counting, blocks, st);
         HIPCHK(c, hipEventRecord(c->ev1, st));

@@ -16,13 +16,21 @@
 /* Traversal stack entries per lane kept in LDS (24 x 256 lanes x 4 B = 24 KB per
    block: 5 blocks per CU); deeper entries go to a per-lane global spill tail sized
    from the tree (rt_host.cpp spill_cap). */
+#ifndef RT_STACK_DEPTH
 #define RT_STACK_DEPTH 24
+#endif
 /* Inner depth bound of the binary tree (median splits below it). */
 #define RT_BVH_MAX_DEPTH 33
 #define RT_BLOCK 256
 /* waves per SIMD the triangle kernel is compiled for (register budget 512 / waves) */
 #ifndef RT_FULL_LOADS
 #define RT_FULL_LOADS 1 /* traversal records as whole dwordx4 loads (rt_kernels.hip trav_step_q) */
+#endif
+#ifndef RT_MIX_PLANES
+#define RT_MIX_PLANES 1 /* node planes through v_perm_b32 + v_fma_mix_f32 (rt_kernels.hip trav_step_q) */
+#endif
+#ifndef RT_PRIO
+#define RT_PRIO 0 /* wave issue priority for waves holding box pixels (long sample chains) */
 #endif
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
@@ -111,6 +119,7 @@ struct RtTriLaunch {
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
     uint32_t fetch_k;           /* resumable queries: completed lanes that end a stepping round */
+    const uint8_t *pixel_flags; /* probe: 1 = the pixel's centre ray hits the mesh (NULL: unknown) */
 };
 
 struct RtSphLaunch {

@@ -16,6 +16,9 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "rt_device.h"
 #include "rt_internal.h"
 #include "rt_quant.h"
@@ -206,6 +209,14 @@ __device__ __forceinline__ void trav_begin(TravState &s, Stack &stk, V3 o, V3 d,
     stk.sp = 0;
 }
 
+/* Half `hi` of a word of two f16 values, widened to f32 (exact; folds into the
+   op_sel of v_fma_mix_f32). */
+__device__ __forceinline__ float half_of(uint32_t w, int hi)
+{
+    const uint16_t b = (uint16_t)(hi ? (w >> 16) : (w & 0xffffu));
+    return (float)__builtin_bit_cast(_Float16, b);
+}
+
 /* One step of the compressed 4-wide traversal (rt_quant.h).  Every lane fetches
    exactly one 48-B record per step — a node, or ONE triangle of its current leaf —
    with the same three dwordx4 loads, so a wave-step costs one memory round trip
@@ -267,9 +278,14 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
         if (COUNT) cnt.nodes++;
         const float tmax_c = t_slack(s.best_t);
         const uint32_t w = q0.w;
-        const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
-        const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
-        const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
+#if RT_MIX_PLANES
+        constexpr int kExpBias = RT_QEXP_MIN + 24; /* scales carry the 2^24 of the f16-subnormal planes */
+#else
+        constexpr int kExpBias = RT_QEXP_MIN;
+#endif
+        const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + kExpBias);
+        const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + kExpBias);
+        const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + kExpBias);
         const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
         const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
         const float bzo = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
@@ -283,8 +299,32 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
 #if RT_QNODE_DWORDS != 16
         int leaf_off = 0; /* triangles of the leaf children before child i */
 #endif
+#if RT_MIX_PLANES
+        /* Plane bytes as f16 subnormals: v_perm_b32 spreads two bytes of a plane word into
+           the low bytes of two 16-bit halves (0x00bb = b * 2^-24 as f16, exact), and
+           v_fma_mix_f32 converts a half and does the FMA in one instruction, with the
+           2^24 folded into the scale's exponent: (b * 2^-24) * (s * 2^24) + base is exactly
+           fma(b, s, base) — the same bits as a byte convert + FMA, in 3/4 of the VALU. */
+        const float sx24 = sx, sy24 = sy, sz24 = sz;
+        const uint32_t nx01 = __builtin_amdgcn_perm(0u, nxw, 0x0c010c00u), nx23 = __builtin_amdgcn_perm(0u, nxw, 0x0c030c02u);
+        const uint32_t ny01 = __builtin_amdgcn_perm(0u, nyw, 0x0c010c00u), ny23 = __builtin_amdgcn_perm(0u, nyw, 0x0c030c02u);
+        const uint32_t nz01 = __builtin_amdgcn_perm(0u, nzw, 0x0c010c00u), nz23 = __builtin_amdgcn_perm(0u, nzw, 0x0c030c02u);
+        const uint32_t fx01 = __builtin_amdgcn_perm(0u, fxw, 0x0c010c00u), fx23 = __builtin_amdgcn_perm(0u, fxw, 0x0c030c02u);
+        const uint32_t fy01 = __builtin_amdgcn_perm(0u, fyw, 0x0c010c00u), fy23 = __builtin_amdgcn_perm(0u, fyw, 0x0c030c02u);
+        const uint32_t fz01 = __builtin_amdgcn_perm(0u, fzw, 0x0c010c00u), fz23 = __builtin_amdgcn_perm(0u, fzw, 0x0c030c02u);
+#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
+#if RT_MIX_PLANES
+            const float tn = __builtin_fmaxf(
+                __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nx01 : nx23, i & 1), sx24, bx),
+                                __builtin_fmaf(half_of(i < 2 ? ny01 : ny23, i & 1), sy24, by)),
+                __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nz01 : nz23, i & 1), sz24, bzo), tmin_c));
+            const float tf = __builtin_fminf(
+                __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fx01 : fx23, i & 1), sx24, bx),
+                                __builtin_fmaf(half_of(i < 2 ? fy01 : fy23, i & 1), sy24, by)),
+                __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fz01 : fz23, i & 1), sz24, bzo), tmax_c));
+#else
             const int sh = 8 * i;
             const float tn = __builtin_fmaxf(
                 __builtin_fmaxf(__builtin_fmaf((float)((nxw >> sh) & 255u), sx, bx),
@@ -294,6 +334,7 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 __builtin_fminf(__builtin_fmaf((float)((fxw >> sh) & 255u), sx, bx),
                                 __builtin_fmaf((float)((fyw >> sh) & 255u), sy, by)),
                 __builtin_fminf(__builtin_fmaf((float)((fzw >> sh) & 255u), sz, bzo), tmax_c));
+#endif
             const bool h = tn <= tf; /* an unused slot's inverted box never passes */
 #if RT_QNODE_DWORDS == 16
             c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
@@ -736,6 +777,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     float stmax = 0.0f;
     bool tri_hit = false;
     bool running = false; /* a resumable query is in flight */
+    [[maybe_unused]] bool costly = false; /* the pixel is a box pixel (long sample chain), from the probe */
     bool fin = false;     /* the lane's query completed: ts.best / ts.best_t hold its result */
     TravState ts;
     ts.node = 0;
@@ -888,6 +930,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
                     mode = M_IDLE;
+                    if (RT_PRIO) costly = false;
                     if (COUNT) {
                         const unsigned long long dt = wave_clock() - pix_t0;
                         cnt[10] = dt > cnt[10] ? dt : cnt[10];
@@ -931,6 +974,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         }
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
+                        if (RT_PRIO) costly = a.pixel_flags && !a.pixel_flags[(size_t)yl * a.W + x];
                         if (spp > 0) {
                             mode = M_NEWSAMPLE;
                         } else { /* no samples: 0/0 pixels, seeds untouched (raytracer.cl:234-242) */
@@ -969,6 +1013,18 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         }
 
         /* ---- C: ray queries ---- */
+        if (RT_PRIO == 1) {
+            /* the waves that hold box pixels (the long serial chains that end the frame)
+               issue first; scheduling only */
+            if (__any(costly)) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        } else if (RT_PRIO == 2) {
+            const int nc = __popcll(__ballot(costly));
+            if (nc > 16) __builtin_amdgcn_s_setprio(3);
+            else if (nc > 4) __builtin_amdgcn_s_setprio(2);
+            else if (nc > 0) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const bool pending = (mode == M_CLOSEST || mode == M_SHADOW) && !running && !fin;
         if (RESUME) {
             if (pending) {
@@ -1402,6 +1458,9 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
     int n_cu = 0;
     const hipError_t he = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
     if (he != hipSuccess) return (int)he;
+    if (getenv("RT_DEBUG_LAUNCH"))
+        fprintf(stderr, "[rtmi] occupancy: trav %d count %d per_cu %d n_cu %d (device %d, err %d)\n", trav, (int)count,
+                per_cu, n_cu, device, e);
     if (per_cu < 1) per_cu = 1;
     *blocks = per_cu * n_cu;
     return 0;

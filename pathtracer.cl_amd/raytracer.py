@@ -23,8 +23,9 @@ class RayTracer:
     KERNEL_SPHERES_SS = _abi.RT_KERNEL_SPHERES_SS
     KERNEL_TRIS = _abi.RT_KERNEL_TRIS
 
-    def __init__(self, device: int = 0):
-        self._lib = _abi.load()
+    def __init__(self, device: int = 0, lib_path=None):
+        # lib_path: another build of librtmi.so (in-process A/B of kernel variants)
+        self._lib = _abi.load(lib_path)
         h = ctypes.c_void_p()
         st = self._lib.rt_create(int(device), ctypes.byref(h))
         if st != _abi.RT_OK:

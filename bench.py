@@ -337,45 +337,68 @@ def _workload_name(cfg, n_tris, W, H, sr, traversal):
 
 
 def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, verts, idx):
-    """The CPU oracle (bit-identical restatement of the reference kernel, oracle/pt_oracle.c)
-    on a bounded sample of the same frame: one full pixel (all sr*sr samples) per thread,
-    pixels strided over the frame; rays counted by the oracle."""
+    """The reference's own kernel (clrt/ocl/raytracer.cl compiled for x86-64 from its source,
+    oracle/_ref/libptref.so: kind "reference") on the host cores, on a bounded sample of the
+    same frame: whole pixels (all sr*sr samples) strided over the frame.  Rays are counted by
+    the oracle (oracle/pt_oracle.c, the bit-identical restatement) on the same pixels, untimed,
+    and the two renders of the sample are compared bit for bit.  Without oracle/_ref (it is
+    built in the container from /root/reference), the oracle itself is timed (kind "port")."""
     sys.path.insert(0, str(ROOT / "oracle"))
-    from oracle import Oracle
+    from oracle import LIBREF, Oracle, Reference
 
     orc = Oracle()
+    ref = Reference(build_if_missing=False) if LIBREF.exists() else None
     threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
     cam = sc.camera_spherical(W, **(sc.PLY_CAMERA if kernel == 2 else sc.MAIN_CAMERA))
     out = np.zeros(W * H * 4, np.float32)
+    out_o = np.zeros_like(out)
     sd = seeds.copy()
+    sd_o = seeds.copy()
+    closest = shadow = 0
+    dt = 0.0
+    batches = 0
+    exact = True
+    # batches of whole pixels, strided over the frame with a different phase per batch, until
+    # the timed renders have taken target_s seconds (bounded)
+    if kernel != 2:  # sphere scene: one full frame (a few seconds on the host cores)
+        t0 = time.perf_counter()
+        if ref is not None:
+            ref.launch(0, out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, nthreads=threads)
+        else:
+            orc.render_spheres(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, nthreads=threads)
+        dt = time.perf_counter() - t0
+        closest, shadow = orc.render_spheres(out_o, cam, S, W, H, Wp, Hp, sr, 6, 0, sd_o, nthreads=threads)
+        batches = 1
+    n_px = threads
+    stride = W * H // n_px
+    while kernel == 2 and dt < target_s and batches < 64:
+        phase = (batches * 7919 + stride // 2) % stride
+        pix = (np.arange(n_px, dtype=np.uint64) * stride + phase).astype(np.uint32)
+        t0 = time.perf_counter()
+        if ref is not None:
+            ref.launch_pixels(2, out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, pix, verts, idx, nthreads=threads)
+        else:
+            orc.render_tris(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix, nthreads=threads)
+        dt += time.perf_counter() - t0
+        c, s = orc.render_tris(out_o, cam, S, W, H, Wp, Hp, sr, 6, 0, sd_o, verts, idx, pixels=pix, nthreads=threads)
+        closest += c
+        shadow += s
+        batches += 1
+    if ref is not None:
+        exact = bool(np.array_equal(out.view(np.uint32), out_o.view(np.uint32)) and np.array_equal(sd, sd_o))
+    rays = closest + shadow
     if kernel == 2:
-        # batches of `threads` whole pixels (all sr*sr samples each), strided over the frame with a
-        # different phase per batch, until the sample has taken target_s seconds (bounded)
-        closest = shadow = 0
-        dt = 0.0
-        batches = 0
-        n_px = threads
-        stride = W * H // n_px
-        while dt < target_s and batches < 64:
-            phase = (batches * 7919 + stride // 2) % stride
-            pix = (np.arange(n_px, dtype=np.uint64) * stride + phase).astype(np.uint32)
-            t0 = time.perf_counter()
-            c, s = orc.render_tris(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix,
-                                   nthreads=threads)
-            dt += time.perf_counter() - t0
-            closest += c
-            shadow += s
-            batches += 1
         sample = (f"{batches * n_px} whole pixels x {sr * sr} samples ({batches} strided batches over the frame), "
                   "linear traversal (the reference algorithm)")
     else:
-        t0 = time.perf_counter()
-        closest, shadow = orc.render_spheres(out, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, nthreads=threads)
-        dt = time.perf_counter() - t0
         sample = f"full {W}x{H} frame"
-    rays = closest + shadow
-    return {"value": round(rays / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": sample, "seconds": round(dt, 2), "rays": int(rays)}
+    res = {"value": round(rays / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads,
+           "kind": "reference" if ref is not None else "port", "sample": sample, "seconds": round(dt, 2),
+           "rays": int(rays)}
+    if ref is not None:
+        res["source"] = "clrt/ocl/raytracer.cl compiled for x86-64 (oracle/Makefile ref), one work-item per pixel"
+        res["bit_exact_vs_oracle"] = exact
+    return res
 
 
 if __name__ == "__main__":

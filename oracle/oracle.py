@@ -101,8 +101,8 @@ class Oracle:
 class Reference:
     """The reference kernel itself (clrt/ocl/raytracer.cl compiled for x86-64) + KAT wrappers."""
 
-    def __init__(self):
-        if not LIBREF.exists():
+    def __init__(self, build_if_missing: bool = True):
+        if not LIBREF.exists() and build_if_missing:
             build(ref=True)
         if not LIBREF.exists():
             raise FileNotFoundError(f"{LIBREF} (needs /root/reference to build)")
@@ -111,6 +111,9 @@ class Reference:
         vp, u32, i32, f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
         L.ref_launch_kernel.argtypes = [i32, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32, vp, vp, vp, u32, i32]
         L.ref_launch_kernel.restype = i32
+        L.ref_launch_pixels.argtypes = [i32, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32, vp, vp, vp, u32,
+                                        vp, u32, i32]
+        L.ref_launch_pixels.restype = i32
         L.ref_camera_spherical.argtypes = [f32, f32, f32, f32, f32, f32, f32, u32, vp]
         L.ref_frand_seq.argtypes = [vp, vp, u32]
         L.ref_strat_seq.argtypes = [vp, vp, u32, i32]
@@ -135,6 +138,16 @@ class Reference:
         st = self.lib.ref_launch_kernel(kernel, _p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad,
                                         sample_rate, max_depth, progressive, _p(seeds), _p(verts), _p(idx), n_tris,
                                         nthreads)
+        assert st == 0
+
+    def launch_pixels(self, kernel, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds,
+                      pixels, verts=None, idx=None, nthreads=8):
+        """The reference kernel on the work-items of `pixels` (y*W + x) only."""
+        n_tris = 0 if idx is None else idx.size // 3
+        px = np.ascontiguousarray(pixels, np.uint32)
+        st = self.lib.ref_launch_pixels(kernel, _p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad,
+                                        sample_rate, max_depth, progressive, _p(seeds), _p(verts), _p(idx), n_tris,
+                                        _p(px), px.size, nthreads)
         assert st == 0
 
     def camera_spherical(self, width, target, elevation, azimuth, distance, fov=53.0):

@@ -117,6 +117,63 @@ REF_API int ref_launch_kernel(int kernel, float *out, const rt_camera *cam, cons
     return 0;
 }
 
+/* The same launch restricted to a pixel subset (pixels[i] = y*W + x): bench.py's
+   bounded CPU baseline runs the reference kernel on strided whole pixels.  Each
+   work-item is the kernel's own (same gid, same padded global size), so every listed
+   pixel and seed slot ends exactly as in a full launch. */
+typedef struct ref_pixels_job {
+    ref_launch L;
+    const uint32_t *pixels;
+    uint32_t n_pixels;
+} ref_pixels_job;
+
+static void *ref_pixels_worker(void *arg)
+{
+    ref_pixels_job *J = (ref_pixels_job *)arg;
+    ref_launch *L = &J->L;
+    clshim_gsz[0] = L->Wpad;
+    clshim_gsz[1] = L->Hpad;
+    clshim_gsz[2] = 1;
+    clshim_gid[2] = 0;
+    for (uint32_t i = (uint32_t)L->tid; i < J->n_pixels; i += (uint32_t)L->nthreads) {
+        clshim_gid[0] = J->pixels[i] % L->W;
+        clshim_gid[1] = J->pixels[i] / L->W;
+        if (L->kernel == REF_TRIS)
+            __clang_ocl_kern_imp_raytrace_tris(L->out, L->cam, L->s, L->n, L->W, L->H, L->sr, L->depth, L->prog,
+                                               L->seeds, L->verts, L->idx, L->n_tris);
+        else
+            __clang_ocl_kern_imp_raytrace(L->out, L->cam, L->s, L->n, L->W, L->H, L->sr, L->depth, L->prog,
+                                          L->seeds);
+    }
+    return NULL;
+}
+
+REF_API int ref_launch_pixels(int kernel, float *out, const rt_camera *cam, const rt_sphere *s, uint32_t n,
+                              uint32_t W, uint32_t H, uint32_t Wpad, uint32_t Hpad, uint32_t sr, uint32_t depth,
+                              uint32_t prog, uint32_t *seeds, const float *verts, const int32_t *idx,
+                              uint32_t n_tris, const uint32_t *pixels, uint32_t n_pixels, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 128) nthreads = 128;
+    if (Wpad < W || Hpad < H || (kernel != REF_TRIS && kernel != REF_SPHERES)) return -1;
+    for (uint32_t i = 0; i < n_pixels; ++i)
+        if (pixels[i] >= W * H) return -1;
+    ref_pixels_job J[128];
+    pthread_t th[128];
+    for (int t = 0; t < nthreads; ++t) {
+        ref_launch l = {kernel, out, cam, s, n, W, H, Wpad, Hpad, sr, depth, prog, seeds,
+                        (const rt_vec3 *)verts, idx, n_tris, t, nthreads};
+        J[t].L = l;
+        J[t].pixels = pixels;
+        J[t].n_pixels = n_pixels;
+    }
+    for (int t = 1; t < nthreads; ++t)
+        if (pthread_create(&th[t], NULL, ref_pixels_worker, &J[t]) != 0) return -2;
+    ref_pixels_worker(&J[0]);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    return 0;
+}
+
 /* ---- per-function known-answer wrappers --------------------------------- */
 
 REF_API void ref_frand_seq(rt_seed *seed, float *out, uint32_t n)

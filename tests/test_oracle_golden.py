@@ -187,3 +187,37 @@ def test_math_model_sanity(oracle):
         got = np.array([L.or_math_pow(float(a), 1.0 / (e + 1.0)) for a in r1], np.float32)
         ref = np.power(r1.astype(np.float64), 1.0 / np.float64(np.float32(1.0) / np.float32(e + 1.0)) ** -1)
         assert np.allclose(got, ref, rtol=2e-7, atol=0)
+
+
+def test_reference_pixel_subset_matches_oracle(golden, golden_meta, oracle, pt):
+    """bench.py's CPU baseline runs the reference kernel (oracle/_ref) on a strided pixel
+    subset; those pixels and their seed slots must end exactly as the oracle's subset render
+    leaves them (and every other pixel and seed untouched)."""
+    from oracle import LIBREF, Reference
+
+    if not LIBREF.exists():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    ref = Reference(build_if_missing=False)
+    name = TRI_CASES[0]
+    g = golden(name)
+    m = golden_meta["cases"][name]
+    spheres = g["spheres"].view(pt._abi.SPHERE_DTYPE)
+    W, H = m["W"], m["H"]
+    pix = np.arange(5, W * H, 37, dtype=np.uint32)
+    outs, seeds = [], []
+    for who in ("ref", "oracle"):
+        out = np.full(W * H * 4, -1.0, np.float32)
+        sd = g["seeds_in"].copy()
+        if who == "ref":
+            ref.launch_pixels(2, out, g["camera"], spheres, W, H, m["Wpad"], m["Hpad"], m["sample_rate"],
+                              m["max_depth"], 0, sd, pix, g["verts"], g["idx"], nthreads=3)
+        else:
+            oracle.render_tris(out, g["camera"], spheres, W, H, m["Wpad"], m["Hpad"], m["sample_rate"],
+                               m["max_depth"], 0, sd, g["verts"], g["idx"], pixels=pix, nthreads=3)
+        outs.append(out)
+        seeds.append(sd)
+    np.testing.assert_array_equal(bits(outs[0]), bits(outs[1]))
+    np.testing.assert_array_equal(seeds[0], seeds[1])
+    assert (outs[0].reshape(-1, 4)[pix] != -1.0).all()
+    untouched = np.setdiff1d(np.arange(W * H), pix)
+    assert (outs[0].reshape(-1, 4)[untouched] == -1.0).all()

@@ -86,7 +86,7 @@ struct rt_ctx {
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
-    uint8_t *d_flags = nullptr;  /* probe flags */
+    uint32_t *d_flags = nullptr; /* cost probe per pixel (k_probe_cost) */
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
     size_t halo_rows_cap = 0, halo_buf_cap = 0;
@@ -94,6 +94,7 @@ struct rt_ctx {
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
     uint32_t fetch_k = 16;
+    uint32_t fetch_k_box = 16; /* waves holding box pixels (probe) */
     int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
@@ -331,48 +332,67 @@ int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
 /* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by
    its paths: a camera ray that hits the mesh ends after one shadow query per
    light (rtcommon.h:411-421), one that misses bounces off the box up to
-   maxDepth+1 times with shadow queries at each (rtcommon.h:425-461).  A probe
-   of one centre ray per pixel estimates each 8x8 tile's cost, and the queue
-   hands out the most expensive tiles first, so the launch does not end on a
-   tail of long box-pixel paths.  Scheduling only: every pixel's result is
-   independent of when it is rendered.  Cached until camera, mesh, frame, tile
-   or path depth change. */
-int tile_order(rt_ctx *c, uint32_t W, uint32_t H, uint32_t hl, uint32_t stripe, uint32_t nr, uint32_t rk,
-               hipStream_t st)
+   maxDepth+1 times with shadow queries at each (rtcommon.h:425-461), and each
+   query costs its traversal steps.  A probe (k_probe_cost) traces every pixel's
+   centre ray and, on a mesh hit, its shadow rays toward the light centres with
+   the real traversal, counting steps; a box pixel is costed at (1 + lights) x
+   (maxDepth + 1) queries of 1.4x the mean probed query.  The queue hands out the
+   most expensive 8x8 tiles first, so the launch does not end on a tail of long
+   pixels (measured: without the step counts the last pixels to finish were mesh
+   pixels of 50 steps per query, handed out late as "cheap").  Scheduling only:
+   every pixel's result is independent of when it is rendered.  Cached until
+   camera, mesh, frame, tile or path depth change. */
+int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
 {
-    std::vector<uint32_t> key = {W, H, hl, stripe, nr, rk, c->max_depth, (uint32_t)c->lights.size(),
-                                 (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32)};
+    const uint32_t W = a.W, hl = a.Hl;
+    std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
+                                 (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks};
     const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
     const uint32_t tx = (W + 7) / 8, ty = (hl + 7) / 8, n_t = tx * ty;
     if (key == c->order_key) return RT_OK;
-    if (c->bvh.stack4 > 64) { /* the wave-coherent probe needs the per-wave stack: keep row-major order */
+    if (a.nodes != reinterpret_cast<const float *>(c->d_nodes4q) || !c->d_nodes4q) {
+        /* the probe walks the compressed tree with its spill layout: other traversal kinds
+           (measurement variants) keep the row-major queue */
         free_dev(c->d_order);
         c->d_order = nullptr;
         c->order_key = key;
         return RT_OK;
     }
     const size_t npx = (size_t)W * hl;
-    if (c->flags_bytes < npx) {
+    if (c->flags_bytes < npx * 4) {
         free_dev(c->d_flags);
         c->d_flags = nullptr;
         c->flags_bytes = 0;
-        HIPCHK(c, hipMalloc(&c->d_flags, npx));
-        c->flags_bytes = npx;
+        HIPCHK(c, hipMalloc(&c->d_flags, npx * 4));
+        c->flags_bytes = npx * 4;
     }
-    const int e = rt_launch_probe(c->d_nodes4, c->d_tris, c->cam, W, H, hl, stripe, nr, rk, c->d_flags, st);
+    const int e = rt_launch_probe_cost(a, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
-    std::vector<uint8_t> f(npx);
-    HIPCHK(c, hipMemcpyAsync(f.data(), c->d_flags, npx, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> f(npx);
+    HIPCHK(c, hipMemcpyAsync(f.data(), c->d_flags, npx * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    const uint64_t c_mesh = 1 + c->lights.size();
-    const uint64_t c_box = (1 + c->lights.size()) * (uint64_t)(c->max_depth + 1);
+    const uint64_t nl = c->lights.size();
+    uint64_t hit_steps = 0, n_hit = 0;
+    for (uint32_t v : f)
+        if (v >> 31) {
+            hit_steps += v & 0x7fffffffu;
+            ++n_hit;
+        }
+    double q_steps = n_hit ? (double)hit_steps / (double)(n_hit * (1 + nl)) : 20.0;
+    if (q_steps < 1.0) q_steps = 1.0;
+    double box_factor = 1.4;
+    if (const char *v = getenv("RT_PROBE_BOX_FACTOR")) box_factor = atof(v); /* tuning knob */
+    const uint64_t c_box = (uint64_t)((double)((1 + nl) * (uint64_t)(c->max_depth + 1)) * q_steps * box_factor);
     std::vector<uint64_t> cost(n_t, 0);
     for (uint32_t y = 0; y < hl; ++y)
-        for (uint32_t x = 0; x < W; ++x) cost[(y / 8) * tx + x / 8] += f[(size_t)y * W + x] ? c_mesh : c_box;
+        for (uint32_t x = 0; x < W; ++x) {
+            const uint32_t v = f[(size_t)y * W + x];
+            cost[(y / 8) * tx + x / 8] += (v >> 31) ? (uint64_t)(v & 0x7fffffffu) + 1 : c_box;
+        }
     std::vector<uint32_t> o(n_t);
     for (uint32_t i = 0; i < n_t; ++i) o[i] = i;
-    std::stable_sort(o.begin(), o.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    std::stable_sort(o.begin(), o.end(), [&](uint32_t p, uint32_t q) { return cost[p] > cost[q]; });
     free_dev(c->d_order);
     c->d_order = nullptr;
     HIPCHK(c, hipMalloc(&c->d_order, n_t * sizeof(uint32_t)));
@@ -417,6 +437,7 @@ int rt_create(int device, rt_ctx **out)
     c->rng.seed(1);
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0"; /* A/B knob */
     if (const char *v = getenv("RT_FETCH_K")) c->fetch_k = (uint32_t)std::max(1, std::min(64, atoi(v))); /* tuning knob */
+    if (const char *v = getenv("RT_FETCH_K_BOX")) c->fetch_k_box = (uint32_t)std::max(1, std::min(64, atoi(v)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
@@ -798,21 +819,41 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         }
         a.spill = c->d_spill;
         a.fetch_k = c->fetch_k;
+        a.fetch_k_box = c->fetch_k_box;
         a.tile_order = nullptr;
         a.pixel_flags = nullptr;
         if (c->schedule) {
-            const int ro = tile_order(c, W, H, hl, stripe, nr, rk, st);
+            const int ro = tile_order(c, a, blocks, st);
             if (ro != RT_OK) return ro;
             a.tile_order = c->d_order;
-            if (a.tile_order) a.pixel_flags = c->d_flags;
+            a.pixel_flags = a.tile_order ? c->d_flags : nullptr;
         }
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
             fprintf(stderr, "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p\n", (void *)c,
                     trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order);
         HIPCHK(c, hipEventRecord(c->ev0, st));
+        /* diagnostics: per-pixel start/finish/queries/steps of a counting launch, dumped raw */
+        const char *stats_path = c->counting ? getenv("RT_PIXEL_STATS") : nullptr;
+        uint32_t *d_stats = nullptr;
+        a.pixel_stats = nullptr;
+        if (stats_path) {
+            HIPCHK(c, hipMalloc(&d_stats, (size_t)W * hl * 16));
+            HIPCHK(c, hipMemsetAsync(d_stats, 0, (size_t)W * hl * 16, st));
+            a.pixel_stats = d_stats;
+        }
         e = rt_launch_tris(a, trav, c->counting, blocks, st);
         HIPCHK(c, hipEventRecord(c->ev1, st));
+        if (d_stats) {
+            std::vector<uint32_t> h((size_t)W * hl * 4);
+            HIPCHK(c, hipMemcpyAsync(h.data(), d_stats, h.size() * 4, hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            (void)hipFree(d_stats);
+            if (FILE *f = fopen(stats_path, "wb")) {
+                fwrite(h.data(), 4, h.size(), f);
+                fclose(f);
+            }
+        }
     } else {
         RtSphLaunch a;
         a.out = dout;

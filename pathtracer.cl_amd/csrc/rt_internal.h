@@ -30,7 +30,7 @@
 #define RT_MIX_PLANES 1 /* node planes through v_perm_b32 + v_fma_mix_f32 (rt_kernels.hip trav_step_q) */
 #endif
 #ifndef RT_PRIO
-#define RT_PRIO 0 /* wave issue priority for waves holding box pixels (long sample chains) */
+#define RT_PRIO 2 /* wave issue priority for waves holding box pixels (long sample chains) */
 #endif
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
@@ -119,7 +119,11 @@ struct RtTriLaunch {
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
     uint32_t fetch_k;           /* resumable queries: completed lanes that end a stepping round */
-    const uint8_t *pixel_flags; /* probe: 1 = the pixel's centre ray hits the mesh (NULL: unknown) */
+    const uint32_t *pixel_flags; /* cost probe per pixel: bit 31 = centre ray hits the mesh, low bits = steps
+                                    (NULL: no probe) */
+    uint32_t fetch_k_box;       /* fetch_k of waves holding box pixels (pixel_flags 0) */
+    uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =
+                                   start / finish (s_memrealtime, 100 MHz, low 32 bits), queries, steps */
 };
 
 struct RtSphLaunch {
@@ -144,8 +148,7 @@ int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
                          void *stream);
 /* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
-int rt_launch_probe(const float *nodes4, const float *tris, const rt_camera &cam, uint32_t W, uint32_t H, uint32_t Hl,
-                    uint32_t stripe, uint32_t n_ranks, uint32_t rank, uint8_t *flags, void *stream);
+int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed
    buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,

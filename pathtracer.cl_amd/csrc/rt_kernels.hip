@@ -761,7 +761,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const float hh = uniform_f(((float)a.H) / 2.0f);
     const float mix_t = uniform_f(a.progressive > 0 ? 1.0f / (float)a.progressive : 0.0f);
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
-    const int fetch_k = (int)a.fetch_k;
+    const int fetch_k_all = (int)a.fetch_k;
+    const int fetch_k_box = (int)a.fetch_k_box;
 
     int mode = M_IDLE;
     uint32_t x = 0, yl = 0; /* pixel column and local row (global row / seed slot derived) */
@@ -777,7 +778,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     float stmax = 0.0f;
     bool tri_hit = false;
     bool running = false; /* a resumable query is in flight */
-    [[maybe_unused]] bool costly = false; /* the pixel is a box pixel (long sample chain), from the probe */
+    bool costly = false; /* the pixel is a box pixel (long sample chain), from the probe */
     bool fin = false;     /* the lane's query completed: ts.best / ts.best_t hold its result */
     TravState ts;
     ts.node = 0;
@@ -790,6 +791,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const unsigned long long t_k0 = COUNT ? wave_clock() : 0ull;
     /* counting launches: this pixel's start clock, queries and traversal steps */
     unsigned long long pix_t0 = 0, pix_q = 0, pix_steps = 0;
+    [[maybe_unused]] uint32_t pix_rt0 = 0;
 
     for (;;) {
         const unsigned long long t_d0 = COUNT ? wave_clock() : 0ull;
@@ -930,8 +932,15 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
                     mode = M_IDLE;
-                    if (RT_PRIO) costly = false;
+                    costly = false;
                     if (COUNT) {
+                        if (a.pixel_stats) {
+                            uint32_t *ps = a.pixel_stats + 4 * ((size_t)yl * a.W + x);
+                            ps[0] = pix_rt0;
+                            ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                            ps[2] = (uint32_t)pix_q;
+                            ps[3] = (uint32_t)pix_steps;
+                        }
                         const unsigned long long dt = wave_clock() - pix_t0;
                         cnt[10] = dt > cnt[10] ? dt : cnt[10];
                         cnt[11] = pix_q > cnt[11] ? pix_q : cnt[11];
@@ -970,11 +979,12 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         seed.y = a.seeds[plane + slot];
                         if (COUNT) {
                             pix_t0 = wave_clock();
+                            if (a.pixel_stats) pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                             pix_q = pix_steps = 0;
                         }
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
-                        if (RT_PRIO) costly = a.pixel_flags && !a.pixel_flags[(size_t)yl * a.W + x];
+                        costly = a.pixel_flags && !(a.pixel_flags[(size_t)yl * a.W + x] >> 31);
                         if (spp > 0) {
                             mode = M_NEWSAMPLE;
                         } else { /* no samples: 0/0 pixels, seeds untouched (raytracer.cl:234-242) */
@@ -1018,6 +1028,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                issue first; scheduling only */
             if (__any(costly)) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
+        } else if (RT_PRIO == 3) {
+            if (__any(costly)) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
         } else if (RT_PRIO == 2) {
             const int nc = __popcll(__ballot(costly));
             if (nc > 16) __builtin_amdgcn_s_setprio(3);
@@ -1046,6 +1059,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 }
             }
             const unsigned long long t_c0 = COUNT ? wave_clock() : 0ull;
+            /* a wave holding box pixels (the long serial chains that set the frame time)
+               leaves the stepping rounds after fewer completed queries: less idling on the
+               critical path, at the price of more (less full) shading passes */
+            const int fetch_k = __any(costly) ? fetch_k_box : fetch_k_all;
             for (;;) {
                 /* four steps per exit check (fewer wave-level ballots and branches) */
 #pragma unroll
@@ -1321,31 +1338,54 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     }
 }
 
-/* Scheduling probe: one pixel-centre camera ray per pixel (8x8 tiles, a wave per
-   tile: coherent, so the wave-coherent traversal), flag = the primary ray hits
-   the mesh.  Used only to order the pixel queue (expensive tiles first); no
-   result of the render depends on it. */
-__global__ __launch_bounds__(RT_BLOCK) void k_probe(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
-                                                    rt_camera cam, uint32_t W, uint32_t H, uint32_t Hl,
-                                                    uint32_t stripe, uint32_t n_ranks, uint32_t rank,
-                                                    uint8_t *__restrict__ flags)
+/* Cost probe for the LPT pixel queue (rt_host.cpp tile_order): per pixel, the centre
+   camera ray's closest-hit query and, when it hits the mesh, one shadow query per light
+   from the hit point toward the light's centre — the per-lane compressed traversal of the
+   real kernel, counting its steps.  out[p] = (1 << 31 if the mesh is hit) | steps.  A
+   persistent grid (the main kernel's) with grid-stride pixels, so the main kernel's
+   traversal spill area serves it.  Scheduling only: no result depends on it. */
+__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLaunch a, uint32_t *__restrict__ out)
 {
-    __shared__ int s_wstack[(RT_BLOCK / 64) * kWaveStack];
-    const uint32_t tiles_x = (W + 7u) >> 3;
-    const uint32_t g = blockIdx.x * RT_BLOCK + threadIdx.x;
-    const uint32_t tile = g >> 6, in = g & 63u;
-    const uint32_t x = (tile % tiles_x) * 8u + (in & 7u);
-    const uint32_t yl = (tile / tiles_x) * 8u + (in >> 3);
-    if (tile >= tiles_x * ((Hl + 7u) >> 3)) return; /* whole waves exit together */
-    const bool valid = x < W && yl < Hl;
-    const uint32_t y = global_row(valid ? yl : 0u, stripe, n_ranks, rank);
-    const V3 o = v3(cam.position.x, cam.position.y, cam.position.z);
-    const V3 d = camera_dir(cam, ((float)x + 0.5f) - ((float)W) / 2.0f, ((float)y + 0.5f) - ((float)H) / 2.0f);
-    float t = kInf;
-    TravCounts tc = {0u, 0u, 0u};
-    const int hit = traverse_packet4<false>(nodes, tris, o, d, RT_SMALL_F, t, false,
-                                            s_wstack + (threadIdx.x >> 6) * kWaveStack, tc);
-    if (valid) flags[(size_t)yl * W + x] = hit >= 0 ? 1 : 0;
+    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
+    Stack stk;
+    stk.init(s_stack, a.spill, a.spill_cap);
+    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
+    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
+    const uint32_t npx = a.W * a.Hl;
+    const uint32_t stride = gridDim.x * RT_BLOCK;
+    const uint32_t rounds = (npx + stride - 1) / stride; /* uniform trip count: whole waves iterate together */
+    for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t p = r * stride + blockIdx.x * RT_BLOCK + threadIdx.x;
+        const bool valid = p < npx;
+        const uint32_t x = valid ? p % a.W : 0u, yl = valid ? p / a.W : 0u;
+        const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+        const V3 o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+        const V3 d = camera_dir(a.cam, ((float)x + 0.5f) - ((float)a.W) / 2.0f, ((float)y + 0.5f) - ((float)a.H) / 2.0f);
+        TravCounts tc = {0u, 0u, 0u};
+        float t = kInf;
+        const int hit = traverse<RT_TRAV_BVH4Q, true>(nodes, tris, a.n_tris, o, d, RT_SMALL_F, t, false, stk, tc);
+        uint32_t steps = tc.nodes + tc.leaves;
+        if (hit >= 0) {
+            const float4 e1 = tris[3 * hit + 1], e2 = tris[3 * hit + 2];
+            const V3 hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z));
+            const V3 so = v3(o.x + d.x * t + hn.x * RT_SMALL_F, o.y + d.y * t + hn.y * RT_SMALL_F,
+                             o.z + d.z * t + hn.z * RT_SMALL_F);
+            for (uint32_t l = 0; l < a.n_lights; ++l) {
+                const rt_sphere &L = a.lights[l];
+                const V3 lc = v3(L.center.x, L.center.y, L.center.z);
+                V3 sd = v3(lc.x - so.x, lc.y - so.y, lc.z - so.z);
+                const float il = rt_rsqrtf(sd.x * sd.x + sd.y * sd.y + sd.z * sd.z);
+                sd = v3(sd.x * il, sd.y * il, sd.z * il);
+                float st = intersect_sphere(so, sd, RT_SMALL_F, lc, L.radius) - RT_SMALL_F;
+                if (st > RT_SMALL_F && sd.x * hn.x + sd.y * hn.y + sd.z * hn.z > 0.0f) {
+                    TravCounts ts = {0u, 0u, 0u};
+                    (void)traverse<RT_TRAV_BVH4Q, true>(nodes, tris, a.n_tris, so, sd, RT_SMALL_F, st, true, stk, ts);
+                    steps += ts.nodes + ts.leaves;
+                }
+            }
+        }
+        if (valid) out[p] = (hit >= 0 ? 0x80000000u : 0u) | (steps & 0x7fffffffu);
+    }
 }
 
 /* Seed-row halo pack / unpack (multi-GPU progressive sphere frames). */
@@ -1466,12 +1506,9 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
     return 0;
 }
 
-int rt_launch_probe(const float *nodes4, const float *tris, const rt_camera &cam, uint32_t W, uint32_t H, uint32_t Hl,
-                    uint32_t stripe, uint32_t n_ranks, uint32_t rank, uint8_t *flags, void *stream)
+int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream)
 {
-    const uint32_t tiles = ((W + 7u) >> 3) * ((Hl + 7u) >> 3);
-    dim3 grid((tiles * 64u + RT_BLOCK - 1) / RT_BLOCK), block(RT_BLOCK);
-    hipLaunchKernelGGL(k_probe, grid, block, 0, (hipStream_t)stream, reinterpret_cast<const float4 *>(nodes4),
-                       reinterpret_cast<const float4 *>(tris), cam, W, H, Hl, stripe, n_ranks, rank, flags);
+    hipLaunchKernelGGL(k_probe_cost, dim3((unsigned)grid_blocks), dim3(RT_BLOCK), 0, (hipStream_t)stream, a, out);
     return (int)hipGetLastError();
 }
+

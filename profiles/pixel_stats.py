@@ -1,0 +1,75 @@
+"""Where does the dragon frame's time go, pixel by pixel?  One counting launch with
+RT_PIXEL_STATS (per-pixel start / finish clock, queries, traversal steps), then: the finish
+time distribution, the last pixels to finish and what they are (probe: box or mesh pixel),
+and how the frame's last milliseconds are spent.  GPU box.
+
+    python profiles/pixel_stats.py [out.json]
+"""
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    import torch
+    import ptload
+
+    dump = "/tmp/rt_pixel_stats.bin"
+    os.environ["RT_PIXEL_STATS"] = dump
+    pt = ptload.load()
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 16
+    rt = pt.RayTracer(0)
+    rt.setSpheres(sc.ply_scene())
+    c = sc.PLY_CAMERA
+    rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS["dragon"]))
+    out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
+    rt.rayTrace(out, W, H, 0, kernel=2)
+    plain_ms = rt.lastKernelMs()
+    rt.setCounting(True)
+    rt.rayTrace(out, W, H, 0, kernel=2)
+    count_ms = rt.lastKernelMs()
+    s = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)
+    t0 = s[..., 0].min()
+    start = (s[..., 0] - t0) / 1e5  # ms (100 MHz)
+    fin = (s[..., 1] - t0) / 1e5
+    q = s[..., 2]
+    steps = s[..., 3]
+    dur = fin - start
+    end = fin.max()
+    res = {"plain_ms": plain_ms, "counting_ms": count_ms, "span_ms": float(end),
+           "finish_pct": {p: float(np.percentile(fin, p)) for p in (50, 90, 99, 99.9, 100)},
+           "dur_pct": {p: float(np.percentile(dur, p)) for p in (50, 90, 99, 99.9, 100)},
+           "queries_pct": {p: float(np.percentile(q, p)) for p in (50, 90, 99, 100)},
+           "pixels_running_at_pct_of_span": {}}
+    for f in (0.5, 0.7, 0.8, 0.9, 0.95, 0.99):
+        t = f * end
+        res["pixels_running_at_pct_of_span"][f] = int(((start <= t) & (fin > t)).sum())
+    # the 20 last finishers
+    idx = np.argsort(fin.ravel())[-20:]
+    res["last"] = [{"x": int(i % W), "y": int(i // W), "start": round(float(start.ravel()[i]), 2),
+                    "finish": round(float(fin.ravel()[i]), 2), "queries": int(q.ravel()[i]),
+                    "steps": int(steps.ravel()[i])} for i in idx]
+    # costly pixels: many queries
+    heavy = q > 2 * np.median(q)
+    res["heavy_pixels"] = int(heavy.sum())
+    res["heavy_start_pct"] = {p: float(np.percentile(start[heavy], p)) for p in (50, 90, 100)}
+    res["heavy_dur_pct"] = {p: float(np.percentile(dur[heavy], p)) for p in (10, 50, 90, 100)}
+    res["light_dur_pct"] = {p: float(np.percentile(dur[~heavy], p)) for p in (10, 50, 90, 100)}
+    txt = json.dumps(res, indent=1)
+    print(txt)
+    if len(sys.argv) > 1:
+        Path(sys.argv[1]).write_text(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -333,10 +333,11 @@ int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
    its paths: a camera ray that hits the mesh ends after one shadow query per
    light (rtcommon.h:411-421), one that misses bounces off the box up to
    maxDepth+1 times with shadow queries at each (rtcommon.h:425-461), and each
-   query costs its traversal steps.  A probe (k_probe_cost) traces every pixel's
-   centre ray and, on a mesh hit, its shadow rays toward the light centres with
-   the real traversal, counting steps; a box pixel is costed at (1 + lights) x
-   (maxDepth + 1) queries of 1.4x the mean probed query.  The queue hands out the
+   query costs its traversal steps.  A probe (k_probe_cost) traces a 2x2 grid of
+   camera rays per pixel and, on mesh hits, their shadow rays toward the light
+   centres with the real traversal, counting steps; a probe ray that misses stands
+   for a box path of (1 + lights) x (maxDepth + 1) queries of 1.4x the mean
+   probed query.  The queue hands out the
    most expensive 8x8 tiles first, so the launch does not end on a tail of long
    pixels (measured: without the step counts the last pixels to finish were mesh
    pixels of 50 steps per query, handed out late as "cheap").  Scheduling only:
@@ -374,21 +375,23 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     HIPCHK(c, hipStreamSynchronize(st));
     const uint64_t nl = c->lights.size();
     uint64_t hit_steps = 0, n_hit = 0;
-    for (uint32_t v : f)
-        if (v >> 31) {
-            hit_steps += v & 0x7fffffffu;
-            ++n_hit;
-        }
-    double q_steps = n_hit ? (double)hit_steps / (double)(n_hit * (1 + nl)) : 20.0;
+    for (uint32_t v : f) {
+        hit_steps += v & 0x1fffffffu;
+        n_hit += v >> 29;
+    }
+    /* mean steps of one probed query (a hit ray's closest-hit + shadow queries, or a missing
+       ray's closest-hit query, in the sums) */
+    double q_steps = n_hit ? (double)hit_steps / (double)(n_hit * (1 + nl) + (4 * npx - n_hit)) : 20.0;
     if (q_steps < 1.0) q_steps = 1.0;
     double box_factor = 1.4;
     if (const char *v = getenv("RT_PROBE_BOX_FACTOR")) box_factor = atof(v); /* tuning knob */
-    const uint64_t c_box = (uint64_t)((double)((1 + nl) * (uint64_t)(c->max_depth + 1)) * q_steps * box_factor);
-    std::vector<uint64_t> cost(n_t, 0);
+    /* one probe ray that misses stands for a box path: (1 + lights) x (maxDepth + 1) queries */
+    const double c_box = (double)((1 + nl) * (uint64_t)(c->max_depth + 1)) * q_steps * box_factor;
+    std::vector<double> cost(n_t, 0.0);
     for (uint32_t y = 0; y < hl; ++y)
         for (uint32_t x = 0; x < W; ++x) {
             const uint32_t v = f[(size_t)y * W + x];
-            cost[(y / 8) * tx + x / 8] += (v >> 31) ? (uint64_t)(v & 0x7fffffffu) + 1 : c_box;
+            cost[(y / 8) * tx + x / 8] += (double)(v & 0x1fffffffu) + (double)(4u - (v >> 29)) * c_box + 1.0;
         }
     std::vector<uint32_t> o(n_t);
     for (uint32_t i = 0; i < n_t; ++i) o[i] = i;

@@ -119,7 +119,7 @@ struct RtTriLaunch {
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
     uint32_t fetch_k;           /* resumable queries: completed lanes that end a stepping round */
-    const uint32_t *pixel_flags; /* cost probe per pixel: bit 31 = centre ray hits the mesh, low bits = steps
+    const uint32_t *pixel_flags; /* cost probe per pixel: mesh hits of its 4 probe rays << 29 | their steps
                                     (NULL: no probe) */
     uint32_t fetch_k_box;       /* fetch_k of waves holding box pixels (pixel_flags 0) */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =

@@ -984,7 +984,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         }
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
-                        costly = a.pixel_flags && !(a.pixel_flags[(size_t)yl * a.W + x] >> 31);
+                        /* some of the probe's rays missed the mesh: box paths, long chains */
+                        costly = a.pixel_flags && (a.pixel_flags[(size_t)yl * a.W + x] >> 29) < 4u;
                         if (spp > 0) {
                             mode = M_NEWSAMPLE;
                         } else { /* no samples: 0/0 pixels, seeds untouched (raytracer.cl:234-242) */
@@ -1338,12 +1339,14 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     }
 }
 
-/* Cost probe for the LPT pixel queue (rt_host.cpp tile_order): per pixel, the centre
-   camera ray's closest-hit query and, when it hits the mesh, one shadow query per light
-   from the hit point toward the light's centre — the per-lane compressed traversal of the
-   real kernel, counting its steps.  out[p] = (1 << 31 if the mesh is hit) | steps.  A
-   persistent grid (the main kernel's) with grid-stride pixels, so the main kernel's
-   traversal spill area serves it.  Scheduling only: no result depends on it. */
+/* Cost probe for the LPT pixel queue (rt_host.cpp tile_order): per pixel, a 2x2 grid of
+   camera rays (the pixel's samples are stratified over its area, so silhouette pixels mix
+   mesh and box paths) — each ray's closest-hit query and, when it hits the mesh, one shadow
+   query per light from the hit point toward the light's centre — with the per-lane
+   compressed traversal of the real kernel, counting its steps.
+   out[p] = (mesh hits, 0..4) << 29 | steps of all those queries.  A persistent grid (the
+   main kernel's) with grid-stride pixels, so the main kernel's traversal spill area serves
+   it.  Scheduling only: no result depends on it. */
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLaunch a, uint32_t *__restrict__ out)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
@@ -1360,12 +1363,16 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
         const uint32_t x = valid ? p % a.W : 0u, yl = valid ? p / a.W : 0u;
         const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
         const V3 o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
-        const V3 d = camera_dir(a.cam, ((float)x + 0.5f) - ((float)a.W) / 2.0f, ((float)y + 0.5f) - ((float)a.H) / 2.0f);
-        TravCounts tc = {0u, 0u, 0u};
-        float t = kInf;
-        const int hit = traverse<RT_TRAV_BVH4Q, true>(nodes, tris, a.n_tris, o, d, RT_SMALL_F, t, false, stk, tc);
-        uint32_t steps = tc.nodes + tc.leaves;
-        if (hit >= 0) {
+        uint32_t steps = 0, hits = 0;
+        for (int k = 0; k < 4; ++k) {
+            const float fx = (float)x + ((k & 1) ? 0.75f : 0.25f), fy = (float)y + ((k & 2) ? 0.75f : 0.25f);
+            const V3 d = camera_dir(a.cam, fx - ((float)a.W) / 2.0f, fy - ((float)a.H) / 2.0f);
+            TravCounts tc = {0u, 0u, 0u};
+            float t = kInf;
+            const int hit = traverse<RT_TRAV_BVH4Q, true>(nodes, tris, a.n_tris, o, d, RT_SMALL_F, t, false, stk, tc);
+            steps += tc.nodes + tc.leaves;
+            if (hit < 0) continue;
+            ++hits;
             const float4 e1 = tris[3 * hit + 1], e2 = tris[3 * hit + 2];
             const V3 hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z));
             const V3 so = v3(o.x + d.x * t + hn.x * RT_SMALL_F, o.y + d.y * t + hn.y * RT_SMALL_F,
@@ -1384,7 +1391,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
                 }
             }
         }
-        if (valid) out[p] = (hit >= 0 ? 0x80000000u : 0u) | (steps & 0x7fffffffu);
+        if (valid) out[p] = (hits << 29) | (steps < (1u << 29) ? steps : (1u << 29) - 1u);
     }
 }
 

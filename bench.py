@@ -31,7 +31,8 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 (per XCD, 32 MiB aggregate) ~34.5 TB/s
 NODE_BYTES = {"bvh": 64, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
 # bytes read per triangle test: the whole 48-B record (one-record steps of the compressed traversal), else
 # v0+orig (16), e1 (12), e2 (12); csrc/rt_internal.h
@@ -255,6 +256,9 @@ def main():
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                # the BVH + triangles are L2/MALL-resident (PMC traffic << algorithmic bytes), so
+                # the algorithmic rate is also stated against the aggregate L2 bandwidth
+                "l2_peak": L2_PEAK_GBS, "frac_of_l2": round(achieved / L2_PEAK_GBS, 4),
                 "kernel": f"k_tris<{args.traversal.upper()}>" if kernel == 2 else "k_spheres",
                 "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
                 "nodes_per_ray": round(cnt["nodes_visited"] / max(rays_cnt, 1), 2),

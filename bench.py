@@ -31,7 +31,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 (per XCD, 32 MiB aggregate) ~34.5 TB/s
 NODE_BYTES = {"bvh": 64, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
 # bytes read per triangle test: the whole 48-B record (one-record steps of the compressed traversal), else

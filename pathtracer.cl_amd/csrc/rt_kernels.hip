@@ -791,7 +791,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const unsigned long long t_k0 = COUNT ? wave_clock() : 0ull;
     /* counting launches: this pixel's start clock, queries and traversal steps */
     unsigned long long pix_t0 = 0, pix_q = 0, pix_steps = 0;
-    [[maybe_unused]] uint32_t pix_rt0 = 0;
+    uint32_t pix_rt0 = 0; /* pixel start (s_memrealtime), RT_PIXEL_STATS diagnostics */
 
     for (;;) {
         const unsigned long long t_d0 = COUNT ? wave_clock() : 0ull;
@@ -933,14 +933,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     a.seeds[plane + slot] = seed.y;
                     mode = M_IDLE;
                     costly = false;
+                    if (a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
+                        uint32_t *ps = a.pixel_stats + 4 * ((size_t)yl * a.W + x);
+                        ps[0] = pix_rt0;
+                        ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        ps[2] = COUNT ? (uint32_t)pix_q : 0u;
+                        ps[3] = COUNT ? (uint32_t)pix_steps : 0u;
+                    }
                     if (COUNT) {
-                        if (a.pixel_stats) {
-                            uint32_t *ps = a.pixel_stats + 4 * ((size_t)yl * a.W + x);
-                            ps[0] = pix_rt0;
-                            ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                            ps[2] = (uint32_t)pix_q;
-                            ps[3] = (uint32_t)pix_steps;
-                        }
                         const unsigned long long dt = wave_clock() - pix_t0;
                         cnt[10] = dt > cnt[10] ? dt : cnt[10];
                         cnt[11] = pix_q > cnt[11] ? pix_q : cnt[11];
@@ -977,9 +977,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
+                        if (a.pixel_stats) pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         if (COUNT) {
                             pix_t0 = wave_clock();
-                            if (a.pixel_stats) pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                             pix_q = pix_steps = 0;
                         }
                         acc_x = acc_y = acc_z = 0.0f;

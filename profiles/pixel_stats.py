@@ -1,5 +1,6 @@
-"""Where does the dragon frame's time go, pixel by pixel?  One counting launch with
-RT_PIXEL_STATS (per-pixel start / finish clock, queries, traversal steps), then: the finish
+"""Where does the dragon frame's time go, pixel by pixel?  A plain launch with
+RT_PIXEL_STATS (per-pixel start / finish clocks) and a counting one (queries, traversal
+steps per pixel), then: the finish
 time distribution, the last pixels to finish and what they are (probe: box or mesh pixel),
 and how the frame's last milliseconds are spent.  GPU box.
 
@@ -33,17 +34,19 @@ def main():
     rt.setMaxPathDepth(6)
     rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS["dragon"]))
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
+    rt.rayTrace(out, W, H, 0, kernel=2)  # probe + warm
     rt.rayTrace(out, W, H, 0, kernel=2)
     plain_ms = rt.lastKernelMs()
+    s = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)  # timing: the plain launch
     rt.setCounting(True)
     rt.rayTrace(out, W, H, 0, kernel=2)
     count_ms = rt.lastKernelMs()
-    s = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)
+    sc_ = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)  # queries / steps
     t0 = s[..., 0].min()
     start = (s[..., 0] - t0) / 1e5  # ms (100 MHz)
     fin = (s[..., 1] - t0) / 1e5
-    q = s[..., 2]
-    steps = s[..., 3]
+    q = sc_[..., 2]
+    steps = sc_[..., 3]
     dur = fin - start
     end = fin.max()
     res = {"plain_ms": plain_ms, "counting_ms": count_ms, "span_ms": float(end),

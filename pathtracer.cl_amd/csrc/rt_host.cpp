@@ -95,6 +95,7 @@ struct rt_ctx {
     bool schedule = true;
     uint32_t fetch_k = 16;
     uint32_t fetch_k_box = 16; /* waves holding box pixels (probe) */
+    uint32_t probe_n = 2;      /* cost probe: probe_n x probe_n rays per pixel (RT_PROBE_N) */
     int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
@@ -368,20 +369,23 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         HIPCHK(c, hipMalloc(&c->d_flags, npx * 4));
         c->flags_bytes = npx * 4;
     }
-    const int e = rt_launch_probe_cost(a, blocks, c->d_flags, st);
+    RtTriLaunch pa = a;
+    pa.probe_n = c->probe_n;
+    const int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
     std::vector<uint32_t> f(npx);
     HIPCHK(c, hipMemcpyAsync(f.data(), c->d_flags, npx * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     const uint64_t nl = c->lights.size();
     uint64_t hit_steps = 0, n_hit = 0;
+    const uint64_t pn2 = (uint64_t)c->probe_n * c->probe_n;
     for (uint32_t v : f) {
-        hit_steps += v & 0x1fffffffu;
-        n_hit += v >> 29;
+        hit_steps += v & RT_PROBE_STEP_MASK;
+        n_hit += v >> RT_PROBE_HIT_SHIFT;
     }
     /* mean steps of one probed query (a hit ray's closest-hit + shadow queries, or a missing
        ray's closest-hit query, in the sums) */
-    double q_steps = n_hit ? (double)hit_steps / (double)(n_hit * (1 + nl) + (4 * npx - n_hit)) : 20.0;
+    double q_steps = n_hit ? (double)hit_steps / (double)(n_hit * (1 + nl) + (pn2 * npx - n_hit)) : 20.0;
     if (q_steps < 1.0) q_steps = 1.0;
     double box_factor = 1.4;
     if (const char *v = getenv("RT_PROBE_BOX_FACTOR")) box_factor = atof(v); /* tuning knob */
@@ -395,7 +399,8 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     for (uint32_t y = 0; y < hl; ++y)
         for (uint32_t x = 0; x < W; ++x) {
             const uint32_t v = f[(size_t)y * W + x];
-            const double pc = (double)(v & 0x1fffffffu) + (double)(4u - (v >> 29)) * c_box + 1.0;
+            const double pc = ((double)(v & RT_PROBE_STEP_MASK) +
+                               (double)(pn2 - (v >> RT_PROBE_HIT_SHIFT)) * c_box) * (4.0 / (double)pn2) + 1.0;
             const uint32_t t = (y / 8) * tx + x / 8;
             cost[t] += pc;
             cmax[t] = std::max(cmax[t], pc);
@@ -449,6 +454,7 @@ int rt_create(int device, rt_ctx **out)
     c->rng.seed(1);
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0"; /* A/B knob */
     if (const char *v = getenv("RT_FETCH_K")) c->fetch_k = (uint32_t)std::max(1, std::min(64, atoi(v))); /* tuning knob */
+    if (const char *v = getenv("RT_PROBE_N")) c->probe_n = (uint32_t)std::max(1, std::min(5, atoi(v)));
     if (const char *v = getenv("RT_FETCH_K_BOX")) c->fetch_k_box = (uint32_t)std::max(1, std::min(64, atoi(v)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -839,6 +845,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             if (ro != RT_OK) return ro;
             a.tile_order = c->d_order;
             a.pixel_flags = a.tile_order ? c->d_flags : nullptr;
+            a.probe_n = c->probe_n;
         }
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */

@@ -32,6 +32,9 @@
 #ifndef RT_PRIO
 #define RT_PRIO 2 /* wave issue priority for waves holding box pixels (long sample chains) */
 #endif
+/* cost-probe word: hits (0..25) in the top 5 bits, traversal steps below */
+#define RT_PROBE_HIT_SHIFT 27
+#define RT_PROBE_STEP_MASK ((1u << RT_PROBE_HIT_SHIFT) - 1u)
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif
@@ -119,8 +122,9 @@ struct RtTriLaunch {
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */
     uint32_t fetch_k;           /* resumable queries: completed lanes that end a stepping round */
-    const uint32_t *pixel_flags; /* cost probe per pixel: mesh hits of its 4 probe rays << 29 | their steps
-                                    (NULL: no probe) */
+    const uint32_t *pixel_flags; /* cost probe per pixel: mesh hits of its probe rays << RT_PROBE_HIT_SHIFT |
+                                    their steps (NULL: no probe) */
+    uint32_t probe_n;            /* probe rays per pixel: probe_n x probe_n (<= 5) */
     uint32_t fetch_k_box;       /* fetch_k of waves holding box pixels (pixel_flags 0) */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =
                                    start / finish (s_memrealtime, 100 MHz, low 32 bits), queries, steps */

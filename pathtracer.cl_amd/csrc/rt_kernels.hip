@@ -985,7 +985,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
                         /* some of the probe's rays missed the mesh: box paths, long chains */
-                        costly = a.pixel_flags && (a.pixel_flags[(size_t)yl * a.W + x] >> 29) < 4u;
+                        costly = a.pixel_flags &&
+                                 (a.pixel_flags[(size_t)yl * a.W + x] >> RT_PROBE_HIT_SHIFT) < a.probe_n * a.probe_n;
                         if (spp > 0) {
                             mode = M_NEWSAMPLE;
                         } else { /* no samples: 0/0 pixels, seeds untouched (raytracer.cl:234-242) */
@@ -1339,12 +1340,12 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     }
 }
 
-/* Cost probe for the LPT pixel queue (rt_host.cpp tile_order): per pixel, a 2x2 grid of
-   camera rays (the pixel's samples are stratified over its area, so silhouette pixels mix
+/* Cost probe for the LPT pixel queue (rt_host.cpp tile_order): per pixel, an n x n grid
+   (probe_n, default 2) of camera rays (the pixel's samples are stratified over its area, so silhouette pixels mix
    mesh and box paths) — each ray's closest-hit query and, when it hits the mesh, one shadow
    query per light from the hit point toward the light's centre — with the per-lane
    compressed traversal of the real kernel, counting its steps.
-   out[p] = (mesh hits, 0..4) << 29 | steps of all those queries.  A persistent grid (the
+   out[p] = (mesh hits, 0..n^2) << RT_PROBE_HIT_SHIFT | steps of all those queries.  A persistent grid (the
    main kernel's) with grid-stride pixels, so the main kernel's traversal spill area serves
    it.  Scheduling only: no result depends on it. */
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLaunch a, uint32_t *__restrict__ out)
@@ -1364,8 +1365,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
         const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
         const V3 o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
         uint32_t steps = 0, hits = 0;
-        for (int k = 0; k < 4; ++k) {
-            const float fx = (float)x + ((k & 1) ? 0.75f : 0.25f), fy = (float)y + ((k & 2) ? 0.75f : 0.25f);
+        const uint32_t pn = a.probe_n;
+        const float step = 1.0f / (float)pn;
+        for (uint32_t k = 0; k < pn * pn; ++k) {
+            const float fx = (float)x + ((float)(k % pn) + 0.5f) * step, fy = (float)y + ((float)(k / pn) + 0.5f) * step;
             const V3 d = camera_dir(a.cam, fx - ((float)a.W) / 2.0f, fy - ((float)a.H) / 2.0f);
             TravCounts tc = {0u, 0u, 0u};
             float t = kInf;
@@ -1391,7 +1394,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
                 }
             }
         }
-        if (valid) out[p] = (hits << 29) | (steps < (1u << 29) ? steps : (1u << 29) - 1u);
+        if (valid) out[p] = (hits << RT_PROBE_HIT_SHIFT) | (steps < RT_PROBE_STEP_MASK ? steps : RT_PROBE_STEP_MASK);
     }
 }
 

@@ -1066,9 +1066,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                critical path, at the price of more (less full) shading passes */
             const int fetch_k = __any(costly) ? fetch_k_box : fetch_k_all;
             for (;;) {
-                /* four steps per exit check (fewer wave-level ballots and branches) */
+                /* RT_STEP_UNROLL steps per exit check (fewer wave-level ballots and branches) */
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < RT_STEP_UNROLL; ++u) {
                     if (running) {
                         const bool shadow = (mode == M_SHADOW);
                         TravCounts tc = {0u, 0u, 0u};

@@ -621,3 +621,36 @@ def test_huge_coordinates_fall_back_to_full_precision_nodes(tracer, pt):
     for key, got in res.items():
         np.testing.assert_array_equal(got[0], ref[0], err_msg=str(key))
         np.testing.assert_array_equal(bits(got[1]), bits(ref[1]), err_msg=str(key))
+
+
+def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
+    """The pixel queue's order (step-counting probe, LPT key), the box-wave priority and the
+    probe density are scheduling only: a frame with box and mesh pixels, 16 spp, renders to
+    the same bits and seeds with the queue row-major (RT_SCHEDULE=0), with the default
+    schedule, and with other probe / key settings."""
+    sc = pt.scenes
+    W, H, sr = 160, 120, 4
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    seeds = sc.default_seeds(Wp, Hp, skip=7)
+    frames = []
+    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_PROBE_N": "1", "RT_LPT_MAX": "0"}, {"RT_PROBE_N": "3"}):
+        for k in ("RT_SCHEDULE", "RT_PROBE_N", "RT_LPT_MAX"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        rt = pt.RayTracer(0)  # the knobs are read when the context is created
+        rt.setSpheres(sc.ply_scene())
+        c = sc.PLY_CAMERA
+        rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        out = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        frames.append((bits(out).copy(), rt.getSeeds().copy()))
+        rt.close()
+    for f, s in frames[1:]:
+        np.testing.assert_array_equal(f, frames[0][0])
+        np.testing.assert_array_equal(s, frames[0][1])

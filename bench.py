@@ -297,6 +297,9 @@ def main():
         "extra_warmup_steps": extra_warm,
         "ms_per_step": round(ms_step, 3),
         "frames_per_sec": round(steps * (world if frames_per_rank else 1) / elapsed, 4),
+        # the same frames counting only the queries that ran a traversal (rank 0's counting
+        # launch share; DESIGN.md §5: shadow rays answered without one are still rays)
+        "mrays_traversed_per_sec": round(mrays * (rays_cnt - cnt.get("rays_skipped", 0)) / max(rays_cnt, 1), 2),
         "higher_is_better": True,
         "scaling": "weak" if frames_per_rank else "strong",
         "vs_baseline": None,

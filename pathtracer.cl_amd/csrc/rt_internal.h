@@ -38,6 +38,10 @@
 #ifndef RT_STEP_UNROLL
 #define RT_STEP_UNROLL 6 /* traversal steps per exit check in k_tris (3 / 4 / 6: 176.3 / 174.0 / 173.4 ms) */
 #endif
+#ifndef RT_PLAIN_PIXEL_STATS
+#define RT_PLAIN_PIXEL_STATS 0 /* RT_PIXEL_STATS clocks in plain (not only counting) launches: a
+                                  diagnostics build (costs registers: 0.5 %) */
+#endif
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif

@@ -933,7 +933,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     a.seeds[plane + slot] = seed.y;
                     mode = M_IDLE;
                     costly = false;
-                    if (a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
+                    if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
                         uint32_t *ps = a.pixel_stats + 4 * ((size_t)yl * a.W + x);
                         ps[0] = pix_rt0;
                         ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -977,7 +977,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
-                        if (a.pixel_stats) pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats)
+                            pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         if (COUNT) {
                             pix_t0 = wave_clock();
                             pix_q = pix_steps = 0;

@@ -5,6 +5,10 @@ time distribution, the last pixels to finish and what they are (probe: box or me
 and how the frame's last milliseconds are spent.  GPU box.
 
     python profiles/pixel_stats.py [out.json]
+
+The plain launch records clocks only in a diagnostics build of the library
+(`bash profiles/build_variant.sh ab/stats.so -DRT_PLAIN_PIXEL_STATS=1`, run with
+RTMI_LIB=ab/stats.so); otherwise the clocks are the counting launch's (slower, distorted).
 """
 import json
 import os
@@ -38,10 +42,14 @@ def main():
     rt.rayTrace(out, W, H, 0, kernel=2)
     plain_ms = rt.lastKernelMs()
     s = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)  # timing: the plain launch
+    if not s[..., 1].any():  # the library records clocks in counting launches only
+        s = None
     rt.setCounting(True)
     rt.rayTrace(out, W, H, 0, kernel=2)
     count_ms = rt.lastKernelMs()
     sc_ = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)  # queries / steps
+    if s is None:
+        s = sc_
     t0 = s[..., 0].min()
     start = (s[..., 0] - t0) / 1e5  # ms (100 MHz)
     fin = (s[..., 1] - t0) / 1e5

@@ -42,6 +42,9 @@
 #define RT_PLAIN_PIXEL_STATS 0 /* RT_PIXEL_STATS clocks in plain (not only counting) launches: a
                                   diagnostics build (costs registers: 0.5 %) */
 #endif
+#ifndef RT_LINKS_NODE_ONLY
+#define RT_LINKS_NODE_ONLY 1 /* trav_step_q: the links' load masked to node lanes (-1 %) */
+#endif
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif

@@ -241,13 +241,20 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     const v4u *vrec = reinterpret_cast<const v4u *>(rec);
     v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2];
-    /* explicit links (64-B nodes): a leaf lane re-reads its record's first 16 B (same line) */
-    v4u w3 = (RT_QNODE_DWORDS == 16) ? vrec[leaf ? 0 : 3] : w0;
+    /* explicit links (64-B nodes) */
+#if RT_LINKS_NODE_ONLY
+    /* the child links only for node lanes (the load runs under their exec mask) */
+    v4u w3 = {0u, 0u, 0u, 0u};
+    if (RT_QNODE_DWORDS == 16 && !leaf) w3 = vrec[3];
+#else
+    v4u w3 = (RT_QNODE_DWORDS == 16) ? vrec[leaf ? 0 : 3] : w0; /* a leaf lane re-reads its first 16 B */
+#endif
     /* Every lane's record arrives as whole dwordx4 loads issued together: without this
        the compiler narrows loads to the components each branch uses (x4 + x3 + x2 +
        dword) and sinks the child links below the box test, i.e. 5-6 vector-memory
        instructions per step instead of 4 (each costs the address path ~16 cycles per
-       wave whatever its width) and a second dependent round trip for node lanes. */
+       wave whatever its width) and a second dependent round trip for node lanes.  The
+       links' load runs for node lanes only: leaf lanes add no addresses to it (-1 %). */
     asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
     const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
     const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);

@@ -117,6 +117,8 @@ typedef struct rt_mesh_stats {
     uint32_t stack4;           /* worst-case traversal stack of the 4-wide tree */
     double build_seconds;
     uint32_t builder; /* RT_BUILD_HOST or RT_BUILD_GPU */
+    uint32_t n_tris_tree; /* triangles in the tree: the host build leaves out those no ray can
+                             hit (|det| < 1e-4 for every unit direction, geometryFuncs.h:167) */
 } rt_mesh_stats;
 /* BVH builder used by the next rt_set_mesh: the host binned-SAH build (default: the best
    trees) or the GPU build (LBVH over Morton codes, collapsed on the device: seconds-to-

@@ -257,6 +257,31 @@ bool rt_validate_mesh(const float *verts, uint32_t n_verts, const int32_t *idx, 
     return true;
 }
 
+/* True when no ray of the kernel can ever accept this triangle.  Moller-Trumbore
+   (geometryFuncs.h:167, rt_kernels.hip mt_test) rejects |det| < 1e-4 with
+   det = dot(cross(d, e2), e1) evaluated in float.  Exactly, |det| <= |d| |e2 x e1|, and
+   every query direction is unit length (camera rays, light samples, Lambert bounces:
+   |d| <= 1.001 covers their rounding).  The float evaluation adds at most
+   7u ||e1||_1 ||e2||_1 (u = 2^-24: two rounded products and a difference per cross
+   component, then a 3-term dot); 16u is used.  The edges are the float records the
+   kernel reads (e = v - v0 rounded as get_triangle does), the bound is evaluated in
+   double.  Such a triangle is never hit, never occludes and never wins a tie, so
+   leaving it out of the tree changes no result bit. */
+static bool never_hit(const float *a, const float *p1, const float *p2)
+{
+    const float e1[3] = {p1[0] - a[0], p1[1] - a[1], p1[2] - a[2]};
+    const float e2[3] = {p2[0] - a[0], p2[1] - a[1], p2[2] - a[2]};
+    const double cx = (double)e2[1] * e1[2] - (double)e2[2] * e1[1];
+    const double cy = (double)e2[2] * e1[0] - (double)e2[0] * e1[2];
+    const double cz = (double)e2[0] * e1[1] - (double)e2[1] * e1[0];
+    const double cr = std::sqrt(cx * cx + cy * cy + cz * cz);
+    const double n1 = std::fabs((double)e1[0]) + std::fabs((double)e1[1]) + std::fabs((double)e1[2]);
+    const double n2 = std::fabs((double)e2[0]) + std::fabs((double)e2[1]) + std::fabs((double)e2[2]);
+    const double u = 1.0 / 16777216.0;
+    const double bound = 1.001 * (cr + 16.0 * u * n1 * n2);
+    return bound < 0.999 * (double)1e-4f;
+}
+
 bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtBvh &out,
                   std::string &err)
 {
@@ -288,10 +313,29 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
             bx.hi[c] += pad;
         }
         b.tbox[t] = bx;
-        b.perm[t] = t;
     }
-    b.nodes.reserve(2ull * n_tris / RT_LEAF_MAX + 16);
-    const int root = b.build(0, n_tris, 1);
+    /* The tree holds the triangles a ray can hit (never_hit above), slots [0, n_hit); the
+       rest follow in slots [n_hit, n_tris) for the linear traversal.  At least one
+       triangle stays in the tree, so it is never empty. */
+    uint32_t n_hit = 0;
+    if (out.cull_unhittable) {
+        std::vector<uint8_t> hit(n_tris);
+        for (uint32_t t = 0; t < n_tris; ++t) {
+            const float *a = verts + 3ull * (uint32_t)idx[3ull * t];
+            const float *p1 = verts + 3ull * (uint32_t)idx[3ull * t + 1];
+            const float *p2 = verts + 3ull * (uint32_t)idx[3ull * t + 2];
+            hit[t] = !never_hit(a, p1, p2);
+            n_hit += hit[t];
+        }
+        if (n_hit == 0) hit[0] = 1, n_hit = 1;
+        for (uint32_t t = 0, k = 0, r = n_hit; t < n_tris; ++t) b.perm[hit[t] ? k++ : r++] = t;
+    } else {
+        n_hit = n_tris;
+        for (uint32_t t = 0; t < n_tris; ++t) b.perm[t] = t;
+    }
+    out.n_hit = n_hit;
+    b.nodes.reserve(2ull * n_hit / RT_LEAF_MAX + 16);
+    const int root = b.build(0, n_hit, 1);
 
     /* Flatten: inner nodes in DFS preorder, each storing both children's boxes. */
     std::vector<int> order; /* TmpNode index per output inner node */
@@ -306,7 +350,7 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
         n[0] = bx.lo[0]; n[1] = bx.hi[0]; n[2] = bx.lo[1]; n[3] = bx.hi[1];
         n[4] = bx.lo[0]; n[5] = bx.hi[0]; n[6] = bx.lo[1]; n[7] = bx.hi[1];
         n[8] = bx.lo[2]; n[9] = bx.hi[2]; n[10] = bx.lo[2]; n[11] = bx.hi[2];
-        const int32_t code = leaf_code(0, n_tris);
+        const int32_t code = leaf_code(0, n_hit);
         std::memcpy(&n[12], &code, 4);
         std::memcpy(&n[13], &code, 4);
         n_leaves = 1;
@@ -514,6 +558,7 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
             remap(&out.nodes[16ull * i + 12]);
             remap(&out.nodes[16ull * i + 13]);
         }
+        for (uint32_t q = cursor; q < n_tris; ++q) new_perm[q] = b.perm[q]; /* the culled tail */
         b.perm.swap(new_perm);
     }
 

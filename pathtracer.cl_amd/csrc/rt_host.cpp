@@ -547,10 +547,12 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
         c->bvh.depth4 = g.depth4;
         c->bvh.stack4 = g.stack4;
         c->bvh.build_seconds = g.build_seconds;
+        c->bvh.n_hit = n_tris; /* the GPU build keeps every triangle */
         c->mesh_builder = RT_BUILD_GPU;
         return RT_OK;
     }
     RtBvh b;
+    if (const char *v = getenv("RT_CULL_UNHITTABLE")) b.cull_unhittable = atoi(v) != 0; /* A/B knob */
     if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
     c->mesh_builder = RT_BUILD_HOST;
@@ -580,6 +582,7 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     c->bvh.depth4 = b.depth4;
     c->bvh.stack4 = b.stack4;
     c->bvh.build_seconds = b.build_seconds;
+    c->bvh.n_hit = b.n_hit;
     return RT_OK;
 }
 
@@ -595,6 +598,7 @@ int rt_mesh_info(const rt_ctx *c, rt_mesh_stats *out)
     out->stack4 = c->bvh.stack4;
     out->builder = (uint32_t)c->mesh_builder;
     out->build_seconds = c->bvh.build_seconds;
+    out->n_tris_tree = c->bvh.n_hit;
     return RT_OK;
 }
 
@@ -1045,8 +1049,20 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
     if (e == hipSuccess) {
-        const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, trav_kind(c),
-                                            c->d_spill, cap, d_idx, d_t, c->stream);
+        /* The tree leaves out triangles no UNIT-length ray can hit (rt_bvh.cpp never_hit); the
+           kernels only trace unit directions, but a caller's rays may be longer: then the
+           linear loop over every triangle answers (same semantics, all triangles). */
+        int kind = trav_kind(c);
+        if (c->bvh.n_hit < c->n_tris)
+            for (uint32_t i = 0; i < n; ++i) {
+                const rt_vec3 &d = rays[i].d;
+                if (!((double)d.x * d.x + (double)d.y * d.y + (double)d.z * d.z <= 1.002)) { /* |d| <= 1.001 */
+                    kind = RT_TRAV_LINEAR;
+                    break;
+                }
+            }
+        const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,
+                                            cap, d_idx, d_t, c->stream);
         e = (hipError_t)le;
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);

@@ -191,6 +191,97 @@ def test_bvh_equals_linear_fuzz_grazing(tracer, pt):
         np.testing.assert_array_equal(out[trav][1][0], out["linear"][1][0])
 
 
+def test_unhittable_triangles_left_out_of_the_tree(tracer, pt, oracle):
+    """The host build leaves out triangles no unit ray can accept (|det| < 1e-4 always,
+    rt_bvh.cpp never_hit).  Triangles straddling that bound, hit at normal incidence and
+    at random angles: BVH == linear for closest and any hit; non-unit directions fall back
+    to the linear loop; a frame of a mesh whose triangles are mostly culled == oracle."""
+    rng = np.random.default_rng(23)
+    nt = 4000
+    cr = np.exp(rng.uniform(np.log(2e-5), np.log(5e-4), nt))  # |e1 x e2| around the 1e-4 bound
+    a = np.sqrt(cr) * np.exp(rng.uniform(-1.5, 1.5, nt))
+    b = cr / a
+    nrm = rng.normal(size=(nt, 3))
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    t1 = np.cross(nrm, rng.normal(size=(nt, 3)))
+    t1 /= np.linalg.norm(t1, axis=1, keepdims=True)
+    t2 = np.cross(nrm, t1)
+    c = rng.uniform(-3, 3, (nt, 3))
+    v = np.stack([c, c + a[:, None] * t1, c + b[:, None] * t2], axis=1).reshape(-1, 3).astype(np.float32)
+    idx = np.arange(nt * 3, dtype=np.int32).reshape(nt, 3)
+    n = 3 * nt
+    rr = np.zeros(n, pt._abi.RAY_DTYPE)
+    k = np.arange(n) % nt
+    inplane = (rng.uniform(0.05, 0.3, (n, 1)) * a[k, None] * t1[k] + rng.uniform(0.05, 0.3, (n, 1)) * b[k, None] * t2[k])
+    sgn = np.where(rng.uniform(size=(n, 1)) < 0.5, 1.0, -1.0)
+    o = c[k] + inplane + sgn * 2.0 * nrm[k]
+    d = -sgn * nrm[k]
+    rnd = np.arange(n) >= 2 * nt  # the last third: random directions toward the triangle
+    d[rnd] = (c[k[rnd]] + inplane[rnd]) - rng.uniform(-6, 6, (rnd.sum(), 3))
+    o[rnd] = c[k[rnd]] + inplane[rnd] - d[rnd]
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rr["o"] = o.astype(np.float32)
+    rr["d"] = d.astype(np.float32)
+    rr["tmin"] = np.float32(1e-4)
+    rr["tmax"] = np.float32(np.inf)
+    rs = rr.copy()
+    rs["tmax"] = np.float32(10.0)
+    rt = tracer
+    rt.setMesh(v, idx)
+    info = rt.meshInfo()
+    assert 0 < info["n_tris_tree"] < nt
+    out = {}
+    for trav in ("linear", "bvh", "bvh4f", "bvh2"):
+        rt.setTraversal(trav)
+        out[trav] = (rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
+    for trav in ("bvh", "bvh4f", "bvh2"):
+        np.testing.assert_array_equal(out[trav][0][0], out["linear"][0][0])
+        np.testing.assert_array_equal(bits(out[trav][0][1]), bits(out["linear"][0][1]))
+        np.testing.assert_array_equal(out[trav][1][0], out["linear"][1][0])
+    hits = out["linear"][0][0] >= 0
+    assert hits.sum() > 500  # triangles above the bound are hit
+    # the hit triangles are all in the tree: |e1 x e2| >= ~1e-4
+    assert cr[out["linear"][0][0][hits]].min() > 0.9e-4
+    # longer directions can accept culled triangles: those queries take the linear loop
+    rl = rr.copy()
+    rl["d"] = (d * 50.0).astype(np.float32)
+    rt.setTraversal("bvh")
+    got = rt.traceRays(rl)
+    rt.setTraversal("linear")
+    exp = rt.traceRays(rl)
+    rt.setTraversal("bvh")
+    np.testing.assert_array_equal(got[0], exp[0])
+    np.testing.assert_array_equal(bits(got[1]), bits(exp[1]))
+    assert (cr[exp[0][exp[0] >= 0]] < 1e-4).any()
+    # a frame of a shrunken bunny-class mesh (most triangles culled) == oracle
+    sc = pt.scenes
+    W, H, sr = 40, 30, 1
+    Wp, Hp = sc.padded_dims(W, H)
+    S = sc.ply_scene()
+    mv, mi = sc.make_mesh(69_451)
+    mv = mv.reshape(-1, 3)
+    cen = mv.mean(axis=0)
+    mv = (cen + (mv - cen) * np.float32(0.15)).astype(np.float32).reshape(-1)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=5)
+    r2 = pt.RayTracer(0)
+    r2.setSpheres(S)
+    r2.setCamera(cam)
+    r2.setSampleRate(sr)
+    r2.setMaxPathDepth(6)
+    r2.setMesh(mv, mi)
+    assert r2.meshInfo()["n_tris_tree"] < 69_451
+    r2.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    r2.rayTrace(got, W, H, 0, kernel=2)
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, mv, mi)
+    np.testing.assert_array_equal(bits(got), bits(exp))
+    np.testing.assert_array_equal(r2.getSeeds(), sd)
+    r2.close()
+
+
 @pytest.mark.parametrize("kernel,prog", [(2, 0), (2, 3), (0, 0), (1, 2)])
 def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt):
     """Row-stripe tiles (the multi-GPU partition) reassemble to the single-device frame."""

@@ -48,6 +48,9 @@
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif
+#ifndef RT_SHADOW_REDO
+#define RT_SHADOW_REDO 1 /* k_tris: shadow rays answered without traversal are consumed in the same D pass (-3.9 %) */
+#endif
 #define RT_LEAF_MAX 8
 /* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots,
    traversal-loop clocks, kernel clocks (the last two: per lane, summed), shadow rays

@@ -803,6 +803,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     for (;;) {
         const unsigned long long t_d0 = COUNT ? wave_clock() : 0ull;
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
+        for (;;) {
         if (fin) {
             fin = false;
             bool want_shadow = false, seg_done = false, sample_done = false;
@@ -955,6 +956,19 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                 }
             }
+        }
+        /* RT_SHADOW_REDO: a shadow ray just issued whose answer is known without a traversal
+           (the C-phase rule below: tmax <= tmin, or cos(wi) <= 0) is answered here and the
+           path advanced again in this pass, instead of after a whole stepping round */
+        if (!RT_SHADOW_REDO) break;
+        const bool redo = mode == M_SHADOW && !fin && !running &&
+                          (!(stmax > RT_SMALL_F) || !(qd.x * hn.x + qd.y * hn.y + qd.z * hn.z > 0));
+        if (!__any(redo)) break;
+        if (redo) {
+            ts.best = -1;
+            fin = true;
+            ++cnt[RT_CNT_SKIPPED];
+        }
         }
 
         if (COUNT) cnt[RT_CNT_SHADE] += wave_clock() - t_d0;

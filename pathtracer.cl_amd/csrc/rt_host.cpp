@@ -93,8 +93,8 @@ struct rt_ctx {
     size_t flags_bytes = 0;
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
-    uint32_t fetch_k = 16;
-    uint32_t fetch_k_box = 16; /* waves holding box pixels (probe) */
+    uint32_t fetch_k = 24;     /* re-swept after RT_SHADOW_REDO: 12 / 16 / 20 / 24 / 32 / 40 -> 166.8 / 163.9 / 163.0 / 162.3 / 163.9 / 168.2 ms */
+    uint32_t fetch_k_box = 24; /* waves holding box pixels (probe); 8 / 16 / 24 within 0.5 % */
     uint32_t probe_n = 2;      /* cost probe: probe_n x probe_n rays per pixel (RT_PROBE_N) */
     int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */

@@ -30,7 +30,7 @@
 #define RT_MIX_PLANES 1 /* node planes through v_perm_b32 + v_fma_mix_f32 (rt_kernels.hip trav_step_q) */
 #endif
 #ifndef RT_PRIO
-#define RT_PRIO 2 /* wave issue priority for waves holding box pixels (long sample chains) */
+#define RT_PRIO 3 /* wave issue priority for waves holding box pixels (long sample chains); 1 / 2 / 3 re-measured after the shadow redo: 161.6 / 162.6 / 161.1 ms */
 #endif
 /* cost-probe word: hits (0..25) in the top 5 bits, traversal steps below */
 #define RT_PROBE_HIT_SHIFT 27

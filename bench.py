@@ -33,10 +33,10 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 (per XCD, 32 MiB aggregate) ~34.5 TB/s
-NODE_BYTES = {"bvh": 64, "bvh4f": 112, "bvh2": 64, "linear": 0, "packet": 112}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
+NODE_BYTES = {"bvh": 64, "bvh4f": 112, "linear": 0}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
 # bytes read per triangle test: the whole 48-B record (one-record steps of the compressed traversal), else
 # v0+orig (16), e1 (12), e2 (12); csrc/rt_internal.h
-TRI_BYTES = {"bvh": 48, "bvh4f": 40, "bvh2": 40, "linear": 40, "packet": 48}
+TRI_BYTES = {"bvh": 48, "bvh4f": 40, "linear": 40}
 PIXEL_BYTES = 16 + 8 + 8  # RGBA32F store + seed read + seed write per pixel
 
 
@@ -55,8 +55,8 @@ def parse():
                          "frame per rank (turntable views 3 degrees apart), frames gathered to rank 0. auto: weak "
                          "for the dragon config (its 256-spp pixels are serial chains: DESIGN.md), else strong")
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
-    ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "bvh2", "linear", "packet"],
-                    help="bvh: 4-wide BVH (default); bvh2: binary BVH; linear: the reference loop")
+    ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "linear"],
+                    help="bvh: 4-wide compressed BVH (default); bvh4f: full-precision nodes; linear: the reference loop")
     ap.add_argument("--builder", default="host", choices=["host", "gpu"],
                     help="BVH builder: host binned SAH (default) or the GPU LBVH build")
     ap.add_argument("--ply", default=None, help="render this PLY mesh (normalised, SURVEY §8d) instead of "
@@ -324,8 +324,7 @@ def main():
         dist.destroy_process_group()
 
 
-TRAVERSAL_NAMES = {"bvh": "4-wide compressed BVH", "bvh4f": "4-wide BVH", "bvh2": "binary BVH", "linear": "linear (reference)",
-                   "packet": "4-wide BVH, wave-coherent"}
+TRAVERSAL_NAMES = {"bvh": "4-wide compressed BVH", "bvh4f": "4-wide BVH", "linear": "linear (reference)"}
 
 
 def workload_name(cfg, n_tris, W, H, sr, traversal, builder="host"):

@@ -48,14 +48,12 @@ enum {
    (identical results: closest hit = minimum t, ties to the highest index).
    RT_TRAVERSAL_BVH is the 4-wide tree with compressed (8-bit quantised) 64-B
    nodes traversed per lane; RT_TRAVERSAL_BVH4F the same tree with full-precision
-   128-B nodes; RT_TRAVERSAL_BVH2 the binary tree they are collapsed from;
-   RT_TRAVERSAL_PACKET the 4-wide tree walked wave-coherently (one node sequence
-   per wave, scalar node fetches). */
+   128-B nodes (also the automatic fallback for meshes whose extent the quantised
+   grid cannot encode).  Values 2 and 3 (a binary-tree and a wave-coherent packet
+   traversal, measured slower) are retired: rt_set_traversal refuses them. */
 enum {
     RT_TRAVERSAL_BVH = 0,
     RT_TRAVERSAL_LINEAR = 1,
-    RT_TRAVERSAL_BVH2 = 2,
-    RT_TRAVERSAL_PACKET = 3,
     RT_TRAVERSAL_BVH4F = 4
 };
 
@@ -122,8 +120,8 @@ typedef struct rt_mesh_stats {
 } rt_mesh_stats;
 /* BVH builder used by the next rt_set_mesh: the host binned-SAH build (default: the best
    trees) or the GPU build (LBVH over Morton codes, collapsed on the device: seconds-to-
-   milliseconds for large meshes, somewhat slower traversal; no binary-tree layout, so
-   RT_TRAVERSAL_BVH2 is refused on its meshes).  Results are identical either way. */
+   milliseconds for large meshes, somewhat slower traversal).  Results are identical
+   either way. */
 enum { RT_BUILD_HOST = 0, RT_BUILD_GPU = 1 };
 int rt_set_builder(rt_ctx *ctx, int builder);
 int rt_mesh_info(const rt_ctx *ctx, rt_mesh_stats *out);
@@ -187,7 +185,7 @@ int rt_read(rt_ctx *ctx, float *host, size_t n_floats);
 uint32_t rt_tile_rows(uint32_t height, const rt_tile *tile);
 
 /* ---- instrumentation ---- */
-int rt_get_counters(const rt_ctx *ctx, rt_counters *out); /* of the last completed render */
+int rt_get_counters(const rt_ctx *ctx, rt_counters *out); /* of the last completed render (or counting rt_trace_rays call) */
 int rt_set_counting(rt_ctx *ctx, int enable);             /* count nodes/tris in the next renders */
 /* Device time of the last render's kernel (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(const rt_ctx *ctx, float *ms);

@@ -35,8 +35,6 @@ RT_KERNEL_TRIS = 2
 
 RT_TRAVERSAL_BVH = 0
 RT_TRAVERSAL_LINEAR = 1
-RT_TRAVERSAL_BVH2 = 2
-RT_TRAVERSAL_PACKET = 3
 RT_TRAVERSAL_BVH4F = 4
 
 RT_BUILD_HOST = 0

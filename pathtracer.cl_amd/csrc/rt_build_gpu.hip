@@ -1,7 +1,7 @@
 /*
  * rt_build_gpu.hip — BVH build on the GPU ("the step before the
  * path").  Produces the same 4-wide layouts the traversal reads (rt_internal.h: 128-B
- * float nodes for the packet traversal / scheduling probe, 64-B compressed nodes for the
+ * float nodes (the full-precision traversal), 64-B compressed nodes for the
  * default traversal) and the leaf-ordered triangle records, from the mesh arrays of
  * raytrace_tris (tri_verts / tri_vert_idx, raytracer.cl:184-188).
  *

@@ -79,7 +79,6 @@ struct rt_ctx {
 
     /* mesh */
     RtBvh bvh;
-    float *d_nodes = nullptr;  /* binary tree */
     float *d_nodes4 = nullptr; /* 4-wide tree */
     uint32_t *d_nodes4q = nullptr; /* 4-wide tree, compressed nodes */
     float *d_tris = nullptr;
@@ -96,6 +95,10 @@ struct rt_ctx {
     uint32_t fetch_k = 24;     /* re-swept after RT_SHADOW_REDO: 12 / 16 / 20 / 24 / 32 / 40 -> 166.8 / 163.9 / 163.0 / 162.3 / 163.9 / 168.2 ms */
     uint32_t fetch_k_box = 24; /* waves holding box pixels (probe); 8 / 16 / 24 within 0.5 % */
     uint32_t probe_n = 2;      /* cost probe: probe_n x probe_n rays per pixel (RT_PROBE_N) */
+    uint32_t fetch_frac = 24;  /* stepping-round exit relative to the live lanes (RT_FETCH_FRAC, 1/64ths; 0 = off):
+                                  r02 A/B (profiles/r02b/fetch_ab.jsonl) full frame 162.8 -> 160.6 ms, one row
+                                  alone 157.8 -> 78.9 ms, slowest of 8 row-stripe tiles 219 -> 107 ms */
+    uint32_t box_exit = 0;     /* a box pixel's completed query ends the stepping round (RT_BOX_EXIT) */
     int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
@@ -280,20 +283,15 @@ int ensure_seeds(rt_ctx *c, uint32_t wpad, uint32_t hpad, const uint32_t *src)
 int trav_kind(const rt_ctx *c)
 {
     if (c->traversal == RT_TRAVERSAL_LINEAR) return RT_TRAV_LINEAR;
-    if (c->traversal == RT_TRAVERSAL_BVH2) return RT_TRAV_BVH2;
-    if (c->traversal == RT_TRAVERSAL_PACKET) return RT_TRAV_PACKET4;
     if (c->traversal == RT_TRAVERSAL_BVH4F || !c->d_nodes4q) return RT_TRAV_BVH4;
     return RT_TRAV_BVH4Q;
 }
 
 uint32_t spill_cap(const rt_ctx *c)
 {
-    /* worst-case stack: the 4-wide tree's stack4; the binary tree pushes at most one
-       entry per level below the root */
+    /* worst-case stack: the 4-wide tree's stack4 */
     const int k = trav_kind(c);
-    uint32_t need = 0;
-    if (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) need = c->bvh.stack4;
-    else if (k == RT_TRAV_BVH2) need = c->bvh.depth;
+    const uint32_t need = (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) ? c->bvh.stack4 : 0u;
     return need > RT_STACK_DEPTH ? need - RT_STACK_DEPTH : 0;
 }
 
@@ -301,7 +299,7 @@ const float *trav_nodes(const rt_ctx *c)
 {
     const int k = trav_kind(c);
     if (k == RT_TRAV_BVH4Q) return reinterpret_cast<const float *>(c->d_nodes4q);
-    return (k == RT_TRAV_BVH4 || k == RT_TRAV_PACKET4) ? c->d_nodes4 : c->d_nodes;
+    return k == RT_TRAV_BVH4 ? c->d_nodes4 : nullptr;
 }
 
 int ensure_spill(rt_ctx *c, size_t entries)
@@ -456,6 +454,8 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_FETCH_K")) c->fetch_k = (uint32_t)std::max(1, std::min(64, atoi(v))); /* tuning knob */
     if (const char *v = getenv("RT_PROBE_N")) c->probe_n = (uint32_t)std::max(1, std::min(5, atoi(v)));
     if (const char *v = getenv("RT_FETCH_K_BOX")) c->fetch_k_box = (uint32_t)std::max(1, std::min(64, atoi(v)));
+    if (const char *v = getenv("RT_FETCH_FRAC")) c->fetch_frac = (uint32_t)std::max(0, std::min(64, atoi(v)));
+    if (const char *v = getenv("RT_BOX_EXIT")) c->box_exit = atoi(v) != 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
@@ -473,7 +473,6 @@ int rt_destroy(rt_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     free_dev(c->d_spheres);
     free_dev(c->d_lights);
-    free_dev(c->d_nodes);
     free_dev(c->d_nodes4);
     free_dev(c->d_nodes4q);
     free_dev(c->d_spill);
@@ -525,11 +524,10 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     std::string err;
     if (c->builder == RT_BUILD_GPU) {
         if (!rt_validate_mesh(verts, n_verts, idx, n_tris, err)) return fail(c, RT_ERR_ARG, err);
-        free_dev(c->d_nodes);
         free_dev(c->d_nodes4);
         free_dev(c->d_nodes4q);
         free_dev(c->d_tris);
-        c->d_nodes = c->d_nodes4 = c->d_tris = nullptr;
+        c->d_nodes4 = c->d_tris = nullptr;
         c->d_nodes4q = nullptr;
         c->n_tris = 0;
         RtGpuBvh g;
@@ -556,18 +554,15 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
     c->mesh_builder = RT_BUILD_HOST;
-    free_dev(c->d_nodes);
     free_dev(c->d_nodes4);
     free_dev(c->d_nodes4q);
     free_dev(c->d_tris);
-    c->d_nodes = c->d_nodes4 = c->d_tris = nullptr;
+    c->d_nodes4 = c->d_tris = nullptr;
     c->d_nodes4q = nullptr;
     c->n_tris = 0;
-    HIPCHK(c, hipMalloc(&c->d_nodes, b.nodes.size() * sizeof(float)));
     HIPCHK(c, hipMalloc(&c->d_nodes4, b.nodes4.size() * sizeof(float)));
     if (!b.nodes4q.empty()) HIPCHK(c, hipMalloc(&c->d_nodes4q, b.nodes4q.size() * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
-    HIPCHK(c, hipMemcpy(c->d_nodes, b.nodes.data(), b.nodes.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
     if (!b.nodes4q.empty())
         HIPCHK(c, hipMemcpy(c->d_nodes4q, b.nodes4q.data(), b.nodes4q.size() * sizeof(uint32_t),
@@ -667,7 +662,7 @@ int rt_set_builder(rt_ctx *c, int builder)
 
 int rt_set_traversal(rt_ctx *c, int t)
 {
-    if (!c || t < RT_TRAVERSAL_BVH || t > RT_TRAVERSAL_BVH4F) return RT_ERR_ARG;
+    if (!c || !(t == RT_TRAVERSAL_BVH || t == RT_TRAVERSAL_LINEAR || t == RT_TRAVERSAL_BVH4F)) return RT_ERR_ARG;
     c->traversal = t;
     return RT_OK;
 }
@@ -754,10 +749,6 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                     "a tile need the seed-row halo (rt_pack_seed_rows / rt_unpack_seed_rows, flag RT_SEEDS_HALO)");
     if (kernel == RT_KERNEL_TRIS && c->n_tris == 0) return fail(c, RT_ERR_NO_MESH, "no mesh set");
     if (kernel != RT_KERNEL_TRIS && c->spheres.empty()) return fail(c, RT_ERR_NO_SCENE, "no spheres set");
-    if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_BVH2 && !c->d_nodes)
-        return fail(c, RT_ERR_STATE, "the GPU builder produces no binary tree: use a 4-wide traversal");
-    if (kernel == RT_KERNEL_TRIS && c->traversal == RT_TRAVERSAL_PACKET && c->bvh.stack4 > 64)
-        return fail(c, RT_ERR_LIMIT, "4-wide BVH stack exceeds the per-wave stack (64)");
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
 
@@ -842,6 +833,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.spill = c->d_spill;
         a.fetch_k = c->fetch_k;
         a.fetch_k_box = c->fetch_k_box;
+        a.fetch_frac = c->fetch_frac;
+        a.box_exit = c->box_exit;
         a.tile_order = nullptr;
         a.pixel_flags = nullptr;
         if (c->schedule) {
@@ -855,21 +848,21 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
             fprintf(stderr, "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p\n", (void *)c,
                     trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order);
-        /* diagnostics: per-pixel start/finish clocks (+ queries/steps in a counting
-           launch), dumped raw to $RT_PIXEL_STATS */
+        /* diagnostics: per-pixel start/finish clocks (+ queries, steps and the wall clocks
+           by phase in a counting launch: 8 x u32 per pixel), dumped raw to $RT_PIXEL_STATS */
         const char *stats_path = getenv("RT_PIXEL_STATS");
         uint32_t *d_stats = nullptr;
         a.pixel_stats = nullptr;
         if (stats_path) {
-            HIPCHK(c, hipMalloc(&d_stats, (size_t)W * hl * 16));
-            HIPCHK(c, hipMemsetAsync(d_stats, 0, (size_t)W * hl * 16, st));
+            HIPCHK(c, hipMalloc(&d_stats, (size_t)W * hl * 32));
+            HIPCHK(c, hipMemsetAsync(d_stats, 0, (size_t)W * hl * 32, st));
             a.pixel_stats = d_stats;
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         e = rt_launch_tris(a, trav, c->counting, blocks, st);
         HIPCHK(c, hipEventRecord(c->ev1, st));
         if (d_stats) {
-            std::vector<uint32_t> h((size_t)W * hl * 4);
+            std::vector<uint32_t> h((size_t)W * hl * 8);
             HIPCHK(c, hipMemcpyAsync(h.data(), d_stats, h.size() * 4, hipMemcpyDeviceToHost, st));
             HIPCHK(c, hipStreamSynchronize(st));
             (void)hipFree(d_stats);
@@ -1061,15 +1054,28 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
                     break;
                 }
             }
-        const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,
-                                            cap, d_idx, d_t, c->stream);
-        e = (hipError_t)le;
+        if (c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_N_COUNTERS * sizeof(unsigned long long), c->stream);
+        if (e == hipSuccess) {
+            const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,
+                                                cap, d_idx, d_t, c->counting ? c->d_counters : nullptr, c->stream);
+            e = (hipError_t)le;
+        }
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev1, c->stream);
     if (e == hipSuccess) c->have_timing = true;
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out_idx, d_idx, n * sizeof(int32_t), hipMemcpyDeviceToHost);
     if (e == hipSuccess && out_t) e = hipMemcpy(out_t, d_t, n * sizeof(float), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && c->counting) { /* rt_get_counters: queries and records of these rays */
+        unsigned long long h[RT_N_COUNTERS];
+        e = hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost);
+        c->last = rt_counters{};
+        c->last.rays_closest = h[0];
+        c->last.rays_shadow = h[1];
+        c->last.nodes_visited = h[2];
+        c->last.tris_tested = h[3];
+        c->last.leaves_visited = h[4];
+    }
     cleanup();
     if (e != hipSuccess) return hip_fail(c, e, "rt_trace_rays");
     return RT_OK;

@@ -23,15 +23,6 @@
 #define RT_BVH_MAX_DEPTH 33
 #define RT_BLOCK 256
 /* waves per SIMD the triangle kernel is compiled for (register budget 512 / waves) */
-#ifndef RT_FULL_LOADS
-#define RT_FULL_LOADS 1 /* traversal records as whole dwordx4 loads (rt_kernels.hip trav_step_q) */
-#endif
-#ifndef RT_MIX_PLANES
-#define RT_MIX_PLANES 1 /* node planes through v_perm_b32 + v_fma_mix_f32 (rt_kernels.hip trav_step_q) */
-#endif
-#ifndef RT_PRIO
-#define RT_PRIO 3 /* wave issue priority for waves holding box pixels (long sample chains); 1 / 2 / 3 re-measured after the shadow redo: 161.6 / 162.6 / 161.1 ms */
-#endif
 /* cost-probe word: hits (0..25) in the top 5 bits, traversal steps below */
 #define RT_PROBE_HIT_SHIFT 27
 #define RT_PROBE_STEP_MASK ((1u << RT_PROBE_HIT_SHIFT) - 1u)
@@ -41,9 +32,6 @@
 #ifndef RT_PLAIN_PIXEL_STATS
 #define RT_PLAIN_PIXEL_STATS 0 /* RT_PIXEL_STATS clocks in plain (not only counting) launches: a
                                   diagnostics build (costs registers: 0.5 %) */
-#endif
-#ifndef RT_LINKS_NODE_ONLY
-#define RT_LINKS_NODE_ONLY 1 /* trav_step_q: the links' load masked to node lanes (-1 %) */
 #endif
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
@@ -141,6 +129,9 @@ struct RtTriLaunch {
                                     their steps (NULL: no probe) */
     uint32_t probe_n;            /* probe rays per pixel: probe_n x probe_n (<= 5) */
     uint32_t fetch_k_box;       /* fetch_k of waves holding box pixels (pixel_flags 0) */
+    uint32_t fetch_frac;        /* stepping-round exit at ceil(live lanes x fetch_frac / 64) completed
+                                   queries when that is below fetch_k (0: fetch_k only) */
+    uint32_t box_exit;          /* a box pixel's completed query ends the stepping round */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =
                                    start / finish (s_memrealtime, 100 MHz, low 32 bits), queries, steps */
 };
@@ -159,13 +150,13 @@ struct RtSphLaunch {
 
 /* All return a hipError_t as int (0 = success). */
 /* traversal kinds (kernel template parameter) */
-enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH2 = 1, RT_TRAV_BVH4 = 2, RT_TRAV_PACKET4 = 3, RT_TRAV_BVH4Q = 4 };
+enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH4 = 2, RT_TRAV_BVH4Q = 4 };
 
 int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream);
 int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
-                         void *stream);
+                         unsigned long long *counters, void *stream); /* counters: NULL, or counting (queries, nodes, tests, leaves) */
 /* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed

@@ -218,7 +218,7 @@ __device__ __forceinline__ float half_of(uint32_t w, int hi)
 }
 
 /* One step of the compressed 4-wide traversal (rt_quant.h).  Every lane fetches
-   exactly one 48-B record per step — a node, or ONE triangle of its current leaf —
+   exactly one 64-B record per step — a node, or ONE triangle of its current leaf —
    with the same three dwordx4 loads, so a wave-step costs one memory round trip
    whatever mix of node and leaf lanes it holds (a leaf of k triangles takes k
    steps; the leaf cursor is the leaf code itself: first slot and remaining count). */
@@ -236,33 +236,23 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     const bool lds_only = !__any(stk.sp + 3 > RT_STACK_DEPTH);
     const uint32_t enc = (uint32_t)(~node);
     const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (enc >> 3)
-                            : reinterpret_cast<const uint4 *>(nodes) + (RT_QNODE_DWORDS / 4) * node;
-#if RT_FULL_LOADS
+                            : reinterpret_cast<const uint4 *>(nodes) + 4 * node;
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     const v4u *vrec = reinterpret_cast<const v4u *>(rec);
     v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2];
-    /* explicit links (64-B nodes) */
-#if RT_LINKS_NODE_ONLY
-    /* the child links only for node lanes (the load runs under their exec mask) */
+    /* the child links (d[12..15]) only for node lanes: the load runs under their exec mask,
+       so leaf lanes add no addresses to it (-1 %) */
     v4u w3 = {0u, 0u, 0u, 0u};
-    if (RT_QNODE_DWORDS == 16 && !leaf) w3 = vrec[3];
-#else
-    v4u w3 = (RT_QNODE_DWORDS == 16) ? vrec[leaf ? 0 : 3] : w0; /* a leaf lane re-reads its first 16 B */
-#endif
+    if (!leaf) w3 = vrec[3];
     /* Every lane's record arrives as whole dwordx4 loads issued together: without this
        the compiler narrows loads to the components each branch uses (x4 + x3 + x2 +
        dword) and sinks the child links below the box test, i.e. 5-6 vector-memory
        instructions per step instead of 4 (each costs the address path ~16 cycles per
-       wave whatever its width) and a second dependent round trip for node lanes.  The
-       links' load runs for node lanes only: leaf lanes add no addresses to it (-1 %). */
+       wave whatever its width) and a second dependent round trip for node lanes. */
     asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
     const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
     const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);
-    [[maybe_unused]] const uint4 q3 = make_uint4(w3.x, w3.y, w3.z, w3.w);
-#else
-    const uint4 q0 = rec[0], q1 = rec[1], q2 = rec[2];
-    [[maybe_unused]] const uint4 q3 = (RT_QNODE_DWORDS == 16) ? rec[leaf ? 0 : 3] : q0;
-#endif
+    const uint4 q3 = make_uint4(w3.x, w3.y, w3.z, w3.w);
     if (leaf) {
         if (COUNT) {
             cnt.tests++;
@@ -285,11 +275,7 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
         if (COUNT) cnt.nodes++;
         const float tmax_c = t_slack(s.best_t);
         const uint32_t w = q0.w;
-#if RT_MIX_PLANES
         constexpr int kExpBias = RT_QEXP_MIN + 24; /* scales carry the 2^24 of the f16-subnormal planes */
-#else
-        constexpr int kExpBias = RT_QEXP_MIN;
-#endif
         const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + kExpBias);
         const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + kExpBias);
         const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + kExpBias);
@@ -303,10 +289,6 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
         float t[4];
         int c[4];
         int nhit = 0;
-#if RT_QNODE_DWORDS != 16
-        int leaf_off = 0; /* triangles of the leaf children before child i */
-#endif
-#if RT_MIX_PLANES
         /* Plane bytes as f16 subnormals: v_perm_b32 spreads two bytes of a plane word into
            the low bytes of two 16-bit halves (0x00bb = b * 2^-24 as f16, exact), and
            v_fma_mix_f32 converts a half and does the FMA in one instruction, with the
@@ -319,10 +301,8 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
         const uint32_t fx01 = __builtin_amdgcn_perm(0u, fxw, 0x0c010c00u), fx23 = __builtin_amdgcn_perm(0u, fxw, 0x0c030c02u);
         const uint32_t fy01 = __builtin_amdgcn_perm(0u, fyw, 0x0c010c00u), fy23 = __builtin_amdgcn_perm(0u, fyw, 0x0c030c02u);
         const uint32_t fz01 = __builtin_amdgcn_perm(0u, fzw, 0x0c010c00u), fz23 = __builtin_amdgcn_perm(0u, fzw, 0x0c030c02u);
-#endif
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-#if RT_MIX_PLANES
             const float tn = __builtin_fmaxf(
                 __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nx01 : nx23, i & 1), sx24, bx),
                                 __builtin_fmaf(half_of(i < 2 ? ny01 : ny23, i & 1), sy24, by)),
@@ -331,27 +311,8 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fx01 : fx23, i & 1), sx24, bx),
                                 __builtin_fmaf(half_of(i < 2 ? fy01 : fy23, i & 1), sy24, by)),
                 __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fz01 : fz23, i & 1), sz24, bzo), tmax_c));
-#else
-            const int sh = 8 * i;
-            const float tn = __builtin_fmaxf(
-                __builtin_fmaxf(__builtin_fmaf((float)((nxw >> sh) & 255u), sx, bx),
-                                __builtin_fmaf((float)((nyw >> sh) & 255u), sy, by)),
-                __builtin_fmaxf(__builtin_fmaf((float)((nzw >> sh) & 255u), sz, bzo), tmin_c));
-            const float tf = __builtin_fminf(
-                __builtin_fminf(__builtin_fmaf((float)((fxw >> sh) & 255u), sx, bx),
-                                __builtin_fmaf((float)((fyw >> sh) & 255u), sy, by)),
-                __builtin_fminf(__builtin_fmaf((float)((fzw >> sh) & 255u), sz, bzo), tmax_c));
-#endif
             const bool h = tn <= tf; /* an unused slot's inverted box never passes */
-#if RT_QNODE_DWORDS == 16
             c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
-#else
-            const uint32_t m = (w >> (16 + 4 * i)) & 15u;
-            const bool lf = (m & 8u) != 0;
-            const int k = (int)(m & 7u); /* leaf: count - 1; inner: rank */
-            c[i] = lf ? ~((((int)q2.w + leaf_off) << 3) | k) : (int)q2.z + k;
-            leaf_off += lf ? k + 1 : 0;
-#endif
             t[i] = h ? tn : kInf;
             nhit += h ? 1 : 0;
         }
@@ -403,31 +364,7 @@ __device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, cons
     if (node >= 0) {
         if (COUNT) cnt.nodes++;
         const float tmax_c = t_slack(s.best_t);
-        if (TRAV == RT_TRAV_BVH2) {
-            const float4 n0 = nodes[4 * node + 0];
-            const float4 n1 = nodes[4 * node + 1];
-            const float4 n2 = nodes[4 * node + 2];
-            const float4 n3 = nodes[4 * node + 3];
-            bool h0, h1;
-            const float t0 = slab(n0.x, n0.y, n0.z, n0.w, n2.x, n2.y, inv, oi, tmin_c, tmax_c, h0);
-            const float t1 = slab(n1.x, n1.y, n1.z, n1.w, n2.z, n2.w, inv, oi, tmin_c, tmax_c, h1);
-            const int c0 = __float_as_int(n3.x);
-            const int c1 = __float_as_int(n3.y);
-            if (h0 && h1) {
-                int nearc = c0, farc = c1;
-                if (t1 < t0) {
-                    nearc = c1;
-                    farc = c0;
-                }
-                stk.push(farc);
-                s.node = nearc;
-                return false;
-            }
-            if (h0 || h1) {
-                s.node = h0 ? c0 : c1;
-                return false;
-            }
-        } else {
+        {
             /* 4-wide: near/far slab planes picked by the direction signs, so each
                child costs 6 FMAs + max3/min3 and no min/max pairs. */
             const int nxo = inv.x >= 0.0f ? 0 : 1, nyo = inv.y >= 0.0f ? 2 : 3, nzo = inv.z >= 0.0f ? 4 : 5;
@@ -534,131 +471,6 @@ __device__ __forceinline__ int traverse(const float4 *__restrict__ nodes, const 
     return st.best;
 }
 
-/* Wave-coherent (packet) traversal of the 4-wide tree.  All participating
-   lanes of the wave walk ONE node sequence: the node index and the stack are
-   wave-uniform (SGPRs / a per-wave LDS stack), node and triangle records come
-   in through scalar loads (one fetch per wave, operands in SGPRs), and every
-   lane tests the fetched children / triangles against its own ray, culling by
-   its own [tmin, best_t].  A child is entered when any live lane hits it; the
-   order follows the first live lane's entry distances.  Suited to the coherent
-   queries of raytrace_tris (an 8x8 pixel tile's camera rays, and the shadow rays
-   from those surface points to the same light).  The result per lane is the
-   same as the per-lane traversal (same accept rule, conservative culling). */
-constexpr int kWaveStack = 64;
-
-/* Read-only scene records through the constant address space: with a
-   wave-uniform address the loads become s_load (scalar cache, SGPR operands). */
-typedef float v4f __attribute__((ext_vector_type(4)));
-#if defined(__HIP_DEVICE_COMPILE__)
-typedef __attribute__((address_space(4))) const v4f cfloat4;
-#else
-typedef const v4f cfloat4;
-#endif
-__device__ __forceinline__ float4 ld4(const cfloat4 *p)
-{
-    const v4f v = *p;
-    return make_float4(v.x, v.y, v.z, v.w);
-}
-
-template <bool COUNT>
-__device__ __forceinline__ int traverse_packet4(const float4 *__restrict__ nodes_g, const float4 *__restrict__ tris_g,
-                                                V3 o, V3 d, float tmin, float &tmax, bool any_hit, int *wstack,
-                                                TravCounts &cnt)
-{
-    const cfloat4 *nodes = (const cfloat4 *)nodes_g;
-    const cfloat4 *tris = (const cfloat4 *)tris_g;
-    int best = -1;
-    int best_orig = -1;
-    float best_t = tmax;
-    bool live = true;
-    const V3 inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
-    const V3 oi = v3(o.x * inv.x, o.y * inv.y, o.z * inv.z);
-    const float tmin_c = -1e-3f;
-    int sp = 0;
-    int node = 0;
-    const bool rep = COUNT && (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
-                               (uint32_t)__builtin_ctzll(__ballot(1)));
-    for (;;) {
-        if (node >= 0) {
-            const cfloat4 *nd = nodes + 8 * node;
-            const float4 lx = ld4(nd + 0), hx = ld4(nd + 1), ly = ld4(nd + 2), hy = ld4(nd + 3), lz = ld4(nd + 4),
-                         hz = ld4(nd + 5), cc = ld4(nd + 6);
-            if (COUNT && rep) cnt.nodes++; /* one fetch per wave */
-            const float tmax_c = t_slack(any_hit ? tmax : best_t);
-            const float lxs[4] = {lx.x, lx.y, lx.z, lx.w}, hxs[4] = {hx.x, hx.y, hx.z, hx.w};
-            const float lys[4] = {ly.x, ly.y, ly.z, ly.w}, hys[4] = {hy.x, hy.y, hy.z, hy.w};
-            const float lzs[4] = {lz.x, lz.y, lz.z, lz.w}, hzs[4] = {hz.x, hz.y, hz.z, hz.w};
-            const int cs[4] = {__float_as_int(cc.x), __float_as_int(cc.y), __float_as_int(cc.z),
-                               __float_as_int(cc.w)};
-            float key[4];
-            int c[4];
-            int nhit = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float x0 = __builtin_fmaf(lxs[i], inv.x, -oi.x), x1 = __builtin_fmaf(hxs[i], inv.x, -oi.x);
-                const float y0 = __builtin_fmaf(lys[i], inv.y, -oi.y), y1 = __builtin_fmaf(hys[i], inv.y, -oi.y);
-                const float z0 = __builtin_fmaf(lzs[i], inv.z, -oi.z), z1 = __builtin_fmaf(hzs[i], inv.z, -oi.z);
-                const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
-                                                 __builtin_fmaxf(__builtin_fminf(z0, z1), tmin_c));
-                const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
-                                                 __builtin_fminf(__builtin_fmaxf(z0, z1), tmax_c));
-                const bool h = live && (tn <= tf) && (cs[i] != RT_EMPTY_CHILD);
-                const bool any = __any(h);
-                /* the first participating lane's entry distance orders the children */
-                const float k = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(tn)));
-                key[i] = any ? k : kInf;
-                c[i] = cs[i];
-                nhit += any ? 1 : 0;
-            }
-            if (nhit == 0) {
-                if (sp == 0) break;
-                --sp;
-                node = __builtin_amdgcn_readfirstlane(wstack[sp]);
-                continue;
-            }
-            cas(key[0], c[0], key[1], c[1]);
-            cas(key[2], c[2], key[3], c[3]);
-            cas(key[0], c[0], key[2], c[2]);
-            cas(key[1], c[1], key[3], c[3]);
-            cas(key[1], c[1], key[2], c[2]);
-            if (nhit >= 4) wstack[sp++] = c[3];
-            if (nhit >= 3) wstack[sp++] = c[2];
-            if (nhit >= 2) wstack[sp++] = c[1];
-            node = __builtin_amdgcn_readfirstlane(c[0]);
-            continue;
-        }
-        const int enc = ~node;
-        const int first = enc >> 3, count = (enc & 7) + 1;
-        for (int k = 0; k < count; ++k) {
-            const int s = first + k;
-            const float4 a = ld4(tris + 3 * s), b = ld4(tris + 3 * s + 1), cc = ld4(tris + 3 * s + 2);
-            if (COUNT && rep) cnt.tests++; /* one fetch per wave */
-            float t;
-            if (live && mt_test(o, d, a, b, cc, t)) {
-                if (any_hit) {
-                    if (t < tmax && t > tmin) {
-                        best = s;
-                        live = false;
-                    }
-                } else {
-                    const int orig = __float_as_int(a.w);
-                    if (!(t < tmin) && (t < best_t || (t == best_t && orig > best_orig))) {
-                        best = s;
-                        best_orig = orig;
-                        best_t = t;
-                    }
-                }
-            }
-        }
-        if (any_hit && !__any(live)) break;
-        if (sp == 0) break;
-        --sp;
-        node = __builtin_amdgcn_readfirstlane(wstack[sp]);
-    }
-    if (!any_hit) tmax = best_t;
-    return best;
-}
-
 /* a launch-uniform float held in an SGPR */
 __device__ __forceinline__ float uniform_f(float v)
 {
@@ -725,14 +537,13 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         start, then the wave steps every running query one node (or leaf) at a
         time until `fetch_k` lanes have completed (or none is running), so lanes
         whose query ended early go back to work instead of idling until the
-        wave's longest query ends.  LINEAR / PACKET: each query runs to
-        completion inside the iteration. */
+        wave's longest query ends.  LINEAR: each query runs to completion inside
+        the iteration (the reference loop, wave-uniform). */
 template <int TRAV, bool COUNT>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
-    constexpr bool PACKET = TRAV == RT_TRAV_PACKET4;
-    constexpr bool RESUME = TRAV == RT_TRAV_BVH2 || TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
-    __shared__ int s_stack[PACKET ? (RT_BLOCK / 64) * kWaveStack : RT_STACK_DEPTH * RT_BLOCK];
+    constexpr bool RESUME = TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
+    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     __shared__ float s_light[kMaxLights * 8];
 
     /* emissive spheres: center.xyz, radius, emission.xyz (materials.h:232, rtcommon.h:97-99) */
@@ -798,6 +609,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const unsigned long long t_k0 = COUNT ? wave_clock() : 0ull;
     /* counting launches: this pixel's start clock, queries and traversal steps */
     unsigned long long pix_t0 = 0, pix_q = 0, pix_steps = 0;
+    /* counting launches with RT_PIXEL_STATS: this pixel's wall clocks by phase (path advance D,
+       refill + camera ray A/B, stepping rounds C) and its loop iterations */
+    unsigned long long pix_d = 0, pix_ab = 0, pix_c = 0, pix_it = 0;
     uint32_t pix_rt0 = 0; /* pixel start (s_memrealtime), RT_PIXEL_STATS diagnostics */
 
     for (;;) {
@@ -942,11 +756,15 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     mode = M_IDLE;
                     costly = false;
                     if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
-                        uint32_t *ps = a.pixel_stats + 4 * ((size_t)yl * a.W + x);
+                        uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
                         ps[0] = pix_rt0;
                         ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         ps[2] = COUNT ? (uint32_t)pix_q : 0u;
                         ps[3] = COUNT ? (uint32_t)pix_steps : 0u;
+                        ps[4] = COUNT ? (uint32_t)(pix_d >> 6) : 0u;
+                        ps[5] = COUNT ? (uint32_t)(pix_ab >> 6) : 0u;
+                        ps[6] = COUNT ? (uint32_t)(pix_c >> 6) : 0u;
+                        ps[7] = COUNT ? (uint32_t)pix_it : 0u;
                     }
                     if (COUNT) {
                         const unsigned long long dt = wave_clock() - pix_t0;
@@ -971,7 +789,12 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         }
         }
 
-        if (COUNT) cnt[RT_CNT_SHADE] += wave_clock() - t_d0;
+        const unsigned long long t_d1 = COUNT ? wave_clock() : 0ull;
+        if (COUNT) {
+            cnt[RT_CNT_SHADE] += t_d1 - t_d0;
+            pix_d += t_d1 - t_d0;
+            ++pix_it;
+        }
         /* ---- A: refill idle lanes from the pixel queue: one atomic per wave,
                 lanes ranked by a prefix popcount of the idle ballot ---- */
         const unsigned long long idle = __ballot(mode == M_IDLE);
@@ -1003,6 +826,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         if (COUNT) {
                             pix_t0 = wave_clock();
                             pix_q = pix_steps = 0;
+                            pix_d = pix_ab = pix_c = pix_it = 0;
                         }
                         acc_x = acc_y = acc_z = 0.0f;
                         sample = 0;
@@ -1047,21 +871,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         }
 
         /* ---- C: ray queries ---- */
-        if (RT_PRIO == 1) {
-            /* the waves that hold box pixels (the long serial chains that end the frame)
-               issue first; scheduling only */
-            if (__any(costly)) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
-        } else if (RT_PRIO == 3) {
-            if (__any(costly)) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(0);
-        } else if (RT_PRIO == 2) {
-            const int nc = __popcll(__ballot(costly));
-            if (nc > 16) __builtin_amdgcn_s_setprio(3);
-            else if (nc > 4) __builtin_amdgcn_s_setprio(2);
-            else if (nc > 0) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
+        /* the waves that hold box pixels (the long serial chains that end the frame) issue
+           at top priority (measured against graded priorities: DESIGN.md §5); scheduling only */
+        if (__any(costly)) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
         const bool pending = (mode == M_CLOSEST || mode == M_SHADOW) && !running && !fin;
         if (RESUME) {
             if (pending) {
@@ -1083,10 +896,21 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 }
             }
             const unsigned long long t_c0 = COUNT ? wave_clock() : 0ull;
+            if (COUNT) pix_ab += t_c0 - t_d1;
             /* a wave holding box pixels (the long serial chains that set the frame time)
                leaves the stepping rounds after fewer completed queries: less idling on the
                critical path, at the price of more (less full) shading passes */
-            const int fetch_k = __any(costly) ? fetch_k_box : fetch_k_all;
+            /* The exit threshold follows the wave's live queries: with few lanes left (the
+               frame's tail, or a small tile) a fixed fetch_k is never reached, and every lane
+               would wait for the wave's longest query before its path moves on — the long
+               serial chains then run at the pace of their slowest neighbours. */
+            const unsigned long long costly_lanes = __ballot(costly);
+            int fetch_k = costly_lanes ? fetch_k_box : fetch_k_all;
+            if (a.fetch_frac) {
+                const int live = __popcll(__ballot(running || fin));
+                const int k_live = (live * (int)a.fetch_frac + 63) >> 6;
+                fetch_k = fetch_k < k_live ? fetch_k : (k_live > 1 ? k_live : 1);
+            }
             for (;;) {
                 /* RT_STEP_UNROLL steps per exit check (fewer wave-level ballots and branches) */
 #pragma unroll
@@ -1108,37 +932,27 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     if (COUNT) ++cnt[5];
                 }
                 if (!__any(running)) break;
-                if (__popcll(__ballot(fin)) >= fetch_k) break;
+                const unsigned long long fin_lanes = __ballot(fin);
+                if (__popcll(fin_lanes) >= fetch_k) break;
+                /* a box pixel's query completed: its chain (the frame's critical path) moves on */
+                if (a.box_exit && (fin_lanes & costly_lanes)) break;
             }
-            if (COUNT) cnt[6] += wave_clock() - t_c0;
+            if (COUNT) {
+                const unsigned long long dc = wave_clock() - t_c0;
+                cnt[6] += dc;
+                pix_c += dc;
+            }
         } else if (pending) {
-            bool go = true;
-            if (PACKET) {
-                /* one query type per wave and iteration (the majority); the other lanes wait */
-                const int nc = __popcll(__ballot(mode == M_CLOSEST));
-                const int ns = __popcll(__ballot(mode == M_SHADOW));
-                go = (ns > nc) ? (mode == M_SHADOW) : (mode == M_CLOSEST);
-                /* a trivially unoccluded shadow ray never waits */
-                go = go || (mode == M_SHADOW && !(stmax > RT_SMALL_F));
-            }
-            if (go) {
-                const bool shadow = (mode == M_SHADOW);
-                ts.best_t = shadow ? stmax : kInf;
-                ts.best = -1;
-                TravCounts tc = {0u, 0u, 0u};
-                if (!shadow || ts.best_t > RT_SMALL_F) {
-                    if (PACKET)
-                        ts.best = traverse_packet4<COUNT>(nodes, tris, qo, qd, RT_SMALL_F, ts.best_t, shadow,
-                                                          s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
-                    else
-                        ts.best = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, qo, qd, RT_SMALL_F, ts.best_t, shadow,
-                                                        stk, tc);
-                }
-                fin = true;
-                if (COUNT) {
-                    cnt[2] += tc.nodes;
-                    cnt[3] += tc.tests;
-                }
+            const bool shadow = (mode == M_SHADOW);
+            ts.best_t = shadow ? stmax : kInf;
+            ts.best = -1;
+            TravCounts tc = {0u, 0u, 0u};
+            if (!shadow || ts.best_t > RT_SMALL_F)
+                ts.best = traverse<TRAV, COUNT>(nodes, tris, a.n_tris, qo, qd, RT_SMALL_F, ts.best_t, shadow, stk, tc);
+            fin = true;
+            if (COUNT) {
+                cnt[2] += tc.nodes;
+                cnt[3] += tc.tests;
             }
         }
     }
@@ -1332,12 +1146,13 @@ __global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
 
 /* ======================================================================== */
 /* Batch ray queries (hit-index parity).                                     */
-template <int TRAV>
+template <int TRAV, bool COUNT>
 __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restrict__ nodes,
                                                          const float4 *__restrict__ tris, uint32_t n_tris,
                                                          const rt_ray *__restrict__ rays, uint32_t n, int any_hit,
                                                          int32_t *spill, uint32_t spill_cap,
-                                                         int32_t *__restrict__ out_idx, float *__restrict__ out_t)
+                                                         int32_t *__restrict__ out_idx, float *__restrict__ out_t,
+                                                         unsigned long long *__restrict__ counters)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     const uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x;
@@ -1347,12 +1162,13 @@ __global__ __launch_bounds__(RT_BLOCK) void k_trace_rays(const float4 *__restric
     TravCounts tc = {0u, 0u, 0u};
     Stack stk;
     stk.init(s_stack, spill, spill_cap);
-    int s;
-    if (TRAV == RT_TRAV_PACKET4)
-        s = traverse_packet4<false>(nodes, tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0,
-                                    s_stack + (threadIdx.x >> 6) * kWaveStack, tc);
-    else
-        s = traverse<TRAV, false>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0, stk, tc);
+    const int s = traverse<TRAV, COUNT>(nodes, tris, n_tris, v3f(r.o), v3f(r.d), r.tmin, t, any_hit != 0, stk, tc);
+    if (COUNT) { /* counting calls (rt_set_counting): records visited, summed over the rays */
+        atomicAdd(&counters[any_hit ? 1 : 0], 1ull);
+        atomicAdd(&counters[2], (unsigned long long)tc.nodes);
+        atomicAdd(&counters[3], (unsigned long long)tc.tests);
+        atomicAdd(&counters[4], (unsigned long long)tc.leaves);
+    }
     if (any_hit) {
         out_idx[i] = (s >= 0) ? 1 : 0;
         if (out_t) out_t[i] = r.tmax;
@@ -1468,8 +1284,6 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
         else hipLaunchKernelGGL((k_tris<T, false>), grid, block, 0, st, a);                                            \
     } while (0)
     if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR);
-    else if (trav == RT_TRAV_BVH2) RT_LAUNCH_TRIS(RT_TRAV_BVH2);
-    else if (trav == RT_TRAV_PACKET4) RT_LAUNCH_TRIS(RT_TRAV_PACKET4);
     else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q);
     else RT_LAUNCH_TRIS(RT_TRAV_BVH4);
 #undef RT_LAUNCH_TRIS
@@ -1487,27 +1301,25 @@ int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream)
 
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
-                         void *stream)
+                         unsigned long long *counters, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((n + RT_BLOCK - 1) / RT_BLOCK), block(RT_BLOCK);
     const float4 *nd = reinterpret_cast<const float4 *>(nodes);
     const float4 *tr = reinterpret_cast<const float4 *>(tris);
-    if (trav == RT_TRAV_LINEAR)
-        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_LINEAR>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
-                           spill_cap, out_idx, out_t);
-    else if (trav == RT_TRAV_BVH2)
-        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH2>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
-                           spill_cap, out_idx, out_t);
-    else if (trav == RT_TRAV_PACKET4)
-        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_PACKET4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit,
-                           spill, spill_cap, out_idx, out_t);
-    else if (trav == RT_TRAV_BVH4Q)
-        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH4Q>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit,
-                           spill, spill_cap, out_idx, out_t);
-    else
-        hipLaunchKernelGGL((k_trace_rays<RT_TRAV_BVH4>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,
-                           spill_cap, out_idx, out_t);
+#define RT_LAUNCH_TRACE(T)                                                                                             \
+    do {                                                                                                               \
+        if (counters)                                                                                                  \
+            hipLaunchKernelGGL((k_trace_rays<T, true>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,   \
+                               spill_cap, out_idx, out_t, counters);                                                   \
+        else                                                                                                           \
+            hipLaunchKernelGGL((k_trace_rays<T, false>), grid, block, 0, st, nd, tr, n_tris, rays, n, any_hit, spill,  \
+                               spill_cap, out_idx, out_t, counters);                                                   \
+    } while (0)
+    if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRACE(RT_TRAV_LINEAR);
+    else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRACE(RT_TRAV_BVH4Q);
+    else RT_LAUNCH_TRACE(RT_TRAV_BVH4);
+#undef RT_LAUNCH_TRACE
     return (int)hipGetLastError();
 }
 
@@ -1517,11 +1329,6 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
     int e;
     if (trav == RT_TRAV_LINEAR)
         e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true>, &per_cu) : occupancy(k_tris<RT_TRAV_LINEAR, false>, &per_cu);
-    else if (trav == RT_TRAV_BVH2)
-        e = count ? occupancy(k_tris<RT_TRAV_BVH2, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH2, false>, &per_cu);
-    else if (trav == RT_TRAV_PACKET4)
-        e = count ? occupancy(k_tris<RT_TRAV_PACKET4, true>, &per_cu)
-                  : occupancy(k_tris<RT_TRAV_PACKET4, false>, &per_cu);
     else if (trav == RT_TRAV_BVH4Q)
         e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4Q, false>, &per_cu);
     else

@@ -18,9 +18,9 @@
  *   d[11]    first triangle slot of the leaf children (a leaf starts after the
  *            triangles of the leaf children before it)
  *   d[12..15] the four child links written out (rt_internal.h encoding)
- * With RT_QNODE_DWORDS 12 the node is the first 48 B only and the traversal decodes the
- * links from d[3] / d[10] / d[11]; measured 4.9 % slower than reading them (the decode's
- * per-child branches cost more than the fourth load), so 64 B is the default.
+ * (A 48-B form without d[12..15], links decoded from d[3] / d[10] / d[11], measured 4.9 %
+ * slower per frame — the decode's per-child branches cost more than the fourth load — and
+ * was removed)
  */
 #ifndef RT_QUANT_H
 #define RT_QUANT_H
@@ -31,9 +31,7 @@
 
 #include "rt_internal.h"
 
-#ifndef RT_QNODE_DWORDS
-#define RT_QNODE_DWORDS 16 /* 12: 48-B nodes (links from the meta nibbles); 16: + explicit links */
-#endif
+#define RT_QNODE_DWORDS 16 /* dwords per compressed node */
 #define RT_QEXP_MIN (-24)
 #define RT_QEXP_MAX 7
 
@@ -123,9 +121,7 @@ RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
     for (int i = 0; i < 6; ++i) q[4 + i] = planes[i];
     q[10] = (uint32_t)inner_base;
     q[11] = (uint32_t)tri_base;
-#if RT_QNODE_DWORDS == 16
-    for (int k = 0; k < 4; ++k) q[12 + k] = (uint32_t)code[k]; /* explicit links (64-B variant) */
-#endif
+    for (int k = 0; k < 4; ++k) q[12 + k] = (uint32_t)code[k]; /* explicit links */
     return true;
 }
 

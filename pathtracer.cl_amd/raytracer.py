@@ -103,10 +103,9 @@ class RayTracer:
 
     def setTraversal(self, linear) -> None:
         """False/"bvh": 4-wide BVH, compressed nodes (default); "bvh4f": the same tree with full-precision
-        nodes; True/"linear": the reference loop; "bvh2": binary BVH; "packet": wave-coherent 4-wide."""
+        nodes; True/"linear": the reference loop."""
         t = {False: _abi.RT_TRAVERSAL_BVH, True: _abi.RT_TRAVERSAL_LINEAR, "bvh": _abi.RT_TRAVERSAL_BVH,
-             "linear": _abi.RT_TRAVERSAL_LINEAR, "bvh2": _abi.RT_TRAVERSAL_BVH2,
-             "packet": _abi.RT_TRAVERSAL_PACKET, "bvh4f": _abi.RT_TRAVERSAL_BVH4F}[linear]
+             "linear": _abi.RT_TRAVERSAL_LINEAR, "bvh4f": _abi.RT_TRAVERSAL_BVH4F}[linear]
         self._check(self._lib.rt_set_traversal(self._h, t), "rt_set_traversal")
 
     def setBuilder(self, builder: str) -> None:

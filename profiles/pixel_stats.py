@@ -41,13 +41,13 @@ def main():
     rt.rayTrace(out, W, H, 0, kernel=2)  # probe + warm
     rt.rayTrace(out, W, H, 0, kernel=2)
     plain_ms = rt.lastKernelMs()
-    s = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)  # timing: the plain launch
+    s = np.fromfile(dump, np.uint32).reshape(H, W, 8).astype(np.int64)  # timing: the plain launch
     if not s[..., 1].any():  # the library records clocks in counting launches only
         s = None
     rt.setCounting(True)
     rt.rayTrace(out, W, H, 0, kernel=2)
     count_ms = rt.lastKernelMs()
-    sc_ = np.fromfile(dump, np.uint32).reshape(H, W, 4).astype(np.int64)  # queries / steps
+    sc_ = np.fromfile(dump, np.uint32).reshape(H, W, 8).astype(np.int64)  # queries / steps
     if s is None:
         s = sc_
     t0 = s[..., 0].min()

@@ -42,7 +42,7 @@ def test_golden_spheres(name, tracer, pt, golden, golden_meta):
     rt.close()
 
 
-TRAVERSALS = ["bvh", "bvh4f", "bvh2", "packet", "linear"]
+TRAVERSALS = ["bvh", "bvh4f", "linear"]
 
 
 @pytest.mark.parametrize("trav", TRAVERSALS)
@@ -153,7 +153,7 @@ def test_bvh_equals_linear_dragon(tracer, pt):
         rt.setTraversal(trav)
         res[trav] = (rt.traceRays(rays), rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
     rt.setTraversal("bvh")
-    for trav in ("bvh", "bvh2", "packet"):
+    for trav in ("bvh", "bvh4f"):
         for k in range(3):
             np.testing.assert_array_equal(res[trav][k][0], res["linear"][k][0])
             np.testing.assert_array_equal(bits(res[trav][k][1]), bits(res["linear"][k][1]))
@@ -185,7 +185,7 @@ def test_bvh_equals_linear_fuzz_grazing(tracer, pt):
         rt.setTraversal(trav)
         out[trav] = (rt.traceRays(rr), rt.traceRays(rr, any_hit=True))
     rt.setTraversal("bvh")
-    for trav in ("bvh", "bvh2", "packet"):
+    for trav in ("bvh", "bvh4f"):
         np.testing.assert_array_equal(out[trav][0][0], out["linear"][0][0])
         np.testing.assert_array_equal(bits(out[trav][0][1]), bits(out["linear"][0][1]))
         np.testing.assert_array_equal(out[trav][1][0], out["linear"][1][0])
@@ -231,10 +231,10 @@ def test_unhittable_triangles_left_out_of_the_tree(tracer, pt, oracle):
     info = rt.meshInfo()
     assert 0 < info["n_tris_tree"] < nt
     out = {}
-    for trav in ("linear", "bvh", "bvh4f", "bvh2"):
+    for trav in ("linear", "bvh", "bvh4f"):
         rt.setTraversal(trav)
         out[trav] = (rt.traceRays(rr), rt.traceRays(rs, any_hit=True))
-    for trav in ("bvh", "bvh4f", "bvh2"):
+    for trav in ("bvh", "bvh4f"):
         np.testing.assert_array_equal(out[trav][0][0], out["linear"][0][0])
         np.testing.assert_array_equal(bits(out[trav][0][1]), bits(out["linear"][0][1]))
         np.testing.assert_array_equal(out[trav][1][0], out["linear"][1][0])
@@ -469,6 +469,8 @@ def test_errors_are_loud(tracer, pt):
         rt.setMesh(np.array([[0, 0, 0], [1, 0, 0], [np.nan, 1, 0]], np.float32), np.array([[0, 1, 2]], np.int32))
     with pytest.raises(pt.RtError):
         rt.setMesh(np.zeros((3, 3), np.float32), np.array([[0, 1, 3]], np.int32))
+    for retired in (2, 3):  # the binary-tree and packet traversals were removed
+        assert rt._lib.rt_set_traversal(rt._h, retired) == pt._abi.RT_ERR_ARG
     rt.close()
 
 
@@ -538,7 +540,7 @@ def test_ply_mesh_cli_and_oracle(tracer, pt, oracle, tmp_path):
 
 # ---- GPU BVH builder (csrc/rt_build_gpu.hip) ----------------------------------------------
 
-@pytest.mark.parametrize("trav", ["bvh", "bvh4f", "packet"])
+@pytest.mark.parametrize("trav", ["bvh", "bvh4f"])
 @pytest.mark.parametrize("name", TRI_CASES)
 def test_gpu_builder_golden_tris(name, trav, pt, golden, golden_meta):
     """Frames from a GPU-built tree equal the reference kernel's (golden fixtures)."""
@@ -553,9 +555,6 @@ def test_gpu_builder_golden_tris(name, trav, pt, golden, golden_meta):
         rt.rayTrace(out, m["W"], m["H"], p, kernel=2)
         np.testing.assert_array_equal(bits(out), bits(g["frames"][p]), err_msg=f"{name} frame {p}")
     np.testing.assert_array_equal(rt.getSeeds(), g["seeds_out"])
-    rt.setTraversal("bvh2")
-    with pytest.raises(pt.RtError):
-        rt.rayTrace(out, m["W"], m["H"], 0, kernel=2)
     rt.close()
 
 
@@ -597,7 +596,7 @@ def test_gpu_builder_equals_linear(case, pt):
         idx = np.arange(nt * 3, dtype=np.int32).reshape(nt, 3)
     rays, rr, rs = _query_sets(pt, verts)
     res = {}
-    for builder, trav in [("host", "linear"), ("gpu", "bvh"), ("gpu", "bvh4f"), ("gpu", "packet")]:
+    for builder, trav in [("host", "linear"), ("gpu", "bvh"), ("gpu", "bvh4f")]:
         rt = pt.RayTracer(0)
         rt.setBuilder(builder)
         rt.setMesh(verts, idx)

@@ -31,6 +31,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 METRIC = "Mrays/sec + frames/sec at 1920×1080, 871k-tri PLY, 1/2/4/8 MI355X"
+# --scaling weak renders one whole frame per rank: a different quantity, never reported as METRIC
+METRIC_WEAK = "Mrays/sec + frames/sec, one 1920×1080 frame per MI355X (weak scaling, not tile-parallel)"
+N_SIMD, N_CU = 1024, 256  # MI355X: 256 CUs x 4 SIMD-32 (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md: L2 (per XCD, 32 MiB aggregate) ~34.5 TB/s
 NODE_BYTES = {"bvh": 64, "bvh4f": 112, "linear": 0}  # bytes read per node visit, csrc/rt_internal.h + rt_quant.h
@@ -50,10 +53,10 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--sample-rate", type=int, default=None)
     ap.add_argument("--stripe", type=int, default=8)
-    ap.add_argument("--scaling", default="auto", choices=["auto", "strong", "weak"],
-                    help="N > 1: strong = one frame split into row-stripe tiles across ranks; weak = one full "
-                         "frame per rank (turntable views 3 degrees apart), frames gathered to rank 0. auto: weak "
-                         "for the dragon config (its 256-spp pixels are serial chains: DESIGN.md), else strong")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="N > 1: strong (default) = one frame split into row-stripe tiles across ranks, gathered "
+                         "to rank 0 over RCCL; weak = one full frame per rank (turntable views 3 degrees apart), "
+                         "reported under its own metric name (METRIC_WEAK)")
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
     ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "linear"],
                     help="bvh: 4-wide compressed BVH (default); bvh4f: full-precision nodes; linear: the reference loop")
@@ -62,6 +65,7 @@ def parse():
     ap.add_argument("--ply", default=None, help="render this PLY mesh (normalised, SURVEY §8d) instead of "
                     "the synthetic mesh of the config")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-linear-leg", action="store_true", help="skip the GPU linear-traversal leg (N = 1)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline sample duration")
     return ap.parse_args()
 
@@ -107,10 +111,7 @@ def main():
     H = args.height or H
     sr = args.sample_rate or sr
 
-    scaling = args.scaling
-    if scaling == "auto":
-        scaling = "weak" if (cfg == "dragon" and world > 1) else "strong"
-    frames_per_rank = world > 1 and scaling == "weak"
+    frames_per_rank = world > 1 and args.scaling == "weak"
 
     rt = pt.RayTracer(device)
     S = sc.ply_scene() if kernel == pt.RayTracer.KERNEL_TRIS else sc.main_scene()
@@ -191,6 +192,15 @@ def main():
     rt.rayTrace(out, W, H, 0, kernel=kernel, tile=tile)
     cnt = rt.counters()
     rt.setCounting(False)
+    chain = None
+    if world == 1 and kernel == pt.RayTracer.KERNEL_TRIS and not args.linear:
+        chain = critical_chain(rt, pt, W, H, Wp, Hp, seeds0, kernel)
+    # the plain (timed) kernel's frame from seeds0, kept for the bit-exact check against the
+    # reference kernel's CPU render of the same pixels (cpu_baseline)
+    rt.setSeeds(Wp, Hp, seeds0)
+    rt.rayTrace(out, W, H, 0, kernel=kernel, tile=tile)
+    frame0 = out.cpu().numpy().copy() if world == 1 else None
+    seeds_after0 = rt.getSeeds() if world == 1 else None
     rt.setSeeds(Wp, Hp, seeds0)
 
     # W warmup steps, then more (untimed) until the launch time has settled: the first
@@ -245,50 +255,21 @@ def main():
     steps = args.steps
     mrays = rays / elapsed / 1e6
     ms_step = elapsed / steps * 1e3
-    # roofline of the dominant kernel, per launch (rank 0's launches)
-    k_ms = float(np.mean(kernel_ms))
+    k_ms = float(np.mean(kernel_ms))  # the dominant kernel's launches (rank 0), HIP events
     rays_cnt = cnt["rays_closest"] + cnt["rays_shadow"]
-    pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0)) if n_ranks > 1 else H)
-    if kernel == pt.RayTracer.KERNEL_TRIS:
-        alg_bytes = cnt["nodes_visited"] * NODE_BYTES[args.traversal] + cnt["tris_tested"] * TRI_BYTES[args.traversal] + pix * PIXEL_BYTES
-    else:
-        alg_bytes = pix * PIXEL_BYTES
-    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                # the BVH + triangles are L2/MALL-resident (PMC traffic << algorithmic bytes), so
-                # the algorithmic rate is also stated against the aggregate L2 bandwidth
-                "l2_peak": L2_PEAK_GBS, "frac_of_l2": round(achieved / L2_PEAK_GBS, 4),
-                "kernel": f"k_tris<{args.traversal.upper()}>" if kernel == 2 else "k_spheres",
-                "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": int(alg_bytes),
-                "nodes_per_ray": round(cnt["nodes_visited"] / max(rays_cnt, 1), 2),
-                "tris_per_ray": round(cnt["tris_tested"] / max(rays_cnt, 1), 2)}
-    if cnt.get("lane_slots"):
-        # share of lanes doing a node or leaf step per traversal round (resumable BVH queries)
-        roofline["simd_efficiency"] = round((cnt["nodes_visited"] + cnt["leaves_visited"]) / cnt["lane_slots"], 4)
-    if cnt.get("clocks_total"):
-        # share of the waves' time spent in traversal rounds (counting launch, s_memtime)
-        roofline["traversal_time_frac"] = round(cnt["clocks_traversal"] / cnt["clocks_total"], 4)
-        roofline["shade_time_frac"] = round(cnt.get("clocks_shade", 0) / cnt["clocks_total"], 4)
-
-    # HBM traffic per launch from the PMC passes (profiles/run_profile.sh + summarize_pmc.py),
-    # when they were taken on this exact workload and kernel variant
-    tp = ROOT / "profiles" / "pmc_traffic.json"
     workload = workload_name(cfg, n_tris, W, H, sr, args.traversal, args.builder)
-    if tp.exists() and kernel == pt.RayTracer.KERNEL_TRIS and not args.linear and n_ranks == 1:
-        t = json.loads(tp.read_text())
-        if t.get("workload") == workload:
-            roofline["traffic"] = t["hbm_bytes_per_launch"]
-            roofline["traffic_unit"] = "bytes/launch (2*FETCH_SIZE + WRITE_SIZE)"
-            roofline["traffic_source"] = t["source"]
+    pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0)) if n_ranks > 1 else H)
+    roofline = roofline_block(pt, kernel, cnt, args.traversal, pix, k_ms, workload, n_ranks, chain, rays_cnt)
 
-    cpu = None
+    cpu = gpu_linear = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds0, Wp, Hp, kernel, args.cpu_seconds,
-                           verts if n_tris else None, idx if n_tris else None)
+        cpu = cpu_baseline(pt, sc, W, H, sr, S, seeds0, Wp, Hp, kernel, args.cpu_seconds,
+                           verts if n_tris else None, idx if n_tris else None, frame0, seeds_after0)
+        if kernel == pt.RayTracer.KERNEL_TRIS and not args.linear and not args.no_linear_leg:
+            gpu_linear = gpu_linear_leg(rt, pt, W, H, Wp, Hp, seeds0, cpu)
 
     line = {
-        "metric": METRIC,
+        "metric": METRIC_WEAK if frames_per_rank else METRIC,
         "value": round(mrays, 2),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -319,9 +300,136 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if cpu is not None and "gpu_vs_reference_bit_exact" in cpu:
+        line["gpu_vs_reference_bit_exact"] = cpu["gpu_vs_reference_bit_exact"]
+        line["gpu_vs_reference_pixels"] = cpu["gpu_vs_reference_pixels"]
+    if gpu_linear is not None:
+        line["gpu_linear"] = gpu_linear
     print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def critical_chain(rt, pt, W, H, Wp, Hp, seeds0, kernel):
+    """The frame's longest serial chain, timed with the chip to itself: a counting launch with
+    per-pixel clocks (RT_PIXEL_STATS) finds the pixel that took longest, then the row holding it
+    is rendered alone (tile = that row: 30 waves on 256 CUs), so the launch time is that chain's
+    latency.  Its share of the frame time is the roofline's critical-path fraction."""
+    import tempfile
+
+    path = os.path.join(tempfile.gettempdir(), f"bench_pixel_stats_{os.getpid()}.bin")
+    os.environ["RT_PIXEL_STATS"] = path
+    try:
+        rt.setCounting(True)
+        rt.setSeeds(Wp, Hp, seeds0)
+        out = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=kernel)
+        rt.setCounting(False)
+        st = np.fromfile(path, np.uint32).reshape(H, W, 8).astype(np.int64)
+    finally:
+        os.environ.pop("RT_PIXEL_STATS", None)
+        if os.path.exists(path):
+            os.remove(path)
+    dur = (st[..., 1] - st[..., 0]) & 0xFFFFFFFF  # s_memrealtime ticks (100 MHz), low 32 bits
+    y, x = np.unravel_index(int(np.argmax(dur)), dur.shape)
+    row = np.zeros(W * 4, np.float32)
+    best = 1e9
+    for _ in range(2):
+        rt.setSeeds(Wp, Hp, seeds0)
+        rt.rayTrace(row, W, H, 0, kernel=kernel, tile=(1, H, int(y)))
+        best = min(best, rt.lastKernelMs())
+    return {"pixel": [int(x), int(y)], "queries": int(st[y, x, 2]), "steps": int(st[y, x, 3]),
+            "in_frame_ms": round(float(dur[y, x]) / 1e5, 2), "alone_ms": round(best, 2)}
+
+
+def roofline_block(pt, kernel, cnt, traversal, pix, k_ms, workload, n_ranks, chain, rays_cnt):
+    """Fractions of the resources the dominant kernel could be bound by, each <= 1:
+      hbm            PMC HBM bytes per launch (profiles/pmc_roofline.json, FETCH_SIZE x 2 + WRITE_SIZE)
+                     / live kernel time, vs 8 TB/s;
+      valu_issue     PMC VALU wave-instructions per launch, 2 cycles each on 1024 SIMD-32s at the
+                     profiled clock;
+      salu_issue     PMC SALU instructions on 256 scalar units;
+      vmem_address   PMC TA busy cycles / kernel cycles (the gather address path);
+      record_gather  node + triangle records per second (device counters) vs the best random
+                     64-B record rate measured on a table of the scene's size (profiles/gather_ceiling.json);
+      critical_path  the longest pixel chain rendered alone / the frame time.
+    bound = the largest.  Algorithmic bytes (every record counted as fetched) are reported too."""
+    is_tris = kernel == pt.RayTracer.KERNEL_TRIS
+    records = (cnt["nodes_visited"] + cnt["tris_tested"]) if is_tris else 0
+    alg_bytes = (cnt["nodes_visited"] * NODE_BYTES[traversal] + cnt["tris_tested"] * TRI_BYTES[traversal]
+                 if is_tris else 0) + pix * PIXEL_BYTES
+    sec = k_ms * 1e-3
+    fr = {}
+    pm = None
+    tp = ROOT / "profiles" / "pmc_roofline.json"
+    if tp.exists() and n_ranks == 1:
+        pm = json.loads(tp.read_text()).get(workload)
+    if pm:
+        f_ghz = pm["effective_clock_ghz"]
+        fr["hbm"] = {"achieved": pm["hbm_bytes_per_launch"] / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+        fr["valu_issue"] = {"achieved": pm["sq_insts_valu"] / sec / 1e9, "peak": N_SIMD * f_ghz / 2,
+                            "unit": "G wave-instr/s"}
+        if pm.get("sq_insts_salu"):
+            fr["salu_issue"] = {"achieved": pm["sq_insts_salu"] / sec / 1e9, "peak": N_CU * f_ghz,
+                                "unit": "G instr/s"}
+        if pm.get("ta_busy_avr"):
+            fr["vmem_address"] = {"achieved": pm["ta_busy_avr"] / sec / 1e9, "peak": f_ghz,
+                                  "unit": "G busy cycles/s per TA"}
+    gp = ROOT / "profiles" / "gather_ceiling.json"
+    if is_tris and gp.exists() and traversal != "linear":
+        g = json.loads(gp.read_text())
+        fr["record_gather"] = {"achieved": records / sec / 1e9, "peak": g["best_grec_per_s"], "unit": "G records/s",
+                               "ceiling": g["source"]}
+    if chain:
+        fr["critical_path"] = {"achieved": chain["alone_ms"], "peak": round(k_ms, 3), "unit": "ms (chain alone / frame)",
+                               **chain}
+    for v in fr.values():
+        v["frac"] = round(v["achieved"] / v["peak"], 4)
+        v["achieved"] = round(v["achieved"], 3)
+        v["peak"] = round(v["peak"], 3)
+    bound = max(fr, key=lambda k: fr[k]["frac"]) if fr else "hbm"
+    top = fr.get(bound) or {"achieved": alg_bytes / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s (algorithmic)"}
+    over = sorted(k for k, v in fr.items() if v["frac"] > 1.0)
+    out = {"bound": bound, "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
+           "frac": top.get("frac", round(top["achieved"] / top["peak"], 4)),
+           "traffic": pm["hbm_bytes_per_launch"] if pm else None,
+           "traffic_unit": "HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE, PMC)" if pm else None,
+           "traffic_source": pm["source"] if pm else None,
+           "fractions": fr,
+           "fractions_over_1": over,
+           "kernel": (f"k_tris<{traversal.upper()}>" if is_tris else "k_spheres"),
+           "kernel_ms": round(k_ms, 3),
+           "algorithmic_bytes_per_launch": int(alg_bytes),
+           "algorithmic_gbps": round(alg_bytes / sec / 1e9, 1)}
+    if is_tris:
+        out["nodes_per_ray"] = round(cnt["nodes_visited"] / max(rays_cnt, 1), 2)
+        out["tris_per_ray"] = round(cnt["tris_tested"] / max(rays_cnt, 1), 2)
+    if cnt.get("lane_slots"):
+        out["simd_efficiency"] = round((cnt["nodes_visited"] + cnt["leaves_visited"]) / cnt["lane_slots"], 4)
+    return out
+
+
+def host_cpus():
+    """CPUs this process may use: the affinity mask, capped by the cgroup CPU quota (a GPU box's
+    share is a quota over a larger machine), with nproc and the CPU model for the report."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": min(aff, quota) if quota else aff, "nproc": os.cpu_count(), "affinity": aff,
+            "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
 TRAVERSAL_NAMES = {"bvh": "4-wide compressed BVH", "bvh4f": "4-wide BVH", "linear": "linear (reference)"}
@@ -342,19 +450,22 @@ def _workload_name(cfg, n_tris, W, H, sr, traversal):
     return f"raytrace spheres main.cpp scene {W}x{H}, sampleRate {sr}, progressive frames (row-shifted seeds)"
 
 
-def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, verts, idx):
+def cpu_baseline(pt, sc, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, verts, idx, frame0, seeds_after0):
     """The reference's own kernel (clrt/ocl/raytracer.cl compiled for x86-64 from its source,
     oracle/_ref/libptref.so: kind "reference") on the host cores, on a bounded sample of the
     same frame: whole pixels (all sr*sr samples) strided over the frame.  Rays are counted by
-    the oracle (oracle/pt_oracle.c, the bit-identical restatement) on the same pixels, untimed,
-    and the two renders of the sample are compared bit for bit.  Without oracle/_ref (it is
-    built in the container from /root/reference), the oracle itself is timed (kind "port")."""
+    the oracle (oracle/pt_oracle.c, the bit-identical restatement) on the same pixels, untimed.
+    Checks: the two CPU renders agree bit for bit, and the GPU's plain-kernel frame from the same
+    seeds (frame0, seeds_after0) equals the reference on every sampled pixel and seed slot
+    (gpu_vs_reference_bit_exact).  Without oracle/_ref (built in the container from
+    /root/reference) the oracle itself is timed (kind "port")."""
     sys.path.insert(0, str(ROOT / "oracle"))
     from oracle import LIBREF, Oracle, Reference
 
     orc = Oracle()
     ref = Reference(build_if_missing=False) if LIBREF.exists() else None
-    threads = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+    hc = host_cpus()
+    threads = hc["threads"]
     cam = sc.camera_spherical(W, **(sc.PLY_CAMERA if kernel == 2 else sc.MAIN_CAMERA))
     out = np.zeros(W * H * 4, np.float32)
     out_o = np.zeros_like(out)
@@ -363,9 +474,7 @@ def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, vert
     closest = shadow = 0
     dt = 0.0
     batches = 0
-    exact = True
-    # batches of whole pixels, strided over the frame with a different phase per batch, until
-    # the timed renders have taken target_s seconds (bounded)
+    sampled = []
     if kernel != 2:  # sphere scene: one full frame (a few seconds on the host cores)
         t0 = time.perf_counter()
         if ref is not None:
@@ -375,6 +484,9 @@ def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, vert
         dt = time.perf_counter() - t0
         closest, shadow = orc.render_spheres(out_o, cam, S, W, H, Wp, Hp, sr, 6, 0, sd_o, nthreads=threads)
         batches = 1
+        sampled = np.arange(W * H, dtype=np.int64)
+    # batches of whole pixels, strided over the frame with a different phase per batch, until
+    # the timed renders have taken target_s seconds (bounded)
     n_px = threads
     stride = W * H // n_px
     while kernel == 2 and dt < target_s and batches < 64:
@@ -390,6 +502,10 @@ def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, vert
         closest += c
         shadow += s
         batches += 1
+        sampled.append(pix.astype(np.int64))
+    if kernel == 2:
+        sampled = np.unique(np.concatenate(sampled))
+    exact = True
     if ref is not None:
         exact = bool(np.array_equal(out.view(np.uint32), out_o.view(np.uint32)) and np.array_equal(sd, sd_o))
     rays = closest + shadow
@@ -400,10 +516,47 @@ def cpu_baseline(pt, sc, cfg, W, H, sr, S, seeds, Wp, Hp, kernel, target_s, vert
         sample = f"full {W}x{H} frame"
     res = {"value": round(rays / dt / 1e6, 6), "unit": "Mrays/s", "cores": threads,
            "kind": "reference" if ref is not None else "port", "sample": sample, "seconds": round(dt, 2),
-           "rays": int(rays)}
+           "rays": int(rays), **{k: v for k, v in hc.items() if k != "threads"}}
     if ref is not None:
         res["source"] = "clrt/ocl/raytracer.cl compiled for x86-64 (oracle/Makefile ref), one work-item per pixel"
         res["bit_exact_vs_oracle"] = exact
+    if frame0 is not None:
+        # the GPU frame (plain kernel, same seeds) against the CPU render, on the sampled pixels
+        # and their seed slots (both planes; raytrace_tris reads unshifted slots, the sphere
+        # frame is progression 0, so slot = y * Wpad + x either way)
+        g = frame0.reshape(-1, 4)[sampled].view(np.uint32)
+        r = out.reshape(-1, 4)[sampled].view(np.uint32)
+        slots = (sampled // W) * Wp + (sampled % W)
+        plane = Wp * Hp
+        ok = (np.array_equal(g, r) and np.array_equal(seeds_after0[slots], sd[slots])
+              and np.array_equal(seeds_after0[plane + slots], sd[plane + slots]))
+        res["gpu_vs_reference_bit_exact"] = bool(ok)
+        res["gpu_vs_reference_pixels"] = int(len(sampled))
+    return res
+
+
+def gpu_linear_leg(rt, pt, W, H, Wp, Hp, seeds0, cpu):
+    """The same algorithm as the CPU baseline on the GPU: the reference's linear
+    loop over every triangle (RT_TRAVERSAL_LINEAR) on the whole frame at sampleRate 1 (a 256-spp
+    linear frame would take tens of minutes; a partial frame is bound by its longest pixel
+    chain rather than by throughput)."""
+    sr0 = rt.getSampleRate()
+    rt.setTraversal("linear")
+    rt.setSampleRate(1)
+    buf = np.zeros(W * H * 4, np.float32)
+    rt.setSeeds(Wp, Hp, seeds0)
+    rt.rayTrace(buf, W, H, 0, kernel=2)
+    ms = rt.lastKernelMs()
+    c = rt.counters()
+    rt.setTraversal("bvh")
+    rt.setSampleRate(sr0)
+    rt.setSeeds(Wp, Hp, seeds0)
+    rays = c["rays_closest"] + c["rays_shadow"]
+    v = rays / (ms * 1e-3) / 1e6
+    res = {"value": round(v, 4), "unit": "Mrays/s", "kernel_ms": round(ms, 1), "rays": int(rays),
+           "sample": f"the full {W}x{H} frame at sampleRate 1, linear traversal (every triangle per query)"}
+    if cpu and cpu.get("value"):
+        res["vs_cpu_baseline"] = round(v / cpu["value"], 2)
     return res
 
 

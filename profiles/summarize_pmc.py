@@ -1,82 +1,104 @@
-"""Summarise a profiles/run_profile.sh run into profiles/<tag>/pmc_summary.json.
+"""Summarise the rocprofv3 passes of one bench command into profiles/<tag>/pmc_summary.json and
+refresh the workload's entry in profiles/pmc_roofline.json (read by bench.py's roofline).
 
-Per launch of the timed triangle kernel (k_tris<false, false>):
-  - HBM traffic: FETCH_SIZE and WRITE_SIZE (KB, rocprofv3 derived counters) from their own
-    --pmc passes; gfx950 correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 64 B per
-    128-B request (½ of the bytes of wide reads), so read bytes = 2 x FETCH_SIZE x 1024
-    (an upper bound for this kernel's 16-B/lane gathers, whose width is uncalibrated);
-    WRITE_SIZE x 1024 is exact for 16-B/lane stores.
-  - L2 hit rate, SQ wave-cycle breakdown, VALU instruction count, effective clock.
-Also refreshes profiles/pmc_traffic.json, which bench.py reads for its roofline.traffic.
+Input: gpurun_out/prof_<tag>/ from profiles/run_profile.sh (kernel trace + pmc_* passes) and
+profiles/pmc_extra.sh (pmcx_* passes), every pass its own `rocprofv3 --pmc` run.
 
-    python profiles/summarize_pmc.py <tag> [gpurun_out/prof_<tag>] [workload]
+Per launch of the timed kernel (default k_tris<4, false>; k_spheres<false> for the sphere
+config), with the gfx950 rules of MI355X_MICROARCH.md §HBM:
+  - HBM traffic: read bytes = 2 x FETCH_SIZE x 1024 (FETCH_SIZE counts 64 B per 128-B request:
+    an upper bound for 16-B/lane gathers), write bytes = WRITE_SIZE x 1024;
+  - VALU issue: SQ_INSTS_VALU wave-instructions, 2 cycles each on a SIMD-32 (wave64), over
+    1024 SIMDs x kernel cycles (GRBM_GUI_ACTIVE / 8 XCDs);
+  - SALU issue: SQ_INSTS_SALU over 256 scalar units x kernel cycles;
+  - vector-memory address path: TA_BUSY_avr / kernel cycles;
+  - L2 hit rate, wave-cycle breakdown, effective clock.
+
+    python profiles/summarize_pmc.py <tag> [gpurun_out/prof_<tag>] [workload] [kernel]
 """
 from __future__ import annotations
 
 import csv
+import glob
 import json
 import sys
 from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-KERNEL = "k_tris<4, false>"
+N_CU, N_SIMD, N_XCD = 256, 1024, 8
 
 
-def counters(path: Path):
-    out = defaultdict(dict)
-    if not path.exists():
-        return out
-    for r in csv.DictReader(open(path)):
-        if KERNEL in r["Kernel_Name"]:
-            out[int(r["Dispatch_Id"])][r["Counter_Name"]] = out[int(r["Dispatch_Id"])].get(r["Counter_Name"], 0.0) + float(
-                r["Counter_Value"])
-    return out
-
-
-def mean_counter(d, name):
-    vals = [v[name] for v in d.values() if name in v]
-    return sum(vals) / len(vals) if vals else None
+def counters(paths, kernel):
+    """mean over dispatches of the kernel, per counter, over the given collection files"""
+    tot = defaultdict(list)
+    for path in paths:
+        per = defaultdict(lambda: defaultdict(float))
+        for r in csv.DictReader(open(path)):
+            if kernel in r["Kernel_Name"]:
+                per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        for d in per.values():
+            for k, v in d.items():
+                tot[k].append(v)
+    return {k: sum(v) / len(v) for k, v in tot.items()}
 
 
 def main():
     tag = sys.argv[1]
     src = Path(sys.argv[2]) if len(sys.argv) > 2 else ROOT / "gpurun_out" / f"prof_{tag}"
     workload = sys.argv[3] if len(sys.argv) > 3 else None
-    c = {}
-    for sub in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
-        d = counters(src / f"pmc_{sub}" / "run_counter_collection.csv")
-        for name in {k for v in d.values() for k in v}:
-            c[name] = mean_counter(d, name)
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_tris<4, false>"
+    files = sorted(glob.glob(f"{src}/pmc_*/run_counter_collection.csv")) + sorted(
+        glob.glob(f"{src}/pmcx_*/run_counter_collection.csv"))
+    c = counters(files, kernel)
     stats = list(csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")))
-    k = next(r for r in stats if KERNEL in r["Name"])
+    k = next(r for r in stats if kernel in r["Name"])
     avg_ns = float(k["AverageNs"])
+    cyc = c["GRBM_GUI_ACTIVE"] / N_XCD if c.get("GRBM_GUI_ACTIVE") else None
     fetch_b = 2 * c["FETCH_SIZE"] * 1024 if c.get("FETCH_SIZE") else None
     write_b = c["WRITE_SIZE"] * 1024 if c.get("WRITE_SIZE") else None
+
+    def frac(num, den):
+        return num / den if (num is not None and den) else None
+
     summ = {
-        "kernel": KERNEL,
+        "kernel": kernel,
         "avg_kernel_ms_rocprof": avg_ns / 1e6,
+        "dispatches": int(k.get("Calls", 0) or 0),
         "fetch_size_kb": c.get("FETCH_SIZE"),
         "write_size_kb": c.get("WRITE_SIZE"),
         "hbm_read_bytes_corrected": fetch_b,
         "hbm_write_bytes": write_b,
         "hbm_bytes_per_launch": (fetch_b or 0) + (write_b or 0),
         "hbm_gbps": ((fetch_b or 0) + (write_b or 0)) / (avg_ns * 1e-9) / 1e9,
-        "l2_hit_rate": c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]) if c.get("TCC_HIT_sum") else None,
-        "sq_wait_any_frac": c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"] if c.get("SQ_WAVE_CYCLES") else None,
-        "sq_active_inst_frac": c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"] if c.get("SQ_WAVE_CYCLES") else None,
+        "l2_hit_rate": frac(c.get("TCC_HIT_sum"), (c.get("TCC_HIT_sum") or 0) + (c.get("TCC_MISS_sum") or 0)),
+        "kernel_cycles_per_xcd": cyc,
+        "effective_clock_ghz": cyc / (avg_ns * 1e-9) / 1e9 if cyc else None,
         "sq_insts_valu": c.get("SQ_INSTS_VALU"),
-        "effective_clock_ghz": c["GRBM_GUI_ACTIVE"] / 8 / (avg_ns * 1e-9) / 1e9 if c.get("GRBM_GUI_ACTIVE") else None,
+        "sq_insts_salu": c.get("SQ_INSTS_SALU"),
+        "sq_insts_vmem_rd": c.get("SQ_INSTS_VMEM_RD"),
+        "sq_insts_lds": c.get("SQ_INSTS_LDS"),
+        "ta_busy_avr": c.get("TA_BUSY_avr"),
+        "valu_issue_frac": frac(c["SQ_INSTS_VALU"] / N_SIMD * 2, cyc) if c.get("SQ_INSTS_VALU") else None,
+        "salu_issue_frac": frac(c["SQ_INSTS_SALU"] / N_CU, cyc) if c.get("SQ_INSTS_SALU") else None,
+        "ta_busy_frac": frac(c.get("TA_BUSY_avr"), cyc),
+        "sq_wait_any_frac": frac(c.get("SQ_WAIT_ANY"), c.get("SQ_WAVE_CYCLES")),
+        "sq_active_inst_frac": frac(c.get("SQ_ACTIVE_INST_ANY"), c.get("SQ_WAVE_CYCLES")),
+        "counters": c,
     }
     out = ROOT / "profiles" / tag
     out.mkdir(parents=True, exist_ok=True)
     (out / "pmc_summary.json").write_text(json.dumps(summ, indent=1) + "\n")
     if workload:
-        (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(
-            {"tag": tag, "workload": workload, "kernel": KERNEL,
-             "hbm_bytes_per_launch": summ["hbm_bytes_per_launch"],
-             "source": f"profiles/{tag}/pmc_summary.json"}, indent=1) + "\n")
-    print(json.dumps(summ, indent=1))
+        p = ROOT / "profiles" / "pmc_roofline.json"
+        allw = json.loads(p.read_text()) if p.exists() else {}
+        allw[workload] = {key: summ[key] for key in (
+            "kernel", "avg_kernel_ms_rocprof", "hbm_bytes_per_launch", "effective_clock_ghz", "sq_insts_valu",
+            "sq_insts_salu", "ta_busy_avr", "kernel_cycles_per_xcd", "valu_issue_frac", "salu_issue_frac",
+            "ta_busy_frac", "l2_hit_rate")}
+        allw[workload]["source"] = f"profiles/{tag}/pmc_summary.json"
+        p.write_text(json.dumps(allw, indent=1) + "\n")
+    print(json.dumps({k: v for k, v in summ.items() if k != "counters"}, indent=1))
 
 
 if __name__ == "__main__":

@@ -10,6 +10,18 @@
  *
  * The scene is re-uploaded only when it changed, as RayTracerCL does when the
  * sphere count changes (RayTracerCL.cpp:251-264).
+ *
+ * Source compatibility with the reference's callers (clrt/main.cpp, plymain.cpp,
+ * GlutCLWindow.cpp): when the reference's own headers are on the include path
+ * (-I<reference>/clrt/ocl for geometry.h, -I<reference>/include for gmtl), the
+ * overloads taking its types are compiled in:
+ *   addSphere / removeSphere (Sphere const &)              RayTracer.h:68-69
+ *   setCameraMatrix(gmtl::Matrix44f const &)               RayTracer.h:56
+ *   setCameraSpherical(gmtl::Point3f const &, el, az, d)   RayTracer.h:57
+ * so `window.rayTracer.addSphere(sphere)` and
+ * `setCameraSpherical(gmtl::Point3f(0, -4, -0), 14.0f, 118.0f, 5)` compile unchanged
+ * (tests/cpp/ref_main_replay.cpp replays main.cpp / plymain.cpp through this class).
+ * Define RT_HIP_NO_REFERENCE_TYPES to leave them out.
  */
 #ifndef RAYTRACER_HIP_HPP
 #define RAYTRACER_HIP_HPP
@@ -20,6 +32,18 @@
 #include <vector>
 
 #include "pathtracer_rt.h"
+
+#if !defined(RT_HIP_NO_REFERENCE_TYPES) && defined(__has_include)
+#if __has_include("geometry.h") && __has_include(<CL/cl.h>)
+#include "geometry.h" /* clrt/ocl/geometry.h: Sphere, material_t, vec3 */
+#define RT_HIP_HAVE_REF_GEOMETRY 1
+#endif
+#if __has_include(<gmtl/Matrix.h>) && __has_include(<gmtl/Point.h>)
+#include <gmtl/Matrix.h>
+#include <gmtl/Point.h>
+#define RT_HIP_HAVE_GMTL 1
+#endif
+#endif
 
 class RayTracerHIP {
 public:
@@ -49,6 +73,16 @@ public:
         check(rt_set_fov(ctx_, fovDeg), "setFoVAngle");
     }
     float getFoVAngle() const { return fov_; }
+#ifdef RT_HIP_HAVE_GMTL
+    /* gmtl stores matrices column-major (gmtl/Matrix.h: getData()), the order
+       rt_set_view_matrix takes. */
+    void setCameraMatrix(gmtl::Matrix44f const &mat) { setCameraMatrix(mat.getData()); }
+    void setCameraSpherical(gmtl::Point3f const &target, float elevationDeg, float azimuthDeg, float distance)
+    {
+        const float t[3] = {target[0], target[1], target[2]};
+        setCameraSpherical(t, elevationDeg, azimuthDeg, distance);
+    }
+#endif
 
     /* ---- settings: RayTracer.h:62-66 ---- */
     void setSampleRate(unsigned s)
@@ -81,6 +115,29 @@ public:
                 return;
             }
     }
+#ifdef RT_HIP_HAVE_REF_GEOMETRY
+    /* The reference's Sphere (geometry.h:156-163), copied field by field into the
+       80-byte rt_sphere record the kernels read (same members, same order). */
+    static rt_sphere to_rt(Sphere const &r)
+    {
+        rt_sphere s;
+        s.mat.diffuse = {r.mat.diffuse.x, r.mat.diffuse.y, r.mat.diffuse.z};
+        s.mat.kd = r.mat.kd;
+        s.mat.extinction = {r.mat.extinction.x, r.mat.extinction.y, r.mat.extinction.z};
+        s.mat.kt = r.mat.kt;
+        s.mat.emission = {r.mat.emission.x, r.mat.emission.y, r.mat.emission.z};
+        s.mat.emission_power = r.mat.emission_power;
+        s.mat.ks = r.mat.ks;
+        s.mat.specExp = r.mat.specExp;
+        s.mat.ior = r.mat.ior;
+        s.mat.refExp = r.mat.refExp;
+        s.center = {r.center.x, r.center.y, r.center.z};
+        s.radius = r.radius;
+        return s;
+    }
+    void addSphere(Sphere const &sphere) { addSphere(to_rt(sphere)); }
+    void removeSphere(Sphere const &sphere) { removeSphere(to_rt(sphere)); }
+#endif
     void clearSpheres()
     {
         spheres_.clear();

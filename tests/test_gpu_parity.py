@@ -283,8 +283,9 @@ def test_unhittable_triangles_left_out_of_the_tree(tracer, pt, oracle):
 
 
 @pytest.mark.parametrize("kernel,prog", [(2, 0), (2, 3), (0, 0), (1, 2)])
-def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt):
-    """Row-stripe tiles (the multi-GPU partition) reassemble to the single-device frame."""
+def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt, oracle):
+    """Row-stripe tiles (the multi-GPU partition) reassemble to the single-device frame,
+    which equals the oracle's frame (and seeds) bit for bit."""
     sc = pt.scenes
     from importlib import import_module
 
@@ -312,6 +313,15 @@ def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt):
     rt.rayTrace(full, W, H, prog, kernel=kernel)
     full_seeds = rt.getSeeds()
     rt.close()
+    # the single-device frame the tiles must reassemble to is itself the oracle's
+    exp = prev.copy().reshape(-1)
+    sd = seeds.copy()
+    if kernel == 2:
+        oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, prog, sd, verts, idx)
+    else:
+        oracle.render_spheres(exp, cam, S, W, H, Wp, Hp, sr, 6, prog, sd, single_sample=kernel == 1)
+    np.testing.assert_array_equal(bits(full), bits(exp))
+    np.testing.assert_array_equal(full_seeds, sd)
     for n_ranks, stripe in [(2, 8), (3, 5), (4, 16)]:
         tiles = []
         for r in range(n_ranks):
@@ -328,12 +338,13 @@ def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt):
 
 
 @pytest.mark.parametrize("n_ranks,stripe,H", [(2, 8, 53), (3, 4, 45)])
-def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt):
+def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt, oracle):
     """raytrace (row-shifted seeds) on row-stripe tiles over progressive frames, with the
     seed-row halo moved between contexts through device buffers (rt_pack/unpack_seed_rows,
     the path dist.exchange_seed_rows drives over RCCL): every frame reassembles bit-exactly
-    to the single-device frame, and every seed row equals the single-device seeds on its
-    last writer.  Includes a restart (progression back to 0)."""
+    to the single-device frame (itself equal to the oracle's frames and seeds), and every
+    seed row equals the single-device seeds on its last writer.  Includes a restart
+    (progression back to 0)."""
     import torch
     from importlib import import_module
 
@@ -360,9 +371,14 @@ def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt)
     rows = [dist.tile_rows(H, stripe, n_ranks, r) for r in range(n_ranks)]
     tiles = [torch.zeros(len(rows[r]) * W * 4, dtype=torch.float32, device="cuda:0") for r in range(n_ranks)]
     moved = 0
+    exp = np.zeros_like(full)
+    sd = seeds.copy()
     try:
         for p in [0, 1, 2, 3, 4, 0, 1, 2]:
             ref.rayTrace(full, W, H, p, kernel=0)
+            # raytrace's row-shifted seeds (raytracer.cl:20-30) over the same progression
+            oracle.render_spheres(exp, cam, sc.main_scene(), W, H, Wp, Hp, sr, 6, p, sd)
+            np.testing.assert_array_equal(bits(full), bits(exp), err_msg=f"oracle, progression {p}")
             for (src, dst), rws in halo.plan(p).items():
                 buf = torch.empty((2, len(rws), Wp), dtype=torch.int32, device="cuda:0")
                 ranks[src].packSeedRows(rws, buf)
@@ -374,6 +390,7 @@ def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt)
             frame = dist.assemble([t.cpu().numpy().reshape(-1, W, 4) for t in tiles], H, W, stripe)
             np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full), err_msg=f"progression {p}")
         ref_seeds = ref.getSeeds().reshape(2, Hp, Wp)
+        np.testing.assert_array_equal(ref_seeds.reshape(-1), sd)
         got = [rk.getSeeds().reshape(2, Hp, Wp) for rk in ranks]
         for row in range(Hp):
             w = halo.writer[row]
@@ -453,6 +470,161 @@ def test_dragon_full_size_properties(tracer, pt, oracle):
     e = exp.reshape(-1, 4)[pix]
     gpx = out.reshape(-1, 4)[pix]
     np.testing.assert_array_equal(bits(gpx), bits(e))
+
+
+def _pixel_seeds(seeds, pix, Wp, Hp, W):
+    """The two seed-plane words of each pixel's slot (raytrace_tris: y * Wpad + x)."""
+    s = seeds.reshape(2, Hp * Wp)
+    slot = (pix // W) * Wp + pix % W
+    return s[:, slot]
+
+
+def test_dragon_headline_config_vs_oracle(tracer, pt, oracle):
+    """The benchmark's own configuration (BASELINE config 4: 871k tris, 1920x1080,
+    sampleRate 16 = 256 samples per pixel with strat_rand total = 16, maxDepth 6,
+    raytracer.cl:184-243): a strided subset of 24 pixels (mesh and box pixels) and their
+    seed slots are bit-exact against the oracle's linear loop."""
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 16
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp)
+    rt = tracer
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    rt.setSeeds(Wp, Hp, seeds)
+    out = np.zeros(W * H * 4, np.float32)
+    rt.rayTrace(out, W, H, 0, kernel=2)
+    s_gpu = rt.getSeeds()
+    pix = np.arange(4_321, W * H, 86_399, dtype=np.uint32)  # 24 pixels over the frame
+    exp = np.zeros_like(out)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix)
+    np.testing.assert_array_equal(bits(out.reshape(-1, 4)[pix]), bits(exp.reshape(-1, 4)[pix]))
+    np.testing.assert_array_equal(_pixel_seeds(s_gpu, pix, Wp, Hp, W), _pixel_seeds(sd, pix, Wp, Hp, W))
+    assert out.reshape(-1, 4)[pix, :3].max() > 0
+
+
+def test_lucy_class_28m_tris(tracer, pt, oracle):
+    """BASELINE config 5's mesh (Lucy class, 28,055,742 triangles) at reduced resolution.
+    Under the reference's absolute |det| < 1e-4 rule (geometryFuncs.h:167) no unit ray can
+    accept any of its triangles, so the host build's tree holds almost none of them
+    (DESIGN §6); the GPU LBVH keeps all 28M.  Both trees render the same bits (16 spp);
+    a pixel subset equals the oracle's linear loop over all 28M triangles; and on the full
+    28M tree, rays long enough to pass the det rule hit real triangles with BVH == linear."""
+    sc = pt.scenes
+    n = sc.MESH_CONFIGS["lucy"]
+    verts, idx = sc.make_mesh(n)
+    S = sc.ply_scene()
+    W, H = 192, 144
+    Wp, Hp = sc.padded_dims(W, H)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=11)
+
+    def make(builder):
+        rt = pt.RayTracer(0)
+        rt.setSpheres(S)
+        rt.setCamera(cam)
+        rt.setMaxPathDepth(6)
+        rt.setBuilder(builder)
+        rt.setMesh(verts, idx)
+        return rt
+
+    culled, full = make("host"), make("gpu")
+    try:
+        assert culled.meshInfo()["n_tris_tree"] < 16
+        assert full.meshInfo()["n_tris_tree"] == n
+        frames = []
+        for rt in (culled, full):
+            rt.setSampleRate(4)
+            rt.setSeeds(Wp, Hp, seeds)
+            f = np.zeros(W * H * 4, np.float32)
+            rt.rayTrace(f, W, H, 0, kernel=2)
+            frames.append((f, rt.getSeeds()))
+        np.testing.assert_array_equal(bits(frames[0][0]), bits(frames[1][0]))
+        np.testing.assert_array_equal(frames[0][1], frames[1][1])
+        # oracle subset at sampleRate 1 (the oracle walks all 28M triangles per ray)
+        culled.setSampleRate(1)
+        culled.setSeeds(Wp, Hp, seeds)
+        got = np.zeros(W * H * 4, np.float32)
+        culled.rayTrace(got, W, H, 0, kernel=2)
+        pix = np.arange(97, W * H, W * H // 16, dtype=np.uint32)
+        exp = np.zeros_like(got)
+        sd = seeds.copy()
+        oracle.render_tris(exp, cam, S, W, H, Wp, Hp, 1, 6, 0, sd, verts, idx, pixels=pix)
+        np.testing.assert_array_equal(bits(got.reshape(-1, 4)[pix]), bits(exp.reshape(-1, 4)[pix]))
+        np.testing.assert_array_equal(_pixel_seeds(culled.getSeeds(), pix, Wp, Hp, W),
+                                      _pixel_seeds(sd, pix, Wp, Hp, W))
+        # closest hits on the full 28M-triangle tree: directions 100x unit length
+        rng = np.random.default_rng(5)
+        m = 2048
+        v = verts.reshape(-1, 3)
+        tri = rng.integers(0, n, m)
+        tgt = v[idx[tri]].mean(axis=1)
+        o = tgt + rng.normal(size=(m, 3)) * 3.0
+        d = tgt - o
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        rr = np.zeros(m, pt._abi.RAY_DTYPE)
+        rr["o"] = o.astype(np.float32)
+        rr["d"] = (d * 100.0).astype(np.float32)
+        rr["tmin"] = np.float32(1e-6)
+        rr["tmax"] = np.float32(np.inf)
+        full.setTraversal("bvh")
+        got_h = full.traceRays(rr)
+        full.setTraversal("linear")
+        exp_h = full.traceRays(rr)
+        np.testing.assert_array_equal(got_h[0], exp_h[0])
+        np.testing.assert_array_equal(bits(got_h[1]), bits(exp_h[1]))
+        assert (exp_h[0] >= 0).sum() > m // 2
+        # and the oracle agrees on a sample of them
+        oh = oracle.closest_hits(rr[:64], verts, idx)
+        np.testing.assert_array_equal(oh[0], exp_h[0][:64])
+        np.testing.assert_array_equal(bits(oh[1]), bits(exp_h[1][:64]))
+    finally:
+        culled.close()
+        full.close()
+
+
+@pytest.mark.parametrize("kernel", [0, 2])
+def test_blurred_refraction_lobe_vs_oracle(kernel, tracer, pt, oracle):
+    """sampleRefraction's blurred lobe (materials.h:183-199, taken when refExp < 1e5): the
+    plymain glass sphere with refExp 40 and a Phong lobe on the mirror, over 3 progressive
+    frames of raytrace and raytrace_tris, bit-exact against the oracle."""
+    sc = pt.scenes
+    S = sc.ply_scene().copy()
+    S["refExp"][1] = 40.0  # the glass sphere (kt 0.8)
+    S["specExp"][2] = 60.0
+    assert S["kt"][1] > 0
+    W, H, sr = 48, 40, 2
+    Wp, Hp = sc.padded_dims(W, H)
+    cam = sc.camera_spherical(W, **sc.MAIN_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=3)
+    verts, idx = sc.make_mesh(3000)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    if kernel == 2:
+        rt.setMesh(verts, idx)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    for p in range(3):
+        rt.rayTrace(got, W, H, p, kernel=kernel)
+        if kernel == 2:
+            oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, p, sd, verts, idx)
+        else:
+            oracle.render_spheres(exp, cam, S, W, H, Wp, Hp, sr, 6, p, sd)
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"progression {p}")
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
+    rt.close()
 
 
 def test_errors_are_loud(tracer, pt):

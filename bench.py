@@ -57,6 +57,10 @@ def parse():
                     help="N > 1: strong (default) = one frame split into row-stripe tiles across ranks, gathered "
                          "to rank 0 over RCCL; weak = one full frame per rank (turntable views 3 degrees apart), "
                          "reported under its own metric name (METRIC_WEAK)")
+    ap.add_argument("--comm", default="native", choices=["native", "torch"],
+                    help="N > 1 strong scaling: native = librtmi's own RCCL communicator (rt_comm_render: "
+                         "seed-row halo + grouped ncclSend/ncclRecv gather + device-side assembly, the C++ "
+                         "host's path); torch = torch.distributed gather (also the gloo rehearsal)")
     ap.add_argument("--linear", action="store_true", help="reference linear traversal instead of the BVH")
     ap.add_argument("--traversal", default="bvh", choices=["bvh", "bvh4f", "linear"],
                     help="bvh: 4-wide compressed BVH (default); bvh4f: full-precision nodes; linear: the reference loop")
@@ -167,8 +171,20 @@ def main():
         rt.packSeedRows(rows, buf)
         return buf
 
+    # native sharding (csrc/rt_comm.hip): librtmi's RCCL communicator renders the rank's
+    # stripes, moves the seed-row halo and assembles the frame on rank 0's GPU
+    comm = None
+    if n_ranks > 1 and args.comm == "native" and dist.get_backend() == "nccl":
+        comm = ptdist.NativeComm.from_torch(device)
+        frame_full = torch.zeros((W * H * 4) if rank == 0 else 4, dtype=torch.float32, device=f"cuda:{device}")
+
     def step():
         p = frame_no[0] if progressive else 0
+        if comm is not None:
+            comm.render(rt, frame_full, W, H, p, kernel, stripe=args.stripe)
+            frame_no[0] += 1
+            c = rt.counters()
+            return c["rays_closest"] + c["rays_shadow"]
         if halo is not None:
             ptdist.exchange_seed_rows(halo.plan(p), pack, rt.unpackSeedRows, Wp, device=halo_dev)
         rt.rayTrace(out, W, H, p, kernel=kernel, tile=tile, halo=halo is not None)
@@ -248,6 +264,8 @@ def main():
         rays = int(r.item())
 
     if rank != 0:
+        if comm is not None:
+            comm.close()
         if dist:
             dist.destroy_process_group()
         return
@@ -290,7 +308,9 @@ def main():
                    "W": W, "H": H, "spp": sr * sr, "n_tris": n_tris,
                    "parallelism": ((f"frames x{world} (one turntable view per rank)" if frames_per_rank
                                     else f"row-stripes({args.stripe})x{world}")
-                                   + ((" + rccl gather" if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl"
+                                   + ((" + librtmi rt_comm (RCCL send/recv gather)" if comm is not None
+                                       else " + rccl gather (torch.distributed)"
+                                       if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl"
                                        else " + gloo gather") if world > 1 else "")),
                    "rays_per_frame": int(rays / steps / (world if frames_per_rank else 1)),
                    # rays = the reference's queries (oracle-equal counts); shadow rays whose answer
@@ -306,6 +326,8 @@ def main():
     if gpu_linear is not None:
         line["gpu_linear"] = gpu_linear
     print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if dist:
         dist.destroy_process_group()
 

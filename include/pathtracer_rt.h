@@ -218,6 +218,48 @@ const char *rt_ply_last_error(void); /* message of the last failed rt_ply_open (
    lowest point on y = floor_y (extent 3 on the box floor y = -5). */
 int rt_normalize_mesh(float *verts_xyz, uint32_t n_verts, float max_extent, float floor_y);
 
+/* ---- multi-GPU from the native host: one process (or thread) per GPU, RCCL over
+   xGMI.  The reference renders on one OpenCL device (RayTracerCL.cpp:52-145,
+   :217-307); this is the sharded form of the same rayTrace call, with no data-path
+   exchange (pixels are independent) besides the frame assembly, plus the seed-row
+   halo of progressive sphere frames.  A communicator is created collectively:
+   rank 0 makes the id, the caller hands the bytes to every rank by any channel
+   (MPI, a file, a TCP store), each rank calls rt_comm_create with its own GPU. ---- */
+typedef struct rt_comm rt_comm;
+#define RT_COMM_ID_BYTES 128
+/* ncclGetUniqueId (rccl.h:187). */
+int rt_comm_get_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+/* ncclCommInitRank (rccl.h:215) on `device`; collective over n_ranks callers. */
+int rt_comm_create(const uint8_t id[RT_COMM_ID_BYTES], int n_ranks, int rank, int device, rt_comm **out);
+int rt_comm_destroy(rt_comm *comm);
+const char *rt_comm_last_error(const rt_comm *comm);
+/* Frame assembly (collective): every rank passes its compact tile (device pointer,
+   rt_tile_rows(H, {stripe, n_ranks, rank}) rows of W RGBA32F pixels); `root` receives
+   them with grouped ncclSend/ncclRecv (one point-to-point xGMI transfer per sender)
+   and scatters the stripes into `frame_dev` (device, W*H*4 floats; others: ignored). */
+int rt_comm_gather_frame(rt_comm *comm, const float *tile_dev, float *frame_dev, uint32_t width, uint32_t height,
+                         uint32_t stripe_rows, int root);
+/* Device-side assembly on one GPU: n_ranks compact tiles (device pointers, rank
+   order) scattered into frame_dev (the root's step of rt_comm_gather_frame). */
+int rt_assemble_tiles(const float *const *tiles_dev, uint32_t n_ranks, uint32_t width, uint32_t height,
+                      uint32_t stripe_rows, float *frame_dev, int device);
+/* Seed-row halo plan (host only).  writer[Hpad]: last rank that wrote each seed row
+   (-1: nobody, the initial seeds are identical on every rank).  Before a raytrace
+   frame with row shift `progressive`, lists the moves (src rank, dst rank, seed row)
+   that bring every row a rank reads up to date; then records the frame's writes in
+   writer.  Capacity of the three output arrays: height entries. */
+int rt_seed_halo_plan(int32_t *writer, uint32_t height, uint32_t hpad, uint32_t stripe_rows, uint32_t n_ranks,
+                      uint32_t progressive, uint32_t *src, uint32_t *dst, uint32_t *rows, uint32_t *n_moves);
+/* One sharded rayTrace (collective): rank renders its stripes into a tile buffer the
+   communicator keeps (progression mixes into it across frames), exchanges the seed-row
+   halo first for RT_KERNEL_SPHERES (grouped ncclSend/ncclRecv of packed rows), then
+   gathers the frame to `root` (frame_dev: device, W*H*4 floats on root).  Bit-identical
+   to rt_render of the whole frame on one GPU.  Call rt_comm_reset_halo after replacing
+   a context's seeds (rt_set_seeds). */
+int rt_comm_render(rt_comm *comm, rt_ctx *ctx, float *frame_dev, uint32_t width, uint32_t height,
+                   uint32_t progression, int kernel, uint32_t stripe_rows, int root);
+int rt_comm_reset_halo(rt_comm *comm);
+
 #ifdef __cplusplus
 }
 #endif

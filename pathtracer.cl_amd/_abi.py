@@ -151,7 +151,18 @@ SIGNATURES = {
     "rt_ply_close": (_i32, [_vp]),
     "rt_ply_last_error": (ctypes.c_char_p, []),
     "rt_normalize_mesh": (_i32, [_vp, _u32, _f32, _f32]),
+    # multi-GPU from the native host (csrc/rt_comm.hip, RCCL)
+    "rt_comm_get_unique_id": (_i32, [_vp]),
+    "rt_comm_create": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)]),
+    "rt_comm_destroy": (_i32, [_vp]),
+    "rt_comm_last_error": (ctypes.c_char_p, [_vp]),
+    "rt_comm_gather_frame": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
+    "rt_assemble_tiles": (_i32, [_vp, _u32, _u32, _u32, _u32, _vp, _i32]),
+    "rt_seed_halo_plan": (_i32, [_vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _vp, ctypes.POINTER(_u32)]),
+    "rt_comm_render": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32, _u32, _i32]),
+    "rt_comm_reset_halo": (_i32, [_vp]),
 }
+RT_COMM_ID_BYTES = 128
 
 _LIB = None
 

@@ -1,0 +1,364 @@
+/*
+ * rt_comm.hip — multi-GPU from the native host: RCCL communicator, frame assembly
+ * and the seed-row halo behind the C-ABI (include/pathtracer_rt.h, "multi-GPU").
+ *
+ * The reference drives one OpenCL device from GlutCLWindow (RayTracerCL.cpp:52-145,
+ * :217-307).  Sharded, every pixel of a frame stays independent (own seed slot, own
+ * read-modify-write of its output pixel, raytracer.cl:20-30, :207-242), so a rank
+ * renders its interleaved row stripes (rt_tile) with a full scene/BVH replica and the
+ * only data-path exchange is the frame assembly on the root: grouped ncclSend /
+ * ncclRecv, one point-to-point xGMI transfer per sender, into a staging buffer that one
+ * kernel scatters into the frame.  raytrace's row-shifted seeds (get_seed/put_seed,
+ * raytracer.cl:20-30) add the seed-row halo: before a progressive frame with shift s,
+ * the rows a rank reads are fetched from their last writer (rt_seed_halo_plan), packed
+ * and moved with the same grouped point-to-point calls.
+ *
+ * Same protocol as pathtracer.cl_amd/dist.py (the torch.distributed form), so a C++
+ * host without Python shards the same way.
+ */
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "pathtracer_rt.h"
+
+#define RT_COMM_MAX_RANKS 64
+
+struct rt_comm {
+    ncclComm_t nccl = nullptr;
+    int n_ranks = 1, rank = 0, device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    float *stage = nullptr; /* root: the other ranks' tiles, rank order */
+    size_t stage_bytes = 0;
+    float *tile = nullptr; /* rt_comm_render: this rank's compact tile (persists: progression mixes into it) */
+    size_t tile_bytes = 0;
+    uint32_t *halo_send = nullptr, *halo_recv = nullptr;
+    size_t halo_send_bytes = 0, halo_recv_bytes = 0;
+    /* seed-row halo state: last writer of every seed row, valid for this frame shape */
+    std::vector<int32_t> writer;
+    uint32_t key_w = 0, key_h = 0, key_stripe = 0, hpad = 0, wpad = 0;
+    const rt_ctx *key_ctx = nullptr;
+};
+
+namespace {
+
+int fail(rt_comm *m, int code, const std::string &what)
+{
+    if (m) m->err = what;
+    return code;
+}
+
+int hip_fail(rt_comm *m, hipError_t e, const char *what)
+{
+    return fail(m, RT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int nccl_fail(rt_comm *m, ncclResult_t r, const char *what)
+{
+    return fail(m, RT_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+#define HIPC(m, call)                                                 \
+    do {                                                              \
+        hipError_t e_ = (call);                                       \
+        if (e_ != hipSuccess) return hip_fail((m), e_, #call);        \
+    } while (0)
+#define NCCLC(m, call)                                                \
+    do {                                                              \
+        ncclResult_t r_ = (call);                                     \
+        if (r_ != ncclSuccess) return nccl_fail((m), r_, #call);      \
+    } while (0)
+
+template <class T>
+int grow(rt_comm *m, T **p, size_t *cap_bytes, size_t bytes)
+{
+    if (*cap_bytes >= bytes) return RT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap_bytes = 0;
+    HIPC(m, hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(bytes, 256)));
+    *cap_bytes = bytes;
+    return RT_OK;
+}
+
+/* Owner of global row y and its position in that owner's compact tile (rt_tile). */
+__host__ __device__ inline uint32_t row_rank(uint32_t y, uint32_t stripe, uint32_t n) { return (y / stripe) % n; }
+__host__ __device__ inline uint32_t row_local(uint32_t y, uint32_t stripe, uint32_t n)
+{
+    return (y / (stripe * n)) * stripe + y % stripe;
+}
+
+struct TilePtrs {
+    const float4 *p[RT_COMM_MAX_RANKS];
+};
+
+/* One thread per output pixel: gather the pixel from its owner's compact tile.  Reads
+   and writes are row-contiguous float4 (16 B per lane, coalesced). */
+__global__ void __launch_bounds__(256) k_assemble(TilePtrs tiles, uint32_t n, uint32_t W, uint32_t H, uint32_t stripe,
+                                                  float4 *frame)
+{
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t y = blockIdx.y;
+    if (x >= W || y >= H) return;
+    const uint32_t r = row_rank(y, stripe, n);
+    frame[(size_t)y * W + x] = tiles.p[r][(size_t)row_local(y, stripe, n) * W + x];
+}
+
+int assemble(rt_comm *m, const float *const *tiles, uint32_t n, uint32_t W, uint32_t H, uint32_t stripe, float *frame,
+             hipStream_t st)
+{
+    TilePtrs tp{};
+    for (uint32_t r = 0; r < n; ++r) tp.p[r] = reinterpret_cast<const float4 *>(tiles[r]);
+    dim3 grid((W + 255) / 256, H);
+    hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, st, tp, n, W, H, stripe, reinterpret_cast<float4 *>(frame));
+    HIPC(m, hipGetLastError());
+    return RT_OK;
+}
+
+uint32_t tile_rows(uint32_t H, uint32_t stripe, uint32_t n, uint32_t r)
+{
+    const rt_tile t{stripe, n, r};
+    return rt_tile_rows(H, &t);
+}
+
+} // namespace
+
+extern "C" {
+
+int rt_comm_get_unique_id(uint8_t id[RT_COMM_ID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RT_COMM_ID_BYTES != NCCL_UNIQUE_ID_BYTES");
+    if (!id) return RT_ERR_ARG;
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return RT_ERR_HIP;
+    std::memcpy(id, &u, sizeof(u));
+    return RT_OK;
+}
+
+int rt_comm_create(const uint8_t id[RT_COMM_ID_BYTES], int n_ranks, int rank, int device, rt_comm **out)
+{
+    if (!out) return RT_ERR_ARG;
+    *out = nullptr;
+    if (!id || n_ranks < 1 || n_ranks > RT_COMM_MAX_RANKS || rank < 0 || rank >= n_ranks) return RT_ERR_ARG;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return RT_ERR_HIP;
+    if (device < 0 || device >= nd) return RT_ERR_ARG;
+    rt_comm *m = new (std::nothrow) rt_comm();
+    if (!m) return RT_ERR_ALLOC;
+    m->n_ranks = n_ranks;
+    m->rank = rank;
+    m->device = device;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess ||
+        ncclCommInitRank(&m->nccl, n_ranks, u, rank) != ncclSuccess) {
+        rt_comm_destroy(m);
+        return RT_ERR_HIP;
+    }
+    *out = m;
+    return RT_OK;
+}
+
+int rt_comm_destroy(rt_comm *m)
+{
+    if (!m) return RT_ERR_ARG;
+    (void)hipSetDevice(m->device);
+    if (m->stream) (void)hipStreamSynchronize(m->stream);
+    if (m->nccl) (void)ncclCommDestroy(m->nccl);
+    for (void *p : {(void *)m->stage, (void *)m->tile, (void *)m->halo_send, (void *)m->halo_recv})
+        if (p) (void)hipFree(p);
+    if (m->stream) (void)hipStreamDestroy(m->stream);
+    delete m;
+    return RT_OK;
+}
+
+const char *rt_comm_last_error(const rt_comm *m) { return m ? m->err.c_str() : "null communicator"; }
+
+int rt_assemble_tiles(const float *const *tiles, uint32_t n, uint32_t W, uint32_t H, uint32_t stripe, float *frame,
+                      int device)
+{
+    if (!tiles || !frame || n < 1 || n > RT_COMM_MAX_RANKS || stripe == 0) return RT_ERR_ARG;
+    for (uint32_t r = 0; r < n; ++r)
+        if (!tiles[r] && tile_rows(H, stripe, n, r) > 0) return RT_ERR_ARG;
+    if (W == 0 || H == 0) return RT_OK;
+    if (hipSetDevice(device) != hipSuccess) return RT_ERR_HIP;
+    rt_comm tmp;
+    if (assemble(&tmp, tiles, n, W, H, stripe, frame, nullptr) != RT_OK) return RT_ERR_HIP;
+    return hipStreamSynchronize(nullptr) == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
+int rt_comm_gather_frame(rt_comm *m, const float *tile, float *frame, uint32_t W, uint32_t H, uint32_t stripe,
+                         int root)
+{
+    if (!m) return RT_ERR_ARG;
+    const uint32_t n = (uint32_t)m->n_ranks, me = (uint32_t)m->rank;
+    if (stripe == 0 || root < 0 || root >= m->n_ranks) return fail(m, RT_ERR_ARG, "bad stripe or root");
+    if (W == 0 || H == 0) return RT_OK;
+    const size_t row_floats = (size_t)W * 4;
+    const uint32_t mine = tile_rows(H, stripe, n, me);
+    if (mine && !tile) return fail(m, RT_ERR_ARG, "null tile");
+    if (me == (uint32_t)root && !frame) return fail(m, RT_ERR_ARG, "null frame on root");
+    HIPC(m, hipSetDevice(m->device));
+    std::vector<const float *> ptrs(n, nullptr);
+    if (me == (uint32_t)root) {
+        size_t total = 0;
+        for (uint32_t r = 0; r < n; ++r)
+            if (r != me) total += tile_rows(H, stripe, n, r) * row_floats;
+        if (int e = grow(m, &m->stage, &m->stage_bytes, total * sizeof(float))) return e;
+        size_t off = 0;
+        NCCLC(m, ncclGroupStart());
+        for (uint32_t r = 0; r < n; ++r) {
+            const size_t cnt = tile_rows(H, stripe, n, r) * row_floats;
+            if (r == me) {
+                ptrs[r] = tile;
+                continue;
+            }
+            ptrs[r] = m->stage + off;
+            if (cnt) NCCLC(m, ncclRecv(m->stage + off, cnt, ncclFloat32, (int)r, m->nccl, m->stream));
+            off += cnt;
+        }
+        NCCLC(m, ncclGroupEnd());
+        if (int e = assemble(m, ptrs.data(), n, W, H, stripe, frame, m->stream)) return e;
+    } else if (mine) {
+        NCCLC(m, ncclSend(tile, mine * row_floats, ncclFloat32, root, m->nccl, m->stream));
+    }
+    HIPC(m, hipStreamSynchronize(m->stream));
+    return RT_OK;
+}
+
+int rt_seed_halo_plan(int32_t *writer, uint32_t H, uint32_t hpad, uint32_t stripe, uint32_t n, uint32_t shift,
+                      uint32_t *src, uint32_t *dst, uint32_t *rows, uint32_t *n_moves)
+{
+    if (!writer || !n_moves || stripe == 0 || n == 0 || hpad < H) return RT_ERR_ARG;
+    /* moves grouped by (src, dst) pair in pair order, rows in pixel-row order within a
+       pair (the order dist.SeedHalo.plan produces) */
+    std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> moves;
+    for (uint32_t y = 0; y < H; ++y) {
+        const uint32_t r = (uint32_t)(((uint64_t)y + shift) % hpad);
+        const int32_t w = writer[r];
+        const uint32_t d = row_rank(y, stripe, n);
+        if (w >= 0 && (uint32_t)w != d) moves[{(uint32_t)w, d}].push_back(r);
+    }
+    uint32_t k = 0;
+    for (auto &kv : moves)
+        for (uint32_t r : kv.second) {
+            if (!src || !dst || !rows) return RT_ERR_ARG;
+            src[k] = kv.first.first;
+            dst[k] = kv.first.second;
+            rows[k] = r;
+            ++k;
+        }
+    *n_moves = k;
+    for (uint32_t y = 0; y < H; ++y) writer[((uint64_t)y + shift) % hpad] = (int32_t)row_rank(y, stripe, n);
+    return RT_OK;
+}
+
+int rt_comm_reset_halo(rt_comm *m)
+{
+    if (!m) return RT_ERR_ARG;
+    m->writer.clear();
+    m->key_ctx = nullptr;
+    return RT_OK;
+}
+
+int rt_comm_render(rt_comm *m, rt_ctx *c, float *frame, uint32_t W, uint32_t H, uint32_t prog, int kernel,
+                   uint32_t stripe, int root)
+{
+    if (!m || !c) return RT_ERR_ARG;
+    if (stripe == 0 || root < 0 || root >= m->n_ranks) return fail(m, RT_ERR_ARG, "bad stripe or root");
+    if (W == 0 || H == 0) return RT_OK;
+    const uint32_t n = (uint32_t)m->n_ranks, me = (uint32_t)m->rank;
+    const rt_tile tile{stripe, n, me};
+    const uint32_t mine = rt_tile_rows(H, &tile);
+    HIPC(m, hipSetDevice(m->device));
+    if (int e = grow(m, &m->tile, &m->tile_bytes, (size_t)std::max(mine, 1u) * W * 4 * sizeof(float))) return e;
+
+    /* halo state belongs to one frame shape on one context: a new shape regenerates the
+       seeds identically on every rank (rt_render), so nothing is stale */
+    const bool fresh = m->writer.empty() || m->key_ctx != c || m->key_w != W || m->key_h != H ||
+                       m->key_stripe != stripe;
+    int flags = RT_OUT_DEVICE;
+    if (kernel == RT_KERNEL_SPHERES && n > 1) {
+        flags |= RT_SEEDS_HALO;
+        if (!fresh) {
+            std::vector<uint32_t> src(H), dst(H), rows(H);
+            std::vector<int32_t> w = m->writer; /* committed after the render */
+            uint32_t k = 0;
+            if (rt_seed_halo_plan(w.data(), H, m->hpad, stripe, n, prog, src.data(), dst.data(), rows.data(), &k))
+                return fail(m, RT_ERR_STATE, "halo plan");
+            /* my sends and receives, one contiguous packed block per peer */
+            std::vector<std::vector<uint32_t>> to(n), from(n);
+            for (uint32_t i = 0; i < k; ++i) {
+                if (src[i] == me) to[dst[i]].push_back(rows[i]);
+                if (dst[i] == me) from[src[i]].push_back(rows[i]);
+            }
+            size_t ns = 0, nr = 0;
+            for (uint32_t p = 0; p < n; ++p) {
+                ns += to[p].size();
+                nr += from[p].size();
+            }
+            const size_t row_words = 2ull * m->wpad;
+            if (ns + nr) {
+                if (int e = grow(m, &m->halo_send, &m->halo_send_bytes, ns * row_words * 4)) return e;
+                if (int e = grow(m, &m->halo_recv, &m->halo_recv_bytes, nr * row_words * 4)) return e;
+                size_t off = 0;
+                for (uint32_t p = 0; p < n; ++p)
+                    if (!to[p].empty()) {
+                        const int e = rt_pack_seed_rows(c, to[p].data(), (uint32_t)to[p].size(), m->halo_send + off,
+                                                        RT_OUT_DEVICE);
+                        if (e) return fail(m, e, std::string("rt_pack_seed_rows: ") + rt_last_error(c));
+                        off += to[p].size() * row_words;
+                    }
+                NCCLC(m, ncclGroupStart());
+                size_t so = 0, ro = 0;
+                for (uint32_t p = 0; p < n; ++p) {
+                    if (!to[p].empty()) {
+                        NCCLC(m, ncclSend(m->halo_send + so, to[p].size() * row_words, ncclUint32, (int)p, m->nccl,
+                                          m->stream));
+                        so += to[p].size() * row_words;
+                    }
+                    if (!from[p].empty()) {
+                        NCCLC(m, ncclRecv(m->halo_recv + ro, from[p].size() * row_words, ncclUint32, (int)p, m->nccl,
+                                          m->stream));
+                        ro += from[p].size() * row_words;
+                    }
+                }
+                NCCLC(m, ncclGroupEnd());
+                HIPC(m, hipStreamSynchronize(m->stream));
+                ro = 0;
+                for (uint32_t p = 0; p < n; ++p)
+                    if (!from[p].empty()) {
+                        const int e = rt_unpack_seed_rows(c, from[p].data(), (uint32_t)from[p].size(),
+                                                          m->halo_recv + ro, RT_OUT_DEVICE);
+                        if (e) return fail(m, e, std::string("rt_unpack_seed_rows: ") + rt_last_error(c));
+                        ro += from[p].size() * row_words;
+                    }
+            }
+        }
+    }
+    const int e = rt_render(c, m->tile, W, H, prog, kernel, &tile, flags);
+    if (e) return fail(m, e, std::string("rt_render: ") + rt_last_error(c));
+    if (fresh) {
+        if (rt_seed_layout(c, &m->wpad, &m->hpad) != RT_OK) return fail(m, RT_ERR_STATE, "no seed layout");
+        m->writer.assign(m->hpad, -1);
+        m->key_ctx = c;
+        m->key_w = W;
+        m->key_h = H;
+        m->key_stripe = stripe;
+    }
+    /* record this frame's seed writes: raytrace writes row (y + prog) % Hpad, the other
+       kernels row y (raytracer.cl:20-30, :142-144, :207-209) */
+    const uint32_t shift = kernel == RT_KERNEL_SPHERES ? prog : 0u;
+    for (uint32_t y = 0; y < H; ++y) m->writer[((uint64_t)y + shift) % m->hpad] = (int32_t)row_rank(y, stripe, n);
+    return rt_comm_gather_frame(m, m->tile, frame, W, H, stripe, root);
+}
+
+} /* extern "C" */

@@ -16,6 +16,10 @@ The sphere kernel (raytrace) is the exception: pixel row y reads and writes seed
 frames one seed row per stripe boundary migrates to the neighbouring rank.  `SeedHalo`
 plans those moves (it tracks the last writer of every seed row) and `exchange_seed_rows`
 performs them with point-to-point sends (RCCL over xGMI, 2 * Wpad * 4 B per row).
+
+`NativeComm` drives the same protocol inside librtmi (csrc/rt_comm.hip: its own RCCL
+communicator, grouped ncclSend/ncclRecv, device-side assembly): the path a C++ host
+without Python uses; torch.distributed only carries its 128-byte id to every rank.
 """
 from __future__ import annotations
 
@@ -152,3 +156,107 @@ def exchange_seed_rows(plan: dict, pack, unpack, n_words_per_row: int, device=No
     for rows, buf in recvs:
         unpack(rows, buf)
     return sum(len(r) for r, _ in recvs)
+
+
+def seed_halo_plan_native(writer: np.ndarray, height: int, hpad: int, stripe: int, n_ranks: int, shift: int):
+    """rt_seed_halo_plan (librtmi, host only): the moves of SeedHalo.plan(shift) as
+    (src, dst, row) arrays, then SeedHalo.commit(shift) applied to `writer` in place."""
+    from . import _abi
+
+    lib = _abi.load()
+    w = np.ascontiguousarray(writer, np.int32)
+    src = np.empty(height, np.uint32)
+    dst = np.empty(height, np.uint32)
+    rows = np.empty(height, np.uint32)
+    k = _abi.ctypes.c_uint32(0)
+    st = lib.rt_seed_halo_plan(_abi.ptr(w), height, hpad, stripe, n_ranks, shift, _abi.ptr(src), _abi.ptr(dst),
+                               _abi.ptr(rows), _abi.ctypes.byref(k))
+    if st != _abi.RT_OK:
+        raise _abi.RtError(st, "rt_seed_halo_plan")
+    writer[...] = w
+    n = k.value
+    return src[:n], dst[:n], rows[:n]
+
+
+class NativeComm:
+    """librtmi's RCCL communicator (rt_comm_*; one per rank and GPU).
+
+    `uid` (RT_COMM_ID_BYTES bytes) comes from `NativeComm.unique_id()` on rank 0 and is
+    handed to every rank by any channel; `from_torch` uses torch.distributed for that."""
+
+    def __init__(self, n_ranks: int, rank: int, device: int, uid: bytes):
+        from . import _abi
+
+        self._abi = _abi
+        self._lib = _abi.load()
+        if len(uid) != _abi.RT_COMM_ID_BYTES:
+            raise ValueError("bad communicator id")
+        self._uid = (_abi.ctypes.c_uint8 * _abi.RT_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = _abi.ctypes.c_void_p()
+        st = self._lib.rt_comm_create(_abi.ctypes.addressof(self._uid), n_ranks, rank, device, _abi.ctypes.byref(h))
+        if st != _abi.RT_OK:
+            raise _abi.RtError(st, "rt_comm_create")
+        self._h = h
+        self.n_ranks, self.rank, self.device = n_ranks, rank, device
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from . import _abi
+
+        buf = (_abi.ctypes.c_uint8 * _abi.RT_COMM_ID_BYTES)()
+        st = _abi.load().rt_comm_get_unique_id(_abi.ctypes.addressof(buf))
+        if st != _abi.RT_OK:
+            raise _abi.RtError(st, "rt_comm_get_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def from_torch(cls, device: int, group=None):
+        """Collective over a torch.distributed group: rank 0 makes the id, a broadcast carries it."""
+        import torch.distributed as dist
+
+        obj = [cls.unique_id() if dist.get_rank(group) == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls(dist.get_world_size(group), dist.get_rank(group), device, obj[0])
+
+    def _check(self, st: int, what: str):
+        if st != self._abi.RT_OK:
+            raise self._abi.RtError(st, f"{what}: {self._lib.rt_comm_last_error(self._h).decode()}")
+
+    def gather(self, tile, frame, width: int, height: int, stripe: int = 8, root: int = 0) -> None:
+        """rt_comm_gather_frame: device tile (this rank's rows) -> device frame on root."""
+        p = self._abi.ptr
+        self._check(self._lib.rt_comm_gather_frame(self._h, p(tile), p(frame), width, height, stripe, root),
+                    "rt_comm_gather_frame")
+
+    def render(self, rt, frame, width: int, height: int, progression: int, kernel: int, stripe: int = 8,
+               root: int = 0) -> None:
+        """rt_comm_render: this rank's stripes (+ the seed-row halo for raytrace) -> frame on root."""
+        rt._sync_scene()
+        self._check(self._lib.rt_comm_render(self._h, rt._h, self._abi.ptr(frame), width, height, progression, kernel,
+                                             stripe, root), "rt_comm_render")
+
+    def reset_halo(self) -> None:
+        self._check(self._lib.rt_comm_reset_halo(self._h), "rt_comm_reset_halo")
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.rt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def assemble_native(tiles, height: int, width: int, stripe: int, frame, device: int = 0) -> None:
+    """rt_assemble_tiles: the root's device-side scatter of compact tiles (device tensors,
+    rank order) into `frame` (device, H*W*4 floats)."""
+    from . import _abi
+
+    arr = (_abi.ctypes.c_void_p * len(tiles))(*[t.data_ptr() for t in tiles])
+    st = _abi.load().rt_assemble_tiles(_abi.ctypes.addressof(arr), len(tiles), width, height, stripe,
+                                       _abi.ptr(frame), device)
+    if st != _abi.RT_OK:
+        raise _abi.RtError(st, "rt_assemble_tiles")

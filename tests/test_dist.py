@@ -180,3 +180,25 @@ def test_gather_frames_gloo(tmp_path):
     assert got.shape == (3, 120)
     for r in range(3):
         assert np.all(got[r] == r + 0.5)
+
+
+@pytest.mark.parametrize("H,hpad,stripe,n", [(53, 56, 8, 2), (45, 48, 4, 3), (64, 64, 8, 8), (30, 32, 16, 4)])
+def test_native_halo_plan_equals_python(pt, H, hpad, stripe, n):
+    """rt_seed_halo_plan (the native host's halo planner, csrc/rt_comm.hip) makes the same
+    moves as dist.SeedHalo over a progression with restarts, and commits the same writers."""
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    halo = dist.SeedHalo(H, hpad, stripe, n)
+    writer = np.full(hpad, -1, np.int32)
+    total = 0
+    for s in [0, 1, 2, 3, 7, 0, 1, 5, hpad - 1, hpad + 3, 2]:
+        plan = halo.plan(s)
+        src, dst, rows = dist.seed_halo_plan_native(writer, H, hpad, stripe, n, s)
+        exp = [(a, b, int(r)) for (a, b), rr in plan.items() for r in rr]
+        got = list(zip(src.tolist(), dst.tolist(), rows.tolist()))
+        assert got == exp, f"shift {s}"
+        total += len(got)
+        halo.commit(s)
+        np.testing.assert_array_equal(writer, halo.writer)
+    assert total > 0

@@ -406,6 +406,72 @@ def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt,
             rk.close()
 
 
+def test_native_comm_assembly_and_single_rank_render(tracer, pt):
+    """The native host's sharding path (csrc/rt_comm.hip).  rt_assemble_tiles (the root's
+    device-side scatter) rebuilds the full frame from 3 ranks' compact tiles; a 1-rank RCCL
+    communicator's rt_comm_render equals rt_render over progressive frames of raytrace_tris
+    and raytrace (halo bookkeeping on), and rt_comm_gather_frame moves the tile unchanged.
+    (RCCL refuses two ranks on one GPU: the multi-rank exchange runs on the 8-GPU node.)"""
+    import torch
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    sc = pt.scenes
+    W, H, stripe = 72, 53, 8
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(5000)
+    seeds = sc.default_seeds(Wp, Hp)
+
+    def make(kernel):
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene() if kernel == 2 else sc.main_scene())
+        rt.setCamera(sc.camera_spherical(W, **(sc.PLY_CAMERA if kernel == 2 else sc.MAIN_CAMERA)))
+        rt.setSampleRate(1)
+        rt.setMaxPathDepth(6)
+        if kernel == 2:
+            rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        return rt
+
+    dev = "cuda:0"
+    rt = make(2)
+    full = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    rt.rayTrace(full, W, H, 0, kernel=2)
+    rt.close()
+    n = 3
+    tiles = []
+    for r in range(n):
+        rows = dist.tile_rows(H, stripe, n, r)
+        t = torch.zeros(len(rows) * W * 4, dtype=torch.float32, device=dev)
+        rk = make(2)
+        rk.rayTrace(t, W, H, 0, kernel=2, tile=(stripe, n, r))
+        rk.close()
+        tiles.append(t)
+    frame = torch.full((W * H * 4,), -1.0, dtype=torch.float32, device=dev)
+    dist.assemble_native(tiles, H, W, stripe, frame)
+    torch.testing.assert_close(frame, full, rtol=0, atol=0)
+
+    comm = dist.NativeComm(1, 0, 0, dist.NativeComm.unique_id())
+    try:
+        for kernel in (2, 0):
+            ref, rk = make(kernel), make(kernel)
+            exp = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+            got = torch.zeros_like(exp)
+            for p in [0, 1, 2, 0, 1]:
+                ref.rayTrace(exp, W, H, p, kernel=kernel)
+                comm.render(rk, got, W, H, p, kernel, stripe=stripe)
+                assert torch.equal(got.view(torch.int32), exp.view(torch.int32)), (kernel, p)
+            np.testing.assert_array_equal(rk.getSeeds(), ref.getSeeds())
+            ref.close()
+            rk.close()
+            comm.reset_halo()
+        moved = torch.zeros_like(full)
+        comm.gather(full, moved, W, H, stripe)
+        assert torch.equal(moved, full)
+    finally:
+        comm.close()
+
+
 def test_device_framebuffer_matches_host(tracer, pt):
     import torch
 

@@ -92,6 +92,7 @@ typedef struct rt_counters {
                                   traversal because the answer cannot change the pixel:
                                   tmax <= tmin, or cos(wi) <= 0 (rtcommon.h:93-95) */
     uint64_t clocks_shade;     /* shader clocks waves spent advancing paths (counting launches) */
+    uint64_t pixels_deferred;  /* box pixels whose shadow rays were deferred (k_defer_shadow) */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */

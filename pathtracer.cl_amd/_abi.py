@@ -105,6 +105,7 @@ class RtCounters(ctypes.Structure):
         ("pixel_steps_max", ctypes.c_uint64),
         ("rays_skipped", ctypes.c_uint64),
         ("clocks_shade", ctypes.c_uint64),
+        ("pixels_deferred", ctypes.c_uint64),
     ]
 
 

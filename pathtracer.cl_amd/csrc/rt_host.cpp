@@ -86,6 +86,18 @@ struct rt_ctx {
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
     uint32_t *d_flags = nullptr; /* cost probe per pixel (k_probe_cost) */
+    /* deferred shadow rays of box pixels (k_tris -> k_defer_shadow -> k_defer_finish) */
+    int32_t *d_class = nullptr;  /* per pixel: -1 mesh, -2 box, >= 0 box with a defer slot */
+    size_t class_bytes = 0;
+    uint32_t *d_defer_pixel = nullptr; /* per slot: yl * W + x */
+    float *d_defer_rec = nullptr;
+    uint8_t *d_defer_seg = nullptr, *d_defer_vis = nullptr;
+    uint32_t *d_defer_queue = nullptr, *d_defer_qcount = nullptr;
+    size_t defer_rec_cap = 0, defer_seg_cap = 0, defer_slot_cap = 0; /* allocated entries */
+    uint32_t n_defer = 0;
+    int defer = -1;          /* RT_DEFER: 1 on, 0 off, unset = auto (on when the launch has fewer than
+                                4 pixels per resident lane: tiles of a multi-GPU frame) */
+    size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer buffers */
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
     size_t halo_rows_cap = 0, halo_buf_cap = 0;
@@ -131,6 +143,7 @@ struct rt_ctx {
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
     rt_counters last = {};
+    uint32_t last_deferred = 0; /* deferred box pixels of the last triangle launch */
     bool have_timing = false;
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
@@ -342,11 +355,93 @@ int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
    pixels of 50 steps per query, handed out late as "cheap").  Scheduling only:
    every pixel's result is independent of when it is rendered.  Cached until
    camera, mesh, frame, tile or path depth change. */
+/* Pixel classes for the triangle kernel, from the probe words: a pixel some of whose probe
+   rays missed the mesh is a box pixel (its samples bounce off the box up to maxDepth + 1
+   times: the long serial chains).  Box pixels get a slot in the deferred-shadow buffers
+   (DESIGN.md §5): per slot, one 32-B record per (sample, segment, light), a segment-kind
+   byte per (sample, segment), a visibility byte and a queue entry per record.  Slots are
+   dealt in pixel order up to RT_DEFER_MB of device memory; further box pixels trace their
+   shadow rays inline (class -2). */
+int classify_pixels(rt_ctx *c, const std::vector<uint32_t> &f, uint32_t W, uint32_t hl, uint64_t lanes,
+                    hipStream_t st)
+{
+    const size_t npx = (size_t)W * hl;
+    /* Deferral shortens the box chains but moves their shadow queries into a second launch
+       that cannot use the tail of the first: it pays where the chains set the frame time (a
+       tile with few pixels per lane), not on a full frame (dragon 1920x1080: 161.7 ->
+       173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) */
+    const bool use = c->defer == 1 || (c->defer < 0 && npx < 4 * lanes);
+    const uint32_t pn2 = c->probe_n * c->probe_n;
+    const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
+    const uint64_t nl = c->lights.size();
+    const uint64_t recs = spp * nd * nl; /* records per slot */
+    uint64_t max_slots = 0;
+    if (use && nl > 0 && spp > 0 && spp <= 1024 && recs > 0) {
+        const uint64_t bytes_per_slot = recs * (32 + 1 + 4) + spp * nd + 4;
+        max_slots = ((uint64_t)c->defer_mb << 20) / bytes_per_slot;
+        max_slots = std::min<uint64_t>(max_slots, 0xffffffffull / recs);
+    }
+    std::vector<int32_t> cls(npx);
+    std::vector<uint32_t> px;
+    for (size_t p = 0; p < npx; ++p) {
+        const bool box = (f[p] >> RT_PROBE_HIT_SHIFT) < pn2;
+        if (!box) cls[p] = -1;
+        else if (px.size() < max_slots) {
+            cls[p] = (int32_t)px.size();
+            px.push_back((uint32_t)p);
+        } else cls[p] = -2;
+    }
+    if (c->class_bytes < npx * 4) {
+        free_dev(c->d_class);
+        c->d_class = nullptr;
+        c->class_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_class, npx * 4));
+        c->class_bytes = npx * 4;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_class, cls.data(), npx * 4, hipMemcpyHostToDevice, st));
+    const uint64_t n = px.size();
+    if (n) {
+        if (c->defer_slot_cap < n) {
+            free_dev(c->d_defer_pixel);
+            c->d_defer_pixel = nullptr;
+            c->defer_slot_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_defer_pixel, n * 4));
+            c->defer_slot_cap = n;
+        }
+        if (c->defer_rec_cap < n * recs) {
+            free_dev(c->d_defer_rec);
+            free_dev(c->d_defer_vis);
+            free_dev(c->d_defer_queue);
+            c->d_defer_rec = nullptr;
+            c->d_defer_vis = nullptr;
+            c->d_defer_queue = nullptr;
+            c->defer_rec_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_defer_rec, n * recs * 32));
+            HIPCHK(c, hipMalloc(&c->d_defer_vis, n * recs));
+            HIPCHK(c, hipMalloc(&c->d_defer_queue, n * recs * 4));
+            c->defer_rec_cap = n * recs;
+        }
+        if (c->defer_seg_cap < n * spp * nd) {
+            free_dev(c->d_defer_seg);
+            c->d_defer_seg = nullptr;
+            c->defer_seg_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_defer_seg, n * spp * nd));
+            c->defer_seg_cap = n * spp * nd;
+        }
+        if (!c->d_defer_qcount) HIPCHK(c, hipMalloc(&c->d_defer_qcount, 2 * sizeof(uint32_t)));
+        HIPCHK(c, hipMemcpyAsync(c->d_defer_pixel, px.data(), n * 4, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->n_defer = (uint32_t)n;
+    return RT_OK;
+}
+
 int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
 {
     const uint32_t W = a.W, hl = a.Hl;
     std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
-                                 (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks};
+                                 (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks,
+                                 c->sample_rate, (uint32_t)(c->defer + 1)};
     const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
     const uint32_t tx = (W + 7) / 8, ty = (hl + 7) / 8, n_t = tx * ty;
@@ -356,6 +451,7 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
            (measurement variants) keep the row-major queue */
         free_dev(c->d_order);
         c->d_order = nullptr;
+        c->n_defer = 0;
         c->order_key = key;
         return RT_OK;
     }
@@ -408,6 +504,10 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     std::vector<uint32_t> o(n_t);
     for (uint32_t i = 0; i < n_t; ++i) o[i] = i;
     std::stable_sort(o.begin(), o.end(), [&](uint32_t p, uint32_t q) { return cost[p] > cost[q]; });
+    {
+        const int r = classify_pixels(c, f, W, hl, (uint64_t)blocks * RT_BLOCK, st);
+        if (r != RT_OK) return r;
+    }
     free_dev(c->d_order);
     c->d_order = nullptr;
     HIPCHK(c, hipMalloc(&c->d_order, n_t * sizeof(uint32_t)));
@@ -456,6 +556,8 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_FETCH_K_BOX")) c->fetch_k_box = (uint32_t)std::max(1, std::min(64, atoi(v)));
     if (const char *v = getenv("RT_FETCH_FRAC")) c->fetch_frac = (uint32_t)std::max(0, std::min(64, atoi(v)));
     if (const char *v = getenv("RT_BOX_EXIT")) c->box_exit = atoi(v) != 0;
+    if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0; /* A/B knob */
+    if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
@@ -478,6 +580,13 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_spill);
     free_dev(c->d_order);
     free_dev(c->d_flags);
+    free_dev(c->d_class);
+    free_dev(c->d_defer_pixel);
+    free_dev(c->d_defer_rec);
+    free_dev(c->d_defer_seg);
+    free_dev(c->d_defer_vis);
+    free_dev(c->d_defer_queue);
+    free_dev(c->d_defer_qcount);
     free_dev(c->d_halo_rows);
     free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
@@ -837,12 +946,25 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.box_exit = c->box_exit;
         a.tile_order = nullptr;
         a.pixel_flags = nullptr;
+        a.pixel_class = nullptr;
+        a.n_defer = 0;
         if (c->schedule) {
             const int ro = tile_order(c, a, blocks, st);
             if (ro != RT_OK) return ro;
             a.tile_order = c->d_order;
             a.pixel_flags = a.tile_order ? c->d_flags : nullptr;
+            a.pixel_class = a.tile_order ? c->d_class : nullptr;
             a.probe_n = c->probe_n;
+            if (a.pixel_class && c->n_defer) {
+                a.n_defer = c->n_defer;
+                a.defer_rec = c->d_defer_rec;
+                a.defer_seg = c->d_defer_seg;
+                a.defer_vis = c->d_defer_vis;
+                a.defer_queue = c->d_defer_queue;
+                a.defer_qcount = c->d_defer_qcount;
+                a.defer_pixel = c->d_defer_pixel;
+                HIPCHK(c, hipMemsetAsync(c->d_defer_qcount, 0, 2 * sizeof(uint32_t), st));
+            }
         }
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
@@ -860,6 +982,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         }
         HIPCHK(c, hipEventRecord(c->ev0, st));
         e = rt_launch_tris(a, trav, c->counting, blocks, st);
+        if (!e && a.n_defer) e = rt_launch_defer(a, c->counting, blocks, st);
+        c->last_deferred = a.n_defer;
         HIPCHK(c, hipEventRecord(c->ev1, st));
         if (d_stats) {
             std::vector<uint32_t> h((size_t)W * hl * 8);
@@ -922,6 +1046,7 @@ int rt_synchronize(rt_ctx *c)
     c->last.pixel_clocks_max = h[10];
     c->last.pixel_rays_max = h[11];
     c->last.pixel_steps_max = h[12];
+    c->last.pixels_deferred = c->last_deferred;
     return RT_OK;
 }
 

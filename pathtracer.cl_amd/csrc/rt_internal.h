@@ -134,7 +134,22 @@ struct RtTriLaunch {
     uint32_t box_exit;          /* a box pixel's completed query ends the stepping round */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =
                                    start / finish (s_memrealtime, 100 MHz, low 32 bits), queries, steps */
+    /* Deferred shadow rays of box pixels (DESIGN.md §5 "Deferred shadow rays"): a box pixel's
+       random-number chain depends only on its closest-hit queries, so its shadow rays are
+       recorded (k_tris), traced afterwards in parallel (k_defer_shadow) and its colour is
+       replayed in the reference's operation order (k_defer_finish). */
+    const int32_t *pixel_class; /* per pixel (W x Hl): -1 mesh pixel, -2 box pixel without a slot, >= 0
+                                   box pixel with deferred-shadow slot (NULL: no probe) */
+    float *defer_rec;           /* per slot and (sample, segment, light): (o.xyz, tmax), (d.xyz, cos wi) */
+    uint8_t *defer_seg;         /* per slot and (sample, segment): RT_SEG_* */
+    uint8_t *defer_vis;         /* per record: 1 = unoccluded (k_defer_shadow) */
+    uint32_t *defer_queue;      /* record indices whose shadow ray needs a traversal */
+    uint32_t *defer_qcount;     /* [0] queue length (k_tris), [1] consumer cursor (k_defer_shadow) */
+    const uint32_t *defer_pixel; /* per slot: yl * W + x */
+    uint32_t n_defer;           /* slots in use */
 };
+/* segment kinds of a deferred pixel's path (trace_path_tri, rtcommon.h:378-468) */
+enum { RT_SEG_BOX = 0, RT_SEG_TRI = 1, RT_SEG_NONE = 2 };
 
 struct RtSphLaunch {
     float *out;
@@ -157,6 +172,9 @@ int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
                          unsigned long long *counters, void *stream); /* counters: NULL, or counting (queries, nodes, tests, leaves) */
+/* Deferred shadow rays: trace the queued records (persistent grid), then replay the deferred
+   pixels' colours and write them (one wave per slot).  Same stream as k_tris, after it. */
+int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *stream);
 /* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed

@@ -955,15 +955,17 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     """The pixel queue's order (step-counting probe, LPT key), the box-wave priority and the
     probe density are scheduling only: a frame with box and mesh pixels, 16 spp, renders to
     the same bits and seeds with the queue row-major (RT_SCHEDULE=0), with the default
-    schedule, and with other probe / key settings."""
+    schedule, with other probe / key settings, and with the box pixels' shadow rays traced
+    inline (RT_DEFER=0) or deferred for only the few box pixels 1 MB of slots holds."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
     verts, idx = sc.make_mesh(20_000)
     seeds = sc.default_seeds(Wp, Hp, skip=7)
     frames = []
-    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_PROBE_N": "1", "RT_LPT_MAX": "0"}, {"RT_PROBE_N": "3"}):
-        for k in ("RT_SCHEDULE", "RT_PROBE_N", "RT_LPT_MAX"):
+    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_PROBE_N": "1", "RT_LPT_MAX": "0"}, {"RT_PROBE_N": "3"},
+                {"RT_DEFER": "0"}, {"RT_DEFER": "1", "RT_DEFER_MB": "1"}):
+        for k in ("RT_SCHEDULE", "RT_PROBE_N", "RT_LPT_MAX", "RT_DEFER", "RT_DEFER_MB"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -982,3 +984,36 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     for f, s in frames[1:]:
         np.testing.assert_array_equal(f, frames[0][0])
         np.testing.assert_array_equal(s, frames[0][1])
+
+
+def test_deferred_shadow_rays_at_full_size(tracer, pt, monkeypatch):
+    """Deferred shadow rays (k_tris records, k_defer_shadow traces, k_defer_finish replays the
+    colour) on the dragon-class frame at full size, sampleRate 4, forced on (RT_DEFER=1: the
+    automatic policy defers only on tiles), as a whole frame and as a row-stripe tile of 8:
+    the same bits and seeds as inline shadow rays (RT_DEFER=0), which the oracle pins."""
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 4
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    seeds = sc.default_seeds(Wp, Hp, skip=2)
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RT_DEFER", mode)
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        rt.setCamera(sc.camera_spherical(W, **sc.PLY_CAMERA))
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        for tile in (None, (8, 8, 3)):
+            rows = H if tile is None else len(np.arange(H)[(np.arange(H) // 8) % 8 == 3])
+            rt.setSeeds(Wp, Hp, seeds)
+            out = np.zeros(W * rows * 4, np.float32)
+            rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
+            res[(mode, tile)] = (bits(out).copy(), rt.getSeeds().copy())
+            n_def = rt.counters()["pixels_deferred"]
+            assert (n_def > 1000) if mode == "1" else (n_def == 0)
+        rt.close()
+    for tile in (None, (8, 8, 3)):
+        np.testing.assert_array_equal(res[("1", tile)][0], res[("0", tile)][0])
+        np.testing.assert_array_equal(res[("1", tile)][1], res[("0", tile)][1])

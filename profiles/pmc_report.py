@@ -2,23 +2,16 @@
 
     python profiles/pmc_report.py gpurun_out/prof_<tag> [kernel substring]
 """
-import collections
-import csv
 import glob
 import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+from summarize_pmc import counters  # full-size dispatches only (the bench's 1-row tile launches excluded)
 
 src = sys.argv[1]
 kname = sys.argv[2] if len(sys.argv) > 2 else "k_tris<4, false>"
-tot = collections.defaultdict(list)
-for f in sorted(glob.glob(f"{src}/pmcx_*/run_counter_collection.csv")):
-    per = collections.defaultdict(lambda: collections.defaultdict(float))
-    for r in csv.DictReader(open(f)):
-        if kname in r["Kernel_Name"]:
-            per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-    for d in per.values():
-        for k, v in d.items():
-            tot[k].append(v)
-c = {k: sum(v) / len(v) for k, v in tot.items()}
+c = counters(sorted(glob.glob(f"{src}/pmcx_*/run_counter_collection.csv")), kname)
 for k in sorted(c):
     print(f"{k:40s} {c[k]:.4g}")
 cyc = c.get("GRBM_GUI_ACTIVE", 0) / 8

@@ -30,17 +30,32 @@ N_CU, N_SIMD, N_XCD = 256, 1024, 8
 
 
 def counters(paths, kernel):
-    """mean over dispatches of the kernel, per counter, over the given collection files"""
+    """mean over the kernel's full-size dispatches (the largest grid: bench.py also launches the
+    kernel on 1-row tiles for its critical-path figure), per counter, over the collection files"""
     tot = defaultdict(list)
     for path in paths:
         per = defaultdict(lambda: defaultdict(float))
+        grid = {}
         for r in csv.DictReader(open(path)):
             if kernel in r["Kernel_Name"]:
                 per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-        for d in per.values():
+                grid[r["Dispatch_Id"]] = int(r["Grid_Size"])
+        gmax = max(grid.values()) if grid else 0
+        for did, d in per.items():
+            if grid[did] != gmax:
+                continue
             for k, v in d.items():
                 tot[k].append(v)
     return {k: sum(v) / len(v) for k, v in tot.items()}
+
+
+def kernel_ns(src, kernel):
+    """mean duration and count of the kernel's full-size dispatches in the kernel trace"""
+    rows = [r for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")) if kernel in r["Kernel_Name"]]
+    size = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+    gmax = max(size(r) for r in rows)
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if size(r) == gmax]
+    return sum(d) / len(d), len(d)
 
 
 def main():
@@ -51,9 +66,7 @@ def main():
     files = sorted(glob.glob(f"{src}/pmc_*/run_counter_collection.csv")) + sorted(
         glob.glob(f"{src}/pmcx_*/run_counter_collection.csv"))
     c = counters(files, kernel)
-    stats = list(csv.DictReader(open(src / "trace" / "run_kernel_stats.csv")))
-    k = next(r for r in stats if kernel in r["Name"])
-    avg_ns = float(k["AverageNs"])
+    avg_ns, n_disp = kernel_ns(src, kernel)
     cyc = c["GRBM_GUI_ACTIVE"] / N_XCD if c.get("GRBM_GUI_ACTIVE") else None
     fetch_b = 2 * c["FETCH_SIZE"] * 1024 if c.get("FETCH_SIZE") else None
     write_b = c["WRITE_SIZE"] * 1024 if c.get("WRITE_SIZE") else None
@@ -64,7 +77,7 @@ def main():
     summ = {
         "kernel": kernel,
         "avg_kernel_ms_rocprof": avg_ns / 1e6,
-        "dispatches": int(k.get("Calls", 0) or 0),
+        "dispatches": n_disp,
         "fetch_size_kb": c.get("FETCH_SIZE"),
         "write_size_kb": c.get("WRITE_SIZE"),
         "hbm_read_bytes_corrected": fetch_b,

@@ -539,7 +539,7 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         whose query ended early go back to work instead of idling until the
         wave's longest query ends.  LINEAR: each query runs to completion inside
         the iteration (the reference loop, wave-uniform). */
-template <int TRAV, bool COUNT>
+template <int TRAV, bool COUNT, bool DEFER>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
     constexpr bool RESUME = TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
@@ -648,7 +648,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         sample_done = true; /* path terminates (rtcommon.h:463-466) */
                     }
                 }
-                if (pclass >= 0) /* deferred pixel: the segment's kind, for the colour replay */
+                if (DEFER && pclass >= 0) /* deferred pixel: the segment's kind, for the colour replay */
                     a.defer_seg[((size_t)pclass * spp + sample) * (a.max_depth + 1u) + depth] =
                         (uint8_t)(surface ? (tri_hit ? RT_SEG_TRI : RT_SEG_BOX) : RT_SEG_NONE);
                 if (surface) { /* sample_direct_illumination_tri, rtcommon.h:78-105 */
@@ -743,7 +743,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 ++sample;
                 mode = M_NEWSAMPLE;
                 if (sample >= spp) { /* raytracer.cl:234-242 */
-                    if (pclass < 0) { /* a deferred pixel's colour is written by k_defer_finish */
+                    if (!DEFER || pclass < 0) { /* a deferred pixel's colour is written by k_defer_finish */
                         const float n = (float)spp;
                         float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
                         float4 *dst = out + ((size_t)yl * a.W + x);
@@ -792,18 +792,18 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         /* a deferred pixel's shadow ray is recorded (and queued for k_defer_shadow when it
            needs a traversal) and its path moves on at once: the ray's answer only enters the
            colour, which k_defer_finish replays; the random-number chain never depends on it */
-        const bool redo = issued && (pclass >= 0 || !need_trav);
+        const bool redo = issued && ((DEFER && pclass >= 0) || !need_trav);
         if (!__any(redo)) break;
-        const bool queue = redo && pclass >= 0 && need_trav;
+        const bool queue = DEFER && redo && pclass >= 0 && need_trav;
         uint32_t ridx = 0;
-        if (redo && pclass >= 0) {
+        if (DEFER && redo && pclass >= 0) {
             ridx = ((((uint32_t)pclass * spp + sample) * (a.max_depth + 1u) + depth) * n_lights + light);
             float4 *r = reinterpret_cast<float4 *>(a.defer_rec) + 2u * (size_t)ridx;
             r[0] = make_float4(qo.x, qo.y, qo.z, stmax);
             r[1] = make_float4(qd.x, qd.y, qd.z, cw_q);
         }
-        const unsigned long long qb = __ballot(queue);
-        if (qb) {
+        const unsigned long long qb = DEFER ? __ballot(queue) : 0ull;
+        if (DEFER && qb) {
             const int leader = __ffsll((long long)qb) - 1;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(a.defer_qcount, (uint32_t)__popcll(qb));
@@ -1459,14 +1459,16 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
 {
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)grid_blocks), block(RT_BLOCK);
-#define RT_LAUNCH_TRIS(T)                                                                                              \
+#define RT_LAUNCH_TRIS(T, D)                                                                                           \
     do {                                                                                                               \
-        if (count) hipLaunchKernelGGL((k_tris<T, true>), grid, block, 0, st, a);                                       \
-        else hipLaunchKernelGGL((k_tris<T, false>), grid, block, 0, st, a);                                            \
+        if (count) hipLaunchKernelGGL((k_tris<T, true, D>), grid, block, 0, st, a);                                    \
+        else hipLaunchKernelGGL((k_tris<T, false, D>), grid, block, 0, st, a);                                         \
     } while (0)
-    if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR);
-    else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q);
-    else RT_LAUNCH_TRIS(RT_TRAV_BVH4);
+    /* the deferred-shadow form only where it is used (its code costs a full frame 1 %) */
+    if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR, false);
+    else if (trav == RT_TRAV_BVH4Q && a.n_defer) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, true);
+    else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, false);
+    else RT_LAUNCH_TRIS(RT_TRAV_BVH4, false);
 #undef RT_LAUNCH_TRIS
     return (int)hipGetLastError();
 }
@@ -1509,11 +1511,14 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
     int per_cu = 0;
     int e;
     if (trav == RT_TRAV_LINEAR)
-        e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true>, &per_cu) : occupancy(k_tris<RT_TRAV_LINEAR, false>, &per_cu);
-    else if (trav == RT_TRAV_BVH4Q)
-        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4Q, false>, &per_cu);
+        e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true, false>, &per_cu)
+                  : occupancy(k_tris<RT_TRAV_LINEAR, false, false>, &per_cu);
+    else if (trav == RT_TRAV_BVH4Q) /* the deferred form has the same launch bounds */
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true, false>, &per_cu)
+                  : occupancy(k_tris<RT_TRAV_BVH4Q, false, false>, &per_cu);
     else
-        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4, false>, &per_cu);
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true, false>, &per_cu)
+                  : occupancy(k_tris<RT_TRAV_BVH4, false, false>, &per_cu);
     if (e) return e;
     int n_cu = 0;
     const hipError_t he = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);

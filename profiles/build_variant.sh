@@ -3,7 +3,7 @@
 # usage: bash profiles/build_variant.sh OUT.so -DNAME=VALUE ...
 set -e
 OUT=$(realpath -m $1); shift
-SRC=$(dirname $(realpath $0))/../pathtracer.cl_amd/csrc
+SRC=${SRC_DIR:-$(dirname $(realpath $0))/../pathtracer.cl_amd/csrc}
 B=$(mktemp -d)
 cd $SRC
 FL="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function -I../../include -I. $@"

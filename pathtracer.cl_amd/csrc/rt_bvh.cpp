@@ -591,6 +591,49 @@ bool rt_build_bvh(const float *verts, uint32_t n_verts, const int32_t *idx, uint
         o[9] = p2[1] - a[1];
         o[10] = p2[2] - a[2];
     }
+    /* Normal boxes of the compressed nodes (rt_quant.h, determinant cull), bottom-up: the
+       4-wide nodes are numbered breadth-first, so children follow their parents. */
+    if (!out.nodes4q.empty() && out.det_cull) {
+        struct NB {
+            double lo[3], hi[3], err;
+        };
+        std::vector<NB> nb(out.n_nodes4);
+        for (uint32_t i = out.n_nodes4; i-- > 0;) {
+            NB b = {{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}, 0.0};
+            const float *f = out.nodes4.data() + 32ull * i;
+            for (int k = 0; k < 4; ++k) {
+                int32_t c;
+                std::memcpy(&c, &f[24 + k], 4);
+                if (c == RT_EMPTY_CHILD) continue;
+                if (c >= 0) {
+                    const NB &cb = nb[(uint32_t)c];
+                    for (int a = 0; a < 3; ++a) {
+                        b.lo[a] = std::min(b.lo[a], cb.lo[a]);
+                        b.hi[a] = std::max(b.hi[a], cb.hi[a]);
+                    }
+                    b.err = std::max(b.err, cb.err);
+                    continue;
+                }
+                const int32_t enc = ~c, first = enc >> 3, cnt = (enc & 7) + 1;
+                for (int32_t j = 0; j < cnt; ++j) {
+                    const float *o = out.tris.data() + 12ull * (uint32_t)(first + j);
+                    const double e1[3] = {o[4], o[5], o[6]}, e2[3] = {o[8], o[9], o[10]};
+                    /* N = e2 x e1 (rtcommon.h:389's normal): det = d . N */
+                    const double n[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                                         e2[0] * e1[1] - e2[1] * e1[0]};
+                    for (int a = 0; a < 3; ++a) {
+                        b.lo[a] = std::min(b.lo[a], n[a]);
+                        b.hi[a] = std::max(b.hi[a], n[a]);
+                    }
+                    const double l1 = std::fabs(e1[0]) + std::fabs(e1[1]) + std::fabs(e1[2]);
+                    const double l2 = std::fabs(e2[0]) + std::fabs(e2[1]) + std::fabs(e2[2]);
+                    b.err = std::max(b.err, l1 * l2);
+                }
+            }
+            nb[i] = b;
+            rt_qnode_set_nbox(out.nodes4q.data() + (uint64_t)RT_QNODE_DWORDS * i, b.lo, b.hi, b.err);
+        }
+    }
     out.build_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (out.depth >= RT_BVH_MAX_DEPTH) {
         err = "BVH deeper than the traversal stack";

@@ -660,6 +660,7 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     }
     RtBvh b;
     if (const char *v = getenv("RT_CULL_UNHITTABLE")) b.cull_unhittable = atoi(v) != 0; /* A/B knob */
+    if (const char *v = getenv("RT_DET_CULL")) b.det_cull = atoi(v) != 0; /* A/B knob */
     if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
     c->mesh_builder = RT_BUILD_HOST;

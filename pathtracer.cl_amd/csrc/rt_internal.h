@@ -83,6 +83,7 @@ struct RtBvh {
     uint32_t stack4 = 0; /* worst-case traversal stack entries of the 4-wide tree */
     double build_seconds = 0.0;
     bool cull_unhittable = true; /* in: leave triangles no ray can hit out of the tree (rt_bvh.cpp never_hit) */
+    bool det_cull = true;        /* in: normal boxes in the compressed nodes (rt_quant.h determinant cull) */
     uint32_t n_hit = 0;          /* out: triangles in the tree (slots [0, n_hit)) */
 };
 

@@ -14,10 +14,19 @@
  *            plane = origin + q * 2^e, rounded outward (floor / ceil, checked in binary64)
  *            so the box contains the exact child box; an unused slot is the inverted
  *            box lo = 255 > hi = 0, which no ray enters
- *   d[10]    index of the first inner child (inner child of rank r = d[10] + r)
- *   d[11]    first triangle slot of the leaf children (a leaf starts after the
- *            triangles of the leaf children before it)
+ *   d[10..11] the node's normal box (determinant cull, below): the box of the reference's
+ *            unnormalised normals N = e2 x e1 over every triangle of the subtree, 8-bit
+ *            two's-complement fields q * 2^(E - 128): d[10] = lo.x | lo.y << 8 | lo.z << 16 |
+ *            E << 24, d[11] = hi.x | hi.y << 8 | hi.z << 16 (E = 255: no cull)
  *   d[12..15] the four child links written out (rt_internal.h encoding)
+ *
+ * Determinant cull.  intersects_triangle rejects |det| < 1e-4 (geometryFuncs.h:167), and
+ * det = (d x e2) . e1 = d . N exactly, so no triangle under a node can be accepted by a ray
+ * whose max over the node's normal box of |d . N| is below 1e-4 minus the float error of
+ * det (<= 8u |d|_1 max(|e1|_1 |e2|_1), which the builder keeps below 5e-7 |d|_1 for every
+ * cullable node).  The traversal then skips the node's subtree: the same hits, the same
+ * occlusion answers, fewer steps (rays that pass through the dragon-class mesh at moderate
+ * incidence cross hundreds of leaf boxes of triangles too small to accept them). 
  * (A 48-B form without d[12..15], links decoded from d[3] / d[10] / d[11], measured 4.9 %
  * slower per frame — the decode's per-child branches cost more than the fourth load — and
  * was removed)
@@ -119,10 +128,43 @@ RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
     }
     q[3] = exps | meta;
     for (int i = 0; i < 6; ++i) q[4 + i] = planes[i];
-    q[10] = (uint32_t)inner_base;
-    q[11] = (uint32_t)tri_base;
+    (void)inner_base;
+    (void)tri_base;
+    q[10] = 255u << 24 | 0x80u << 16 | 0x80u << 8 | 0x80u; /* no cull until rt_qnode_set_nbox */
+    q[11] = 0x7fu << 16 | 0x7fu << 8 | 0x7fu;
     for (int k = 0; k < 4; ++k) q[12 + k] = (uint32_t)code[k]; /* explicit links */
     return true;
+}
+
+/* Encode a node's normal box (exact bounds in double) into d[10..11]; `err` is the node's
+   max |e1|_1 |e2|_1, so 8u * err bounds det's float error per unit |d|_1.  Nodes whose error
+   bound or range the encoding cannot honour keep the no-cull box. */
+inline void rt_qnode_set_nbox(uint32_t *q, const double lo[3], const double hi[3], double err)
+{
+    if (!(8.0 * 0x1p-24 * err <= 5e-7)) return;
+    double m = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        if (!(lo[k] <= hi[k])) return;
+        m = fmax(m, fmax(fabs(lo[k]), fabs(hi[k])));
+    }
+    int e = (m > 0.0) ? (int)ceil(log2(m / 127.0)) : -120;
+    if (e < -120) e = -120; /* scales stay normal floats */
+    for (;; ++e) {
+        if (e > 126) return;
+        const double step = ldexp(1.0, e);
+        int32_t ql[3], qh[3];
+        bool ok = true;
+        for (int k = 0; k < 3; ++k) {
+            ql[k] = (int32_t)floor(lo[k] / step);
+            qh[k] = (int32_t)ceil(hi[k] / step);
+            if (ql[k] < -128 || qh[k] > 127 || ql[k] * step > lo[k] || qh[k] * step < hi[k]) ok = false;
+        }
+        if (!ok) continue;
+        q[10] = ((uint32_t)ql[0] & 0xffu) | ((uint32_t)ql[1] & 0xffu) << 8 | ((uint32_t)ql[2] & 0xffu) << 16 |
+                (uint32_t)(e + 128) << 24;
+        q[11] = ((uint32_t)qh[0] & 0xffu) | ((uint32_t)qh[1] & 0xffu) << 8 | ((uint32_t)qh[2] & 0xffu) << 16;
+        return;
+    }
 }
 
 #endif /* RT_QUANT_H */

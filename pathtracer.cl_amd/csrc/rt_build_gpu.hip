@@ -351,6 +351,54 @@ __global__ void k_tri_records(const float *__restrict__ verts, const int32_t *__
     o[11] = 0.0f;
 }
 
+/* 6c. normal boxes of the compressed nodes (rt_quant.h determinant cull), one level of the
+   4-wide tree per launch from the deepest up: a node's inner children (the next level) are
+   done, its leaf children's triangles are read from the records.  binary64, as the host
+   builder. */
+struct NBox {
+    double lo[3], hi[3], err;
+};
+__global__ void k_nbox(const float *__restrict__ nodes4, uint32_t first, uint32_t last, const float *__restrict__ tris,
+                       NBox *__restrict__ nb, uint32_t *__restrict__ q4)
+{
+    const uint32_t i = first + blockIdx.x * kB + threadIdx.x;
+    if (i >= last) return;
+    NBox b;
+    for (int a = 0; a < 3; ++a) {
+        b.lo[a] = __builtin_huge_val();
+        b.hi[a] = -__builtin_huge_val();
+    }
+    b.err = 0.0;
+    const float *f = nodes4 + 32ull * i;
+    for (int k = 0; k < 4; ++k) {
+        const int32_t c = __float_as_int(f[24 + k]);
+        if (c == RT_EMPTY_CHILD) continue;
+        if (c >= 0) {
+            const NBox &cb = nb[c];
+            for (int a = 0; a < 3; ++a) {
+                b.lo[a] = fmin(b.lo[a], cb.lo[a]);
+                b.hi[a] = fmax(b.hi[a], cb.hi[a]);
+            }
+            b.err = fmax(b.err, cb.err);
+            continue;
+        }
+        const int32_t enc = ~c, lf = enc >> 3, cnt = (enc & 7) + 1;
+        for (int32_t j = 0; j < cnt; ++j) {
+            const float *o = tris + 12ull * (uint32_t)(lf + j);
+            const double e1[3] = {o[4], o[5], o[6]}, e2[3] = {o[8], o[9], o[10]};
+            const double n[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                                 e2[0] * e1[1] - e2[1] * e1[0]};
+            for (int a = 0; a < 3; ++a) {
+                b.lo[a] = fmin(b.lo[a], n[a]);
+                b.hi[a] = fmax(b.hi[a], n[a]);
+            }
+            b.err = fmax(b.err, (fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2])) * (fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2])));
+        }
+    }
+    nb[i] = b;
+    rt_qnode_set_nbox(q4 + (uint64_t)RT_QNODE_DWORDS * i, b.lo, b.hi, b.err);
+}
+
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kB - 1) / kB); }
 
 /* RAII scratch */
@@ -374,7 +422,7 @@ struct DevBuf {
     } while (0)
 
 int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_h, uint32_t n_tris, RtGpuBvh &out,
-                     std::string &err, void *stream)
+                     std::string &err, void *stream, bool det_cull)
 {
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t st = (hipStream_t)stream;
@@ -446,6 +494,7 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
     uint32_t *cnt = (uint32_t *)d_counts.p;
     uint32_t level_size = 1, depth = 0;
     int cur = 0;
+    std::vector<uint32_t> level_end{1}; /* node ids of level L: [level_end[L-1], level_end[L]) */
     while (level_size > 0) {
         ++depth;
         GCHK(hipMemsetAsync(cnt + (1 - cur), 0, sizeof(uint32_t), st));
@@ -456,7 +505,10 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
                            cnt + 4, (uint32_t *)d_perm2.p);
         GCHK(hipGetLastError());
         GCHK(hipMemcpyAsync(&level_size, cnt + (1 - cur), sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        uint32_t n_alloc = 0;
+        GCHK(hipMemcpyAsync(&n_alloc, cnt + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         GCHK(hipStreamSynchronize(st));
+        if (level_size > 0) level_end.push_back(n_alloc);
         cur = 1 - cur;
         if (depth > 4096) {
             err = "GPU BVH collapse did not terminate";
@@ -487,6 +539,18 @@ int rt_build_bvh_gpu(const float *verts_h, uint32_t n_verts, const int32_t *idx_
                        (const int32_t *)d_idx.p, (const uint32_t *)d_perm.p, (const uint32_t *)d_perm2.p, n_tris,
                        tris);
     GCHK(hipGetLastError());
+    if (det_cull) {
+        DevBuf d_nb;
+        GCHK(hipMalloc(&d_nb.p, sizeof(NBox) * out.n_nodes4));
+        for (size_t L = level_end.size(); L-- > 0;) {
+            const uint32_t a = L ? level_end[L - 1] : 0u, b = level_end[L];
+            if (b <= a) continue;
+            hipLaunchKernelGGL(k_nbox, dim3(blocks_for(b - a)), dim3(kB), 0, st, (const float *)nodes4, a, b,
+                               (const float *)tris, (NBox *)d_nb.p, q4);
+            GCHK(hipGetLastError());
+        }
+        GCHK(hipStreamSynchronize(st));
+    }
     uint32_t qfail = 0;
     GCHK(hipMemcpyAsync(&qfail, cnt + 5, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     GCHK(hipStreamSynchronize(st));

@@ -640,7 +640,9 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
         c->d_nodes4q = nullptr;
         c->n_tris = 0;
         RtGpuBvh g;
-        const int e = rt_build_bvh_gpu(verts, n_verts, idx, n_tris, g, err, c->stream);
+        bool det_cull = true;
+        if (const char *v = getenv("RT_DET_CULL")) det_cull = atoi(v) != 0; /* A/B knob */
+        const int e = rt_build_bvh_gpu(verts, n_verts, idx, n_tris, g, err, c->stream, det_cull);
         c->d_nodes4 = g.nodes4;
         c->d_nodes4q = g.nodes4q;
         c->d_tris = g.tris;

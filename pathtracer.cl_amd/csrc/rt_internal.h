@@ -103,7 +103,7 @@ struct RtGpuBvh {
     double build_seconds = 0.0;
 };
 int rt_build_bvh_gpu(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, RtGpuBvh &out,
-                     std::string &err, void *stream);
+                     std::string &err, void *stream, bool det_cull = true);
 /* Input checks shared by both builders (finite coordinates, indices in range, size limit). */
 bool rt_validate_mesh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, std::string &err);
 

@@ -320,17 +320,23 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
            subtree; below 1e-4 (with the float error bound) no triangle can be accepted, so
            the subtree is skipped.  Culling only: the same results, fewer steps. */
         {
+            /* v_perm_b32 picks, per axis, the hi byte (d >= 0) or the lo byte into `nb` (the box
+               corner maximising d . N) and the other into `fb`; v_cvt_f32_ubyteN converts in
+               place; the +128 byte bias folds into one per-ray term */
             const uint32_t nlo = q2.z, nhi = q2.w;
             const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
-            const int lx = __builtin_amdgcn_sbfe((int)nlo, 0, 8), ly = __builtin_amdgcn_sbfe((int)nlo, 8, 8),
-                      lz = __builtin_amdgcn_sbfe((int)nlo, 16, 8);
-            const int hx = __builtin_amdgcn_sbfe((int)nhi, 0, 8), hy = __builtin_amdgcn_sbfe((int)nhi, 8, 8),
-                      hz = __builtin_amdgcn_sbfe((int)nhi, 16, 8);
-            const float fhi = __builtin_fmaf(d.x, (float)(px ? hx : lx),
-                                             __builtin_fmaf(d.y, (float)(py ? hy : ly), d.z * (float)(pz ? hz : lz)));
-            const float flo = __builtin_fmaf(d.x, (float)(px ? lx : hx),
-                                             __builtin_fmaf(d.y, (float)(py ? ly : hy), d.z * (float)(pz ? lz : hz)));
+            const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
+            const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
+            const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
+            const float bias = 128.0f * (d.x + d.y + d.z);
+            const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
+                                             __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu),
+                                                            __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
+            const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
+                                             __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu),
+                                                            __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
             const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
+            /* bias rounding: |fl(128 sum d) - 128 sum d| <= 3u * 128 |d|_1, inside the margin */
             const float bound = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
             if (bound < 1e-4f) nhit = 0;
         }

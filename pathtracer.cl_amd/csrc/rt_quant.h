@@ -15,9 +15,9 @@
  *            so the box contains the exact child box; an unused slot is the inverted
  *            box lo = 255 > hi = 0, which no ray enters
  *   d[10..11] the node's normal box (determinant cull, below): the box of the reference's
- *            unnormalised normals N = e2 x e1 over every triangle of the subtree, 8-bit
- *            two's-complement fields q * 2^(E - 128): d[10] = lo.x | lo.y << 8 | lo.z << 16 |
- *            E << 24, d[11] = hi.x | hi.y << 8 | hi.z << 16 (E = 255: no cull)
+ *            unnormalised normals N = e2 x e1 over every triangle of the subtree, bytes
+ *            b = q + 128 for q * 2^(E - 128), q in [-128, 127]: d[10] = lo.x | lo.y << 8 |
+ *            lo.z << 16 | E << 24, d[11] = hi.x | hi.y << 8 | hi.z << 16 (E = 255: no cull)
  *   d[12..15] the four child links written out (rt_internal.h encoding)
  *
  * Determinant cull.  intersects_triangle rejects |det| < 1e-4 (geometryFuncs.h:167), and
@@ -130,8 +130,8 @@ RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
     for (int i = 0; i < 6; ++i) q[4 + i] = planes[i];
     (void)inner_base;
     (void)tri_base;
-    q[10] = 255u << 24 | 0x80u << 16 | 0x80u << 8 | 0x80u; /* no cull until rt_qnode_set_nbox */
-    q[11] = 0x7fu << 16 | 0x7fu << 8 | 0x7fu;
+    q[10] = 255u << 24; /* no cull until rt_qnode_set_nbox: [-128, 127] * 2^127 */
+    q[11] = 0xffu << 16 | 0xffu << 8 | 0xffu;
     for (int k = 0; k < 4; ++k) q[12 + k] = (uint32_t)code[k]; /* explicit links */
     return true;
 }
@@ -139,7 +139,7 @@ RT_QHD inline bool rt_quantize_node4(const float *f, uint32_t *q)
 /* Encode a node's normal box (exact bounds in double) into d[10..11]; `err` is the node's
    max |e1|_1 |e2|_1, so 8u * err bounds det's float error per unit |d|_1.  Nodes whose error
    bound or range the encoding cannot honour keep the no-cull box. */
-inline void rt_qnode_set_nbox(uint32_t *q, const double lo[3], const double hi[3], double err)
+RT_QHD inline void rt_qnode_set_nbox(uint32_t *q, const double lo[3], const double hi[3], double err)
 {
     if (!(8.0 * 0x1p-24 * err <= 5e-7)) return;
     double m = 0.0;
@@ -160,9 +160,9 @@ inline void rt_qnode_set_nbox(uint32_t *q, const double lo[3], const double hi[3
             if (ql[k] < -128 || qh[k] > 127 || ql[k] * step > lo[k] || qh[k] * step < hi[k]) ok = false;
         }
         if (!ok) continue;
-        q[10] = ((uint32_t)ql[0] & 0xffu) | ((uint32_t)ql[1] & 0xffu) << 8 | ((uint32_t)ql[2] & 0xffu) << 16 |
+        q[10] = (uint32_t)(ql[0] + 128) | (uint32_t)(ql[1] + 128) << 8 | (uint32_t)(ql[2] + 128) << 16 |
                 (uint32_t)(e + 128) << 24;
-        q[11] = ((uint32_t)qh[0] & 0xffu) | ((uint32_t)qh[1] & 0xffu) << 8 | ((uint32_t)qh[2] & 0xffu) << 16;
+        q[11] = (uint32_t)(qh[0] + 128) | (uint32_t)(qh[1] + 128) << 8 | (uint32_t)(qh[2] + 128) << 16;
         return;
     }
 }

@@ -112,7 +112,7 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
             if ((g_det_cull == 4 || g_det_cull == 5) && !det_possible(&g_nbox[6 * it.c], d)) continue; /* own box */
             if (g_det_cull == 7) { /* the kernel's formula on the encoded box (rt_kernels.hip trav_step_q) */
                 const uint32_t *q = g_q4 + 16ull * it.c;
-                auto sx = [](uint32_t w, int off) { int v = (w >> off) & 0xff; return v >= 128 ? v - 256 : v; };
+                auto sx = [](uint32_t w, int off) { return (int)((w >> off) & 0xff) - 128; };
                 const float nsc = std::ldexp(1.0f, (int)(q[10] >> 24) - 128);
                 const bool px = d.x >= 0, py = d.y >= 0, pz = d.z >= 0;
                 const float fhi = std::fma(d.x, (float)(px ? sx(q[11], 0) : sx(q[10], 0)),

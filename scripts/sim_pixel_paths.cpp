@@ -33,6 +33,8 @@ static V norm(V a) { return mul(a, 1.0f / std::sqrt(dot(a, a))); }
 static const float *g_n4, *g_tris;
 static const uint32_t *g_q4; /* compressed nodes: the kernel's own cull (mode 7) */
 static long g_node_steps, g_tri_steps; /* of all queries */
+static long g_near[2], g_far[2];         /* shadow-query steps entered within / beyond t = 0.05 (node, tri) */
+static bool g_track;
 /* per 4-wide node: box of the unnormalised normals e2 x e1 of its subtree's triangles (det cull) */
 static std::vector<float> g_nbox; /* 6 floats per node: lo xyz, hi xyz */
 static int g_det_cull = 0; /* 1 per child at the parent, 2 per leaf in its first record, 3 inner children only */
@@ -106,6 +108,7 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
     while (!st.empty()) {
         It it = st.back();
         st.pop_back();
+        if (g_track) (it.tn < 0.05f ? g_near : g_far)[it.c >= 0 ? 0 : 1] += it.c >= 0 ? 1 : ((~it.c) & 7) + 1;
         if (it.c >= 0) {
             ++steps;
             ++g_node_steps;
@@ -275,7 +278,9 @@ int main(int argc, char **argv)
                 float tl = std::sqrt(dot(sub(light, so), sub(light, so))) - 0.5f;
                 int h2;
                 float t2;
+                g_track = src == 0;
                 long k2 = query(so, ld, tl, true, t2, h2);
+                g_track = false;
                 st_s[src] += k2;
                 n_s[src] += 1;
                 total += k2;
@@ -292,5 +297,7 @@ int main(int argc, char **argv)
         printf("  from %-14s closest %6.0f x %5.1f steps (%4.1f%% hit mesh)   shadow %6.0f x %5.1f steps\n", names[i],
                n_c[i], n_c[i] ? st_c[i] / n_c[i] : 0, n_c[i] ? 100 * mesh_hits[i] / n_c[i] : 0, n_s[i],
                n_s[i] ? st_s[i] / n_s[i] : 0);
+    printf("camera-hit shadow queries: near (t < 0.05) %ld node + %ld tri steps, far %ld node + %ld tri\n", g_near[0],
+           g_near[1], g_far[0], g_far[1]);
     return 0;
 }

@@ -10,7 +10,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 from summarize_pmc import counters  # full-size dispatches only (the bench's 1-row tile launches excluded)
 
 src = sys.argv[1]
-kname = sys.argv[2] if len(sys.argv) > 2 else "k_tris<4, false>"
+kname = sys.argv[2] if len(sys.argv) > 2 else "k_tris<4, false, false>"
 c = counters(sorted(glob.glob(f"{src}/pmcx_*/run_counter_collection.csv")), kname)
 for k in sorted(c):
     print(f"{k:40s} {c[k]:.4g}")

@@ -263,10 +263,27 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
         const float4 b = make_float4(__uint_as_float(q1.x), __uint_as_float(q1.y), __uint_as_float(q1.z), 0.0f);
         const float4 c = make_float4(__uint_as_float(q2.x), __uint_as_float(q2.y), __uint_as_float(q2.z), 0.0f);
         float t = 0.0f;
-        bool done = false;
         const bool h = mt_test(o, d, a, b, c, t);
-        leaf_accept<COUNT>((int)(enc >> 3), a, d, h, t, tmin, s.best_t, any_hit, s.best, s.best_orig, s.best_t, done);
-        if (done) return true;
+        const int slot = (int)(enc >> 3);
+        if (h) {
+            if (any_hit) {
+                if (t < s.best_t && t > tmin) {
+                    s.best = slot;
+                    return true;
+                }
+            } else if (!(t < tmin)) {
+                /* the accept rule t < best_t || (t == best_t && orig > best_orig): the best hit's
+                   original index is read back from its record on the rare exact tie instead of
+                   being carried in a register (which the compiler spilled on every step) */
+                bool acc = t < s.best_t;
+                if (!acc && t == s.best_t)
+                    acc = s.best < 0 || __float_as_int(a.w) > __float_as_int(tris[3 * s.best].w);
+                if (acc) {
+                    s.best = slot;
+                    s.best_t = t;
+                }
+            }
+        }
         if (enc & 7u) { /* next triangle of this leaf */
             s.node = ~(int)((((enc >> 3) + 1u) << 3) | ((enc & 7u) - 1u));
             return false;

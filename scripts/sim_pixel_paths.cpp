@@ -35,6 +35,7 @@ static const uint32_t *g_q4; /* compressed nodes: the kernel's own cull (mode 7)
 static long g_node_steps, g_tri_steps; /* of all queries */
 static long g_near[2], g_far[2];         /* shadow-query steps entered within / beyond t = 0.05 (node, tri) */
 static bool g_track;
+static int g_order = 0; /* 0 sorted push (k_tris), 1 nearest first only */
 /* per 4-wide node: box of the unnormalised normals e2 x e1 of its subtree's triangles (det cull) */
 static std::vector<float> g_nbox; /* 6 floats per node: lo xyz, hi xyz */
 static int g_det_cull = 0; /* 1 per child at the parent, 2 per leaf in its first record, 3 inner children only */
@@ -157,7 +158,14 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
                 }
                 buf[k++] = {c, tn};
             }
-            std::sort(buf, buf + k, [](const It &a, const It &b) { return a.tn > b.tn; });
+            if (g_order == 0) {
+                std::sort(buf, buf + k, [](const It &a, const It &b) { return a.tn > b.tn; });
+            } else if (k > 1) { /* nearest visited first, the others pushed in slot order */
+                int m = 0;
+                for (int j = 1; j < k; ++j)
+                    if (buf[j].tn < buf[m].tn) m = j;
+                std::swap(buf[m], buf[k - 1]);
+            }
             for (int j = 0; j < k; ++j) st.push_back(buf[j]);
         } else {
             int enc = ~it.c, first = enc >> 3, cnt = (enc & 7) + 1;
@@ -232,6 +240,7 @@ int main(int argc, char **argv)
     g_nbox.resize(6ull * bvh.n_nodes4);
     build_nbox(0);
     g_det_cull = argc > 4 ? atoi(argv[4]) : 0;
+    g_order = argc > 5 ? atoi(argv[5]) : 0;
     float cam[16];
     rt_camera_spherical(0, -4, 0, 40, 105, 5, 53, W, reinterpret_cast<rt_camera *>(cam));
     const V view{cam[0], cam[1], cam[2]}, up{cam[4], cam[5], cam[6]}, right{cam[8], cam[9], cam[10]},

@@ -185,6 +185,17 @@ public:
               "rayTrace");
     }
 
+    /* Upload a changed sphere list now (rayTrace does it itself; callers that drive the
+       C-ABI directly with handle(), e.g. rt_comm_render, call this first). */
+    void flushScene()
+    {
+        if (dirty_) {
+            check(rt_set_spheres(ctx_, spheres_.empty() ? nullptr : spheres_.data(), (uint32_t)spheres_.size()),
+                  "scene upload");
+            dirty_ = false;
+        }
+    }
+
     /* Blocking readback of the last frame into host memory (the non-sharing display
        path, GlutCLWindow.cpp:214-225); n_floats = capacity of `host`. */
     void read(float *host, size_t n_floats) { check(rt_read(ctx_, host, n_floats), "read"); }

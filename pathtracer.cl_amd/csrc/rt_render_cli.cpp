@@ -10,11 +10,18 @@
  *             [--raw out.f32] [--pfm out.pfm] [--device K]
  *             [--events d,d,l,d,m:5:-3,s:64:32,d,...]   (interactive replay: ProgressiveViewHIP
  *              display / arrow keys l r u n / drag motion / reshape, GlutCLWindow.cpp:136-301)
+ *             [--tile STRIPE,N,R]   (this process renders rank R's row stripes of N: the raw output
+ *              is the compact tile — the sharding path rehearsed as separate processes)
+ *             [--comm-ranks N --comm-rank R --comm-id FILE]   (native multi-GPU: one process per
+ *              GPU, librtmi's RCCL communicator; rank 0 writes the id to FILE, the others read
+ *              it; rt_comm_render per frame, the assembled frame written by rank 0)
  */
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
+#include <fstream>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -84,17 +91,41 @@ int usage()
 {
     std::fprintf(stderr, "usage: rt_render [--scene main|ply] [--width W] [--height H] [--frames F] "
                          "[--sample-rate S] [--depth D] [--mesh N | --ply FILE] [--linear] [--raw f] [--pfm f] "
-                         "[--device K]\n");
+                         "[--device K] [--tile STRIPE,N,R] [--comm-ranks N --comm-rank R --comm-id FILE]\n");
     return 2;
+}
+
+/* The communicator id travels through a file: rank 0 writes it (rename makes it appear
+   whole), the other ranks wait for it. */
+bool share_comm_id(const std::string &path, int rank, uint8_t id[RT_COMM_ID_BYTES])
+{
+    if (rank == 0) {
+        if (rt_comm_get_unique_id(id) != RT_OK) return false;
+        const std::string tmp = path + ".tmp";
+        FILE *f = std::fopen(tmp.c_str(), "wb");
+        if (!f || std::fwrite(id, 1, RT_COMM_ID_BYTES, f) != RT_COMM_ID_BYTES) return false;
+        std::fclose(f);
+        return std::rename(tmp.c_str(), path.c_str()) == 0;
+    }
+    for (int i = 0; i < 600; ++i) {
+        if (FILE *f = std::fopen(path.c_str(), "rb")) {
+            const size_t n = std::fread(id, 1, RT_COMM_ID_BYTES, f);
+            std::fclose(f);
+            if (n == RT_COMM_ID_BYTES) return true;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    return false;
 }
 
 } // namespace
 
 int main(int argc, char **argv)
 {
-    std::string scene = "main", raw, pfm, ply_path, events;
+    std::string scene = "main", raw, pfm, ply_path, events, comm_id;
     unsigned W = 512, H = 512, frames = 1, sr = 1, depth = 6, n_tris = 0;
-    int device = 0;
+    int device = 0, comm_ranks = 0, comm_rank = 0;
+    rt_tile tile{8, 1, 0};
     bool linear = false;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -117,6 +148,11 @@ int main(int argc, char **argv)
         else if (a == "--raw") raw = v;
         else if (a == "--pfm") pfm = v;
         else if (a == "--device") device = std::atoi(v);
+        else if (a == "--tile") {
+            if (std::sscanf(v, "%u,%u,%u", &tile.stripe_rows, &tile.n_ranks, &tile.rank) != 3) return usage();
+        } else if (a == "--comm-ranks") comm_ranks = std::atoi(v);
+        else if (a == "--comm-rank") comm_rank = std::atoi(v);
+        else if (a == "--comm-id") comm_id = v;
         else return usage();
     }
     const bool ply = scene == "ply" || n_tris > 0 || !ply_path.empty();
@@ -172,17 +208,44 @@ int main(int argc, char **argv)
             }
             return 0;
         }
+        rt_comm *comm = nullptr;
+        if (comm_ranks > 0) { /* native multi-GPU: librtmi's RCCL communicator */
+            uint8_t id[RT_COMM_ID_BYTES];
+            if (comm_id.empty() || !share_comm_id(comm_id, comm_rank, id)) {
+                std::fprintf(stderr, "rt_render: no communicator id (--comm-id)\n");
+                return 1;
+            }
+            if (rt_comm_create(id, comm_ranks, comm_rank, device, &comm) != RT_OK) {
+                std::fprintf(stderr, "rt_render: rt_comm_create failed\n");
+                return 1;
+            }
+        }
+        const bool tiled = !comm && tile.n_ranks > 1;
+        const unsigned rows = tiled ? rt_tile_rows(H, &tile) : H;
         float *dbuf = nullptr;
-        if (hipMalloc(&dbuf, (size_t)W * H * 16) != hipSuccess) return 1;
+        if (hipMalloc(&dbuf, (size_t)W * std::max(rows, 1u) * 16) != hipSuccess) return 1;
         double rays = 0;
         const auto t0 = std::chrono::steady_clock::now();
         for (unsigned p = 0; p < frames; ++p) {
-            rt.rayTrace(dbuf, W, H, p, kernel, true);
+            if (comm) {
+                rt.flushScene();
+                if (rt_comm_render(comm, rt.handle(), dbuf, W, H, p, kernel, 8, 0) != RT_OK) {
+                    std::fprintf(stderr, "rt_render: rt_comm_render: %s\n", rt_comm_last_error(comm));
+                    return 1;
+                }
+            } else {
+                rt.rayTrace(dbuf, W, H, p, kernel, true, tiled ? &tile : nullptr);
+            }
             const rt_counters c = rt.counters();
             rays += (double)(c.rays_closest + c.rays_shadow);
         }
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::vector<float> img((size_t)W * H * 4);
+        if (comm) rt_comm_destroy(comm);
+        if (comm && comm_rank != 0) { /* the frame lives on rank 0 */
+            (void)hipFree(dbuf);
+            return 0;
+        }
+        std::vector<float> img((size_t)W * rows * 4);
         if (hipMemcpy(img.data(), dbuf, img.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return 1;
         (void)hipFree(dbuf);
         std::printf("{\"frames\": %u, \"seconds\": %.6f, \"frames_per_sec\": %.4f, \"mrays_per_sec\": %.2f}\n", frames,
@@ -195,8 +258,8 @@ int main(int argc, char **argv)
         if (!pfm.empty()) { /* PFM: bottom-to-top rows, RGB, little-endian */
             FILE *f = std::fopen(pfm.c_str(), "wb");
             if (!f) return 1;
-            std::fprintf(f, "PF\n%u %u\n-1.0\n", W, H);
-            for (int y = (int)H - 1; y >= 0; --y)
+            std::fprintf(f, "PF\n%u %u\n-1.0\n", W, rows);
+            for (int y = (int)rows - 1; y >= 0; --y)
                 for (unsigned x = 0; x < W; ++x) std::fwrite(&img[((size_t)y * W + x) * 4], 4, 3, f);
             std::fclose(f);
         }

@@ -731,6 +731,38 @@ def test_cpp_host_replays_reference_app(args, name, tracer, golden, tmp_path):
     np.testing.assert_array_equal(bits(got), bits(exp))
 
 
+def test_cpp_host_shards(tracer, golden, tmp_path):
+    """The C++ host's sharding paths (rt_render_cli.cpp): two separate processes each render
+    one rank's row stripes (`--tile 8,2,r`), and the compact tiles reassemble to the reference
+    kernel's frame; a native RCCL communicator (`--comm-ranks 1`: rt_comm_create,
+    rt_comm_render, gather to rank 0) writes the same frame.  (RCCL refuses two ranks on one
+    GPU; the multi-rank exchange runs on the 8-GPU node.)"""
+    import subprocess
+    from importlib import import_module
+
+    from conftest import ROOT
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    cli = str(ROOT / "pathtracer.cl_amd" / "rt_render")
+    base = ["--mesh", "2000", "--width", "64", "--height", "48", "--frames", "3"]
+    W, H = 64, 48
+    exp = golden("tris_64x48_sr1")["frames"][-1]
+    procs, tiles = [], []
+    for r in range(2):
+        raw = tmp_path / f"tile{r}.f32"
+        procs.append(subprocess.Popen([cli, *base, "--tile", f"8,2,{r}", "--raw", str(raw)]))
+        tiles.append(raw)
+    for p in procs:
+        assert p.wait(timeout=120) == 0
+    parts = [np.fromfile(t, np.float32).reshape(-1, W, 4) for t in tiles]
+    frame = dist.assemble(parts, H, W, 8)
+    np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(exp))
+    raw = tmp_path / "comm.f32"
+    subprocess.run([cli, *base, "--comm-ranks", "1", "--comm-rank", "0", "--comm-id", str(tmp_path / "id"),
+                    "--raw", str(raw)], check=True, timeout=120)
+    np.testing.assert_array_equal(bits(np.fromfile(raw, np.float32)), bits(exp))
+
+
 def test_ply_mesh_cli_and_oracle(tracer, pt, oracle, tmp_path):
     """A PLY file (binary LE, Stanford-scan layout) through both hosts: the C++ CLI (--ply,
     plymain.cpp's scene with the mesh actually handed to the tracer) and the Python RayTracer

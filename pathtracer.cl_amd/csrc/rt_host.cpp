@@ -96,7 +96,8 @@ struct rt_ctx {
     size_t defer_rec_cap = 0, defer_seg_cap = 0, defer_slot_cap = 0; /* allocated entries */
     uint32_t n_defer = 0;
     int defer = -1;          /* RT_DEFER: 1 on, 0 off, unset = auto (on when the launch has fewer than
-                                4 pixels per resident lane: tiles of a multi-GPU frame) */
+                                4 pixels per resident lane at sampleRate >= 4: tiles of a multi-GPU
+                                many-sample frame) */
     size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer buffers */
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
@@ -368,9 +369,10 @@ int classify_pixels(rt_ctx *c, const std::vector<uint32_t> &f, uint32_t W, uint3
     const size_t npx = (size_t)W * hl;
     /* Deferral shortens the box chains but moves their shadow queries into a second launch
        that cannot use the tail of the first: it pays where the chains set the frame time (a
-       tile with few pixels per lane), not on a full frame (dragon 1920x1080: 161.7 ->
-       173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) */
-    const bool use = c->defer == 1 || (c->defer < 0 && npx < 4 * lanes);
+       tile with few pixels per lane) of a many-sample frame, not on a full frame (dragon
+       1920x1080: 161.7 -> 173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) nor on short
+       chains (bunny class 1024^2 at 1 spp: 0.95 -> 1.35 ms, r02u) */
+    const bool use = c->defer == 1 || (c->defer < 0 && npx < 4 * lanes && c->sample_rate >= 4);
     const uint32_t pn2 = c->probe_n * c->probe_n;
     const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
     const uint64_t nl = c->lights.size();

@@ -82,6 +82,10 @@ struct rt_ctx {
     float *d_nodes4 = nullptr; /* 4-wide tree */
     uint32_t *d_nodes4q = nullptr; /* 4-wide tree, compressed nodes */
     float *d_tris = nullptr;
+    size_t tris_cap = 0;       /* triangle records d_tris holds (mesh + camera-ray candidate lists) */
+    uint8_t *d_lists = nullptr; /* candidate count per pixel (k_pixel_lists) */
+    size_t lists_bytes = 0;
+    bool pixel_lists = true;   /* RT_PIXEL_LISTS=0: camera rays always traverse the BVH */
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
@@ -314,6 +318,20 @@ const float *trav_nodes(const rt_ctx *c)
     const int k = trav_kind(c);
     if (k == RT_TRAV_BVH4Q) return reinterpret_cast<const float *>(c->d_nodes4q);
     return k == RT_TRAV_BVH4 ? c->d_nodes4 : nullptr;
+}
+
+/* Grow the triangle buffer to `records` 48-B records, keeping the first `keep` (the mesh's). */
+int ensure_tris_capacity(rt_ctx *c, size_t records, size_t keep, hipStream_t st)
+{
+    if (records <= c->tris_cap) return RT_OK;
+    float *nt = nullptr;
+    HIPCHK(c, hipMalloc(&nt, records * 48));
+    HIPCHK(c, hipMemcpyAsync(nt, c->d_tris, keep * 48, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    free_dev(c->d_tris);
+    c->d_tris = nt;
+    c->tris_cap = records;
+    return RT_OK;
 }
 
 int ensure_spill(rt_ctx *c, size_t entries)
@@ -559,6 +577,7 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_FETCH_FRAC")) c->fetch_frac = (uint32_t)std::max(0, std::min(64, atoi(v)));
     if (const char *v = getenv("RT_BOX_EXIT")) c->box_exit = atoi(v) != 0;
     if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0; /* A/B knob */
+    if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0; /* A/B knob */
     if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -592,6 +611,7 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_halo_rows);
     free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
+    free_dev(c->d_lists);
     free_dev(c->d_seeds);
     free_dev(c->d_work);
     free_dev(c->d_counters);
@@ -648,6 +668,7 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
         c->d_nodes4 = g.nodes4;
         c->d_nodes4q = g.nodes4q;
         c->d_tris = g.tris;
+        c->tris_cap = n_tris;
         if (e) return fail(c, RT_ERR_HIP, "GPU BVH build: " + err);
         c->n_tris = n_tris;
         c->mesh_serial++;
@@ -677,6 +698,7 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     HIPCHK(c, hipMalloc(&c->d_nodes4, b.nodes4.size() * sizeof(float)));
     if (!b.nodes4q.empty()) HIPCHK(c, hipMalloc(&c->d_nodes4q, b.nodes4q.size() * sizeof(uint32_t)));
     HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
+    c->tris_cap = b.tris.size() / 12;
     HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
     if (!b.nodes4q.empty())
         HIPCHK(c, hipMemcpy(c->d_nodes4q, b.nodes4q.data(), b.nodes4q.size() * sizeof(uint32_t),
@@ -985,8 +1007,32 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             HIPCHK(c, hipMemsetAsync(d_stats, 0, (size_t)W * hl * 32, st));
             a.pixel_stats = d_stats;
         }
+        /* camera-ray candidate lists (k_pixel_lists, rebuilt every frame): list slots after the
+           mesh's triangle records, one count per pixel */
+        a.pixel_lists = nullptr;
+        const bool bvh4 = c->d_nodes4 && (trav == RT_TRAV_BVH4Q || trav == RT_TRAV_BVH4);
+        const uint64_t kept = c->n_tris;
+        a.list_base = (uint32_t)kept;
+        const uint64_t list_recs = (uint64_t)W * hl * RT_LIST_MAX;
+        const bool lists = c->pixel_lists && bvh4 && kept + list_recs < (1ull << 28);
+        if (lists) {
+            const int r = ensure_tris_capacity(c, (size_t)(kept + list_recs), kept, st);
+            if (r != RT_OK) return r;
+            if (c->lists_bytes < (size_t)W * hl) {
+                free_dev(c->d_lists);
+                c->d_lists = nullptr;
+                c->lists_bytes = 0;
+                HIPCHK(c, hipMalloc(&c->d_lists, (size_t)W * hl));
+                c->lists_bytes = (size_t)W * hl;
+            }
+            a.pixel_lists = c->d_lists;
+        }
+        a.tris = c->d_tris;
         HIPCHK(c, hipEventRecord(c->ev0, st));
-        e = rt_launch_tris(a, trav, c->counting, blocks, st);
+        e = lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr, c->d_lists,
+                                          st)
+                  : 0;
+        if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
         if (!e && a.n_defer) e = rt_launch_defer(a, c->counting, blocks, st);
         c->last_deferred = a.n_defer;
         HIPCHK(c, hipEventRecord(c->ev1, st));

@@ -148,7 +148,16 @@ struct RtTriLaunch {
     uint32_t *defer_qcount;     /* [0] queue length (k_tris), [1] consumer cursor (k_defer_shadow) */
     const uint32_t *defer_pixel; /* per slot: yl * W + x */
     uint32_t n_defer;           /* slots in use */
+    /* Camera-ray candidate lists (k_pixel_lists): per pixel the triangles any of its sample
+       rays could accept, RT_LIST_MAX at most, their records copied to triangle slots
+       list_base + pixel * RT_LIST_MAX + i; pixel_lists[pixel] = count, RT_LIST_NONE = no list */
+    const uint8_t *pixel_lists;
+    uint32_t list_base;
 };
+#ifndef RT_LIST_MAX
+#define RT_LIST_MAX 32
+#endif
+#define RT_LIST_NONE 255
 /* segment kinds of a deferred pixel's path (trace_path_tri, rtcommon.h:378-468) */
 enum { RT_SEG_BOX = 0, RT_SEG_TRI = 1, RT_SEG_NONE = 2 };
 
@@ -176,6 +185,11 @@ int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris,
 /* Deferred shadow rays: trace the queued records (persistent grid), then replay the deferred
    pixels' colours and write them (one wave per slot).  Same stream as k_tris, after it. */
 int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *stream);
+/* Camera-ray candidate lists for the launch's pixels (writes a.pixel_lists and the list
+   records in the triangle buffer at a.list_base); nodes4 = full-precision 4-wide tree,
+   q4 = compressed nodes (their normal boxes; may be NULL). */
+int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint8_t *counts,
+                          void *stream);
 /* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed

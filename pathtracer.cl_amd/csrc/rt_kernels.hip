@@ -963,6 +963,27 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 } else {
                     trav_begin(ts, stk, qo, qd, qt);
                     running = true;
+                    if (!shadow && depth == 0 && a.pixel_lists) { /* a camera ray: the pixel's candidate list */
+                        const uint32_t pix = yl * a.W + x;
+                        const uint32_t pc = a.pixel_lists[pix];
+                        uint32_t first = a.list_base + pix * RT_LIST_MAX;
+                        if (pc == 0) { /* no triangle can be accepted by any of the pixel's camera rays */
+                            running = false;
+                            ts.best = -1;
+                            fin = true;
+                        } else if (pc <= RT_LIST_MAX) {
+                            /* the candidates as virtual leaves of up to 8: the first is stepped
+                               now, the others wait on the (empty) stack */
+                            const uint32_t k0 = pc < 8u ? pc : 8u;
+                            ts.node = ~(int)((first << 3) | (k0 - 1u));
+                            for (uint32_t rem = pc - k0; rem > 0;) {
+                                first += 8u;
+                                const uint32_t k = rem < 8u ? rem : 8u;
+                                stk.push(~(int)((first << 3) | (k - 1u)));
+                                rem -= k;
+                            }
+                        }
+                    }
                 }
             }
             const unsigned long long t_c0 = COUNT ? wave_clock() : 0ull;
@@ -1458,6 +1479,185 @@ __global__ __launch_bounds__(64) void k_defer_finish(RtTriLaunch a)
     }
 }
 
+/* Camera-ray candidate lists.  A pixel's sampleRate^2 camera rays share the camera position
+   and leave through the pixel's square (strat_rand offsets in [0, 1], raytracer.cl:216-224), so
+   one conservative traversal of that narrow frustum finds every triangle any of them could
+   accept: directions bounded component-wise by the four corner rays (camera_dir, the kernel's
+   own arithmetic) padded by 1e-5; boxes tested with interval slabs in binary64 (per axis the
+   earliest entry and latest exit over the direction interval — a necessary condition for a
+   hit); nodes whose normal box keeps |d . N| below the determinant threshold for every
+   direction skipped (rt_quant.h); triangles kept if their padded box (the builder's pad) meets
+   the frustum and some direction could give |det| >= 1e-4 (with det's float error).  Up to
+   RT_LIST_MAX survivors are copied into the pixel's list slots; k_tris then answers each camera
+   query by testing only them (a virtual leaf: the same tests and accept rule on the same
+   records, so the same closest hit), and an empty list answers "no mesh hit" outright.  Pixels
+   with more candidates (or a stack overflow) keep the BVH. */
+__device__ __forceinline__ bool frustum_slab(const double olo[3], const double ohi[3], const double dlo[3],
+                                             const double dhi[3], const double lo[3], const double hi[3], double tmax)
+{
+    /* rays o + t d with o in [olo, ohi], d in [dlo, dhi]: per axis (P - o) / d is monotonic in
+       o and in d (d of one sign), so its range is spanned by the four corner quotients */
+    double tin = -1e300, tout = 1e300;
+    for (int k = 0; k < 3; ++k) {
+        const double a = dlo[k], b = dhi[k];
+        if (!(a > 0.0 || b < 0.0)) {
+            /* d straddles 0 on this axis: at t >= 0 the rays' coordinate spans
+               [olo + t a, ohi + t b], which must reach [lo, hi] (a lower bound on t) */
+            if (a < 0.0) tin = fmax(tin, (hi[k] - olo[k]) / a);
+            else if (olo[k] > hi[k]) return false;
+            if (b > 0.0) tin = fmax(tin, (lo[k] - ohi[k]) / b);
+            else if (ohi[k] < lo[k]) return false;
+            continue;
+        }
+        const double ne = a > 0.0 ? lo[k] : hi[k], fa = a > 0.0 ? hi[k] : lo[k];
+        const double n1 = (ne - olo[k]) / a, n2 = (ne - olo[k]) / b, n3 = (ne - ohi[k]) / a, n4 = (ne - ohi[k]) / b;
+        const double f1 = (fa - olo[k]) / a, f2 = (fa - olo[k]) / b, f3 = (fa - ohi[k]) / a, f4 = (fa - ohi[k]) / b;
+        tin = fmax(tin, fmin(fmin(n1, n2), fmin(n3, n4)));
+        tout = fmin(tout, fmax(fmax(f1, f2), fmax(f3, f4)));
+    }
+    tin = fmax(tin, -1e-3); /* accepted hits have t > tmin > 0 */
+    return tin <= tout && tin <= tmax;
+}
+
+/* max over the direction box of |d . n| for n in [nlo, nhi] */
+__device__ __forceinline__ double frustum_det(const double dlo[3], const double dhi[3], const double nlo[3],
+                                              const double nhi[3])
+{
+    double mx = 0.0, mn = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double c0 = dlo[k] * nlo[k], c1 = dlo[k] * nhi[k], c2 = dhi[k] * nlo[k], c3 = dhi[k] * nhi[k];
+        mx += fmax(fmax(c0, c1), fmax(c2, c3));
+        mn += fmin(fmin(c0, c1), fmin(c2, c3));
+    }
+    return fmax(mx, -mn);
+}
+
+/* The builder's padded triangle box (rt_bvh.cpp: extent / 512 + 1e-6 (1 + |coord|), doubled
+   here), from a record's vertices, and the largest |N| component of its normal e2 x e1. */
+__device__ __forceinline__ void tri_padded_box(float4 r0, float4 r1, float4 r2, double lo[3], double hi[3],
+                                               double &nmax)
+{
+    const float vx[3] = {r0.x, r0.x + r1.x, r0.x + r2.x}, vy[3] = {r0.y, r0.y + r1.y, r0.y + r2.y},
+                vz[3] = {r0.z, r0.z + r1.z, r0.z + r2.z};
+    const float *vv[3] = {vx, vy, vz};
+    float bl[3], bh[3], mabs = 0.0f;
+    for (int q = 0; q < 3; ++q) {
+        bl[q] = fminf(vv[q][0], fminf(vv[q][1], vv[q][2]));
+        bh[q] = fmaxf(vv[q][0], fmaxf(vv[q][1], vv[q][2]));
+        mabs = fmaxf(mabs, fmaxf(fabsf(bl[q]), fabsf(bh[q])));
+    }
+    const float ext = fmaxf(bh[0] - bl[0], fmaxf(bh[1] - bl[1], bh[2] - bl[2]));
+    const double pad = 2.0 * ((double)ext * (1.0 / 512.0) + 1e-6 * (1.0 + mabs));
+    for (int q = 0; q < 3; ++q) {
+        lo[q] = bl[q] - pad;
+        hi[q] = bh[q] + pad;
+    }
+    const double e1[3] = {r1.x, r1.y, r1.z}, e2[3] = {r2.x, r2.y, r2.z};
+    nmax = fmax(fabs(e2[1] * e1[2] - e2[2] * e1[1]),
+                fmax(fabs(e2[2] * e1[0] - e2[0] * e1[2]), fabs(e2[0] * e1[1] - e2[1] * e1[0])));
+}
+
+__device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *__restrict__ q4,
+                             const float4 *__restrict__ tris, const double olo[3], const double ohi[3],
+                             const double dlo[3], const double dhi[3], double l1, double tmax, float4 *lst, uint32_t cap,
+                             uint32_t &n);
+
+__global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const float *__restrict__ nodes4,
+                                                          const uint32_t *__restrict__ q4, uint8_t *__restrict__ counts)
+{
+    const uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x;
+    if (p >= a.W * a.Hl) return;
+    const uint32_t x = p % a.W, yl = p / a.W;
+    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+    const float hw = ((float)a.W) / 2.0f, hh = ((float)a.H) / 2.0f;
+    double dlo[3] = {1e300, 1e300, 1e300}, dhi[3] = {-1e300, -1e300, -1e300};
+    for (int c = 0; c < 4; ++c) {
+        const V3 d = camera_dir(a.cam, (float)(x + (c & 1)) - hw, (float)(y + (c >> 1)) - hh);
+        const double dv[3] = {d.x, d.y, d.z};
+        for (int k = 0; k < 3; ++k) {
+            dlo[k] = fmin(dlo[k], dv[k]);
+            dhi[k] = fmax(dhi[k], dv[k]);
+        }
+    }
+    double l1 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        dlo[k] -= 1e-5;
+        dhi[k] += 1e-5;
+        l1 += fmax(fabs(dlo[k]), fabs(dhi[k]));
+    }
+    const double o[3] = {a.cam.position.x, a.cam.position.y, a.cam.position.z};
+    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
+    float4 *__restrict__ lst = const_cast<float4 *>(tris) + 3ull * (a.list_base + (size_t)p * RT_LIST_MAX);
+    uint32_t n = 0;
+    const bool ok = frustum_list(nodes4, q4, tris, o, o, dlo, dhi, l1, 1e300, lst, RT_LIST_MAX, n);
+    counts[p] = ok ? (uint8_t)n : (uint8_t)RT_LIST_NONE;
+}
+
+/* Conservative traversal for k_pixel_lists: every triangle some ray o + t d (o in [olo, ohi],
+   d in [dlo, dhi], t <= tmax) could accept under intersects_triangle's tests is copied to
+   `lst` (`cap` at most: false on overflow). */
+__device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *__restrict__ q4,
+                             const float4 *__restrict__ tris, const double olo[3], const double ohi[3],
+                             const double dlo[3], const double dhi[3], double l1, double tmax, float4 *lst, uint32_t cap,
+                             uint32_t &n)
+{
+    int stack[64];
+    int sp = 0, node = 0;
+    n = 0;
+    bool ok = true;
+    for (;;) {
+        const float *f = nodes4 + 32ull * (uint32_t)node;
+        for (int k = 0; k < 4 && ok; ++k) {
+            const int c = __float_as_int(f[24 + k]);
+            if (c == RT_EMPTY_CHILD) continue;
+            const double lo[3] = {f[0 + k], f[8 + k], f[16 + k]}, hi[3] = {f[4 + k], f[12 + k], f[20 + k]};
+            if (!frustum_slab(olo, ohi, dlo, dhi, lo, hi, tmax)) continue;
+            if (c >= 0) {
+                if (q4) { /* the child's normal box (determinant cull) */
+                    const uint32_t wl = q4[(size_t)RT_QNODE_DWORDS * (uint32_t)c + 10];
+                    const uint32_t wh = q4[(size_t)RT_QNODE_DWORDS * (uint32_t)c + 11];
+                    const double sc = ldexp(1.0, (int)(wl >> 24) - 128);
+                    const double nlo[3] = {((int)(wl & 255u) - 128) * sc, ((int)((wl >> 8) & 255u) - 128) * sc,
+                                           ((int)((wl >> 16) & 255u) - 128) * sc};
+                    const double nhi[3] = {((int)(wh & 255u) - 128) * sc, ((int)((wh >> 8) & 255u) - 128) * sc,
+                                           ((int)((wh >> 16) & 255u) - 128) * sc};
+                    if (frustum_det(dlo, dhi, nlo, nhi) * 1.02 + 5e-7 * l1 < 1e-4) continue;
+                }
+                if (sp >= 64) {
+                    ok = false;
+                    break;
+                }
+                stack[sp++] = c;
+                continue;
+            }
+            const int enc = ~c, first = enc >> 3, cnt = (enc & 7) + 1;
+            for (int j = 0; j < cnt; ++j) {
+                const int s = first + j;
+                const float4 r0 = tris[3 * s], r1 = tris[3 * s + 1], r2 = tris[3 * s + 2];
+                double lo[3], hi[3], nmax;
+                tri_padded_box(r0, r1, r2, lo, hi, nmax);
+                if (!frustum_slab(olo, ohi, dlo, dhi, lo, hi, tmax)) continue;
+                const double e1[3] = {r1.x, r1.y, r1.z}, e2[3] = {r2.x, r2.y, r2.z};
+                const double nv[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
+                                      e2[0] * e1[1] - e2[1] * e1[0]};
+                const double el = (fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2])) * (fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2]));
+                if (frustum_det(dlo, dhi, nv, nv) * (1.0 + 1e-6) + 8.0 * 0x1p-24 * l1 * el < 1e-4) continue;
+                if (n >= cap) {
+                    ok = false;
+                    break;
+                }
+                lst[3 * n] = r0;
+                lst[3 * n + 1] = r1;
+                lst[3 * n + 2] = r2;
+                ++n;
+            }
+        }
+        if (!ok || sp == 0) break;
+        node = stack[--sp];
+    }
+    return ok;
+}
+
 /* Seed-row halo pack / unpack (multi-GPU progressive sphere frames). */
 __global__ __launch_bounds__(RT_BLOCK) void k_seed_rows(uint32_t *__restrict__ seeds, uint32_t wpad, uint32_t hpad,
                                                         const uint32_t *__restrict__ rows, uint32_t n,
@@ -1582,6 +1782,15 @@ int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *str
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_defer_finish, dim3(a.n_defer), dim3(64), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint8_t *counts, void *stream)
+{
+    const uint32_t npx = a.W * a.Hl;
+    if (!npx) return 0;
+    hipLaunchKernelGGL(k_pixel_lists, dim3((npx + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, (hipStream_t)stream,
+                       a, nodes4, q4, counts);
     return (int)hipGetLastError();
 }
 

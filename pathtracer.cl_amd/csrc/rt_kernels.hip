@@ -330,7 +330,10 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fz01 : fz23, i & 1), sz24, bzo), tmax_c));
             const bool h = tn <= tf; /* an unused slot's inverted box never passes */
             c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
-            t[i] = h ? tn : kInf;
+            /* any hit: children whose box holds the ray origin (the surface the shadow ray
+               leaves, whose own triangles it cannot hit) are visited last — the occluder,
+               when there is one, is found in fewer steps; the answer is order-free */
+            t[i] = h ? (any_hit && tn <= 0.0f ? tn + 1e4f : tn) : kInf;
             nhit += h ? 1 : 0;
         }
         /* Determinant cull (rt_quant.h): the node's normal box bounds d . N = det over its

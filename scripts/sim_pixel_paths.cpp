@@ -35,7 +35,8 @@ static const uint32_t *g_q4; /* compressed nodes: the kernel's own cull (mode 7)
 static long g_node_steps, g_tri_steps; /* of all queries */
 static long g_near[2], g_far[2];         /* shadow-query steps entered within / beyond t = 0.05 (node, tri) */
 static bool g_track;
-static int g_order = 0; /* 0 sorted push (k_tris), 1 nearest first only */
+static double g_occ[2], g_occ_steps[2]; /* camera-hit shadow queries: unoccluded / occluded, and their steps */
+static int g_order = 0; /* 0 sorted push, 1 nearest first only, 2 sorted with any-hit origin boxes last (k_tris) */
 /* per 4-wide node: box of the unnormalised normals e2 x e1 of its subtree's triangles (det cull) */
 static std::vector<float> g_nbox; /* 6 floats per node: lo xyz, hi xyz */
 static int g_det_cull = 0; /* 1 per child at the parent, 2 per leaf in its first record, 3 inner children only */
@@ -158,7 +159,12 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
                 }
                 buf[k++] = {c, tn};
             }
-            if (g_order == 0) {
+            if (g_order == 2 && any) { /* any-hit: children holding the origin visited last */
+                It key[4];
+                for (int j = 0; j < k; ++j) key[j] = {buf[j].c, buf[j].tn <= -1e-3f ? buf[j].tn + 1e4f : buf[j].tn};
+                std::sort(key, key + k, [](const It &a, const It &b) { return a.tn > b.tn; });
+                for (int j = 0; j < k; ++j) buf[j] = {key[j].c, key[j].tn >= 1e3f ? key[j].tn - 1e4f : key[j].tn};
+            } else if (g_order == 0 || g_order == 2) {
                 std::sort(buf, buf + k, [](const It &a, const It &b) { return a.tn > b.tn; });
             } else if (k > 1) { /* nearest visited first, the others pushed in slot order */
                 int m = 0;
@@ -292,6 +298,10 @@ int main(int argc, char **argv)
                 g_track = false;
                 st_s[src] += k2;
                 n_s[src] += 1;
+                if (src == 0) {
+                    g_occ[h2 >= 0] += 1;
+                    g_occ_steps[h2 >= 0] += k2;
+                }
                 total += k2;
             }
             if (hit >= 0) break;
@@ -308,5 +318,7 @@ int main(int argc, char **argv)
                n_s[i] ? st_s[i] / n_s[i] : 0);
     printf("camera-hit shadow queries: near (t < 0.05) %ld node + %ld tri steps, far %ld node + %ld tri\n", g_near[0],
            g_near[1], g_far[0], g_far[1]);
+    printf("camera-hit shadow queries: %.0f unoccluded x %.1f steps, %.0f occluded x %.1f steps\n", g_occ[0],
+           g_occ[0] ? g_occ_steps[0] / g_occ[0] : 0, g_occ[1], g_occ[1] ? g_occ_steps[1] / g_occ[1] : 0);
     return 0;
 }

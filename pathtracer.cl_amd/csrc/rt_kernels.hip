@@ -225,7 +225,7 @@ __device__ __forceinline__ float half_of(uint32_t w, int hi)
 template <bool COUNT>
 __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                             TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
-                                            TravCounts &cnt)
+                                            TravCounts &cnt, bool longest = false)
 {
     const float tmin_c = -1e-3f;
     const V3 inv = s.inv, oi = s.oi;
@@ -330,10 +330,13 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fz01 : fz23, i & 1), sz24, bzo), tmax_c));
             const bool h = tn <= tf; /* an unused slot's inverted box never passes */
             c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
-            /* any hit: children whose box holds the ray origin (the surface the shadow ray
-               leaves, whose own triangles it cannot hit) are visited last — the occluder,
-               when there is one, is found in fewer steps; the answer is order-free */
-            t[i] = h ? (any_hit && tn <= 0.0f ? tn + 1e4f : tn) : kInf;
+            /* Any hit (the answer is order-free): children whose box holds the ray origin (the
+               surface a shadow ray leaves, whose own triangles it cannot hit) are visited
+               last, and a ray leaving the mesh (`longest`) takes the others by the length of
+               its box segment, longest first — measured on the CPU model to find an occluder
+               in the fewest steps; rays from the box walls keep nearest first. */
+            const float key = longest ? tn - tf : tn;
+            t[i] = h ? (any_hit && tn <= 0.0f ? key + 1e4f : key) : kInf;
             nhit += h ? 1 : 0;
         }
         /* Determinant cull (rt_quant.h): the node's normal box bounds d . N = det over its
@@ -399,9 +402,9 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                           TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
-                                          TravCounts &cnt)
+                                          TravCounts &cnt, bool longest = false)
 {
-    if (TRAV == RT_TRAV_BVH4Q) return trav_step_q<COUNT>(nodes, tris, s, stk, o, d, tmin, any_hit, cnt);
+    if (TRAV == RT_TRAV_BVH4Q) return trav_step_q<COUNT>(nodes, tris, s, stk, o, d, tmin, any_hit, cnt, longest);
     const float tmin_c = -1e-3f;
     const V3 inv = s.inv, oi = s.oi;
     int node = s.node;
@@ -1012,7 +1015,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     if (running) {
                         const bool shadow = (mode == M_SHADOW);
                         TravCounts tc = {0u, 0u, 0u};
-                        if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, shadow, tc)) {
+                        if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, shadow, tc,
+                                                   shadow && tri_hit)) {
                             running = false;
                             fin = true;
                         }

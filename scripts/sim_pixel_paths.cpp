@@ -35,8 +35,9 @@ static const uint32_t *g_q4; /* compressed nodes: the kernel's own cull (mode 7)
 static long g_node_steps, g_tri_steps; /* of all queries */
 static long g_near[2], g_far[2];         /* shadow-query steps entered within / beyond t = 0.05 (node, tri) */
 static bool g_track;
+static bool g_from_mesh; /* the shadow query leaves a mesh hit */
 static double g_occ[2], g_occ_steps[2]; /* camera-hit shadow queries: unoccluded / occluded, and their steps */
-static int g_order = 0; /* 0 sorted push, 1 nearest first only, 2 sorted with any-hit origin boxes last (k_tris) */
+static int g_order = 0; /* 0 sorted push, 1 nearest first only, 2 sorted with any-hit origin boxes last, 3 and those by segment length, 5 = 3 for shadow rays leaving the mesh else 2 (k_tris) */
 /* per 4-wide node: box of the unnormalised normals e2 x e1 of its subtree's triangles (det cull) */
 static std::vector<float> g_nbox; /* 6 floats per node: lo xyz, hi xyz */
 static int g_det_cull = 0; /* 1 per child at the parent, 2 per leaf in its first record, 3 inner children only */
@@ -139,6 +140,7 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
             }
             const float *f = g_n4 + 32 * it.c;
             It buf[4];
+            float bt[4];
             int k = 0;
             for (int i = 0; i < 4; ++i) {
                 int c;
@@ -157,14 +159,19 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
                     else leaf_nbox(c, cb);
                     if (!det_possible(cb, d)) continue;
                 }
+                bt[k] = tf;
                 buf[k++] = {c, tn};
             }
-            if (g_order == 2 && any) { /* any-hit: children holding the origin visited last */
+            if (g_order >= 2 && any) { /* any-hit: children holding the origin visited last */
                 It key[4];
-                for (int j = 0; j < k; ++j) key[j] = {buf[j].c, buf[j].tn <= -1e-3f ? buf[j].tn + 1e4f : buf[j].tn};
+                for (int j = 0; j < k; ++j) {
+                    const bool longest = g_order == 3 || (g_order == 5 && g_from_mesh);
+                    float kk = longest ? -(bt[j] - buf[j].tn) : g_order == 4 ? -buf[j].tn : buf[j].tn;
+                    key[j] = {buf[j].c, buf[j].tn <= -1e-3f ? kk + 1e4f : kk};
+                }
                 std::sort(key, key + k, [](const It &a, const It &b) { return a.tn > b.tn; });
-                for (int j = 0; j < k; ++j) buf[j] = {key[j].c, key[j].tn >= 1e3f ? key[j].tn - 1e4f : key[j].tn};
-            } else if (g_order == 0 || g_order == 2) {
+                for (int j = 0; j < k; ++j) buf[j] = {key[j].c, 0.0f};
+            } else if (g_order != 1) {
                 std::sort(buf, buf + k, [](const It &a, const It &b) { return a.tn > b.tn; });
             } else if (k > 1) { /* nearest visited first, the others pushed in slot order */
                 int m = 0;
@@ -294,6 +301,7 @@ int main(int argc, char **argv)
                 int h2;
                 float t2;
                 g_track = src == 0;
+                g_from_mesh = hit >= 0;
                 long k2 = query(so, ld, tl, true, t2, h2);
                 g_track = false;
                 st_s[src] += k2;

@@ -153,7 +153,7 @@ struct rt_ctx {
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
     /* persistent-grid size per (traversal kind, counting): index trav * 2 + count */
-    int grid_cache[2 * (RT_TRAV_BVH4Q + 1)] = {};
+    int grid_cache[4 * (RT_TRAV_BVH4Q + 1)] = {};
 };
 
 namespace {
@@ -345,14 +345,14 @@ int ensure_spill(rt_ctx *c, size_t entries)
     return RT_OK;
 }
 
-int grid_blocks(rt_ctx *c, int trav, bool count, int *out)
+int grid_blocks(rt_ctx *c, int trav, bool count, bool defer, int *out)
 {
-    const int key = trav * 2 + (count ? 1 : 0);
+    const int key = trav * 4 + (count ? 2 : 0) + (defer ? 1 : 0);
     if (key < 0 || key >= (int)(sizeof(c->grid_cache) / sizeof(c->grid_cache[0])))
         return fail(c, RT_ERR_ARG, "unknown traversal kind");
     if (!c->grid_cache[key]) {
         int b = 0;
-        const int e = rt_tris_grid_blocks(c->device, trav, count, &b);
+        const int e = rt_tris_grid_blocks(c->device, trav, count, defer, &b);
         if (e) return hip_fail(c, (hipError_t)e, "occupancy query");
         c->grid_cache[key] = b;
     }
@@ -956,9 +956,11 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.counters = c->d_counters;
         const int trav = trav_kind(c);
         int blocks = 0;
-        const int r = grid_blocks(c, trav, c->counting, &blocks);
+        const int r = grid_blocks(c, trav, c->counting, false, &blocks);
         if (r != RT_OK) return r;
         const uint64_t items = (uint64_t)((W + 7) / 8) * ((hl + 7) / 8) * 64;
+        if (const char *v = getenv("RT_GRID_PCT")) /* A/B knob: persistent grid as a share of full occupancy */
+            blocks = std::max(1, blocks * std::max(1, std::min(100, atoi(v))) / 100);
         blocks = (int)std::min<uint64_t>((uint64_t)blocks, (items + RT_BLOCK - 1) / RT_BLOCK);
         if (blocks < 1) blocks = 1;
         a.spill_cap = spill_cap(c);
@@ -991,6 +993,11 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 a.defer_qcount = c->d_defer_qcount;
                 a.defer_pixel = c->d_defer_pixel;
                 HIPCHK(c, hipMemsetAsync(c->d_defer_qcount, 0, 2 * sizeof(uint32_t), st));
+                /* the deferred form's own occupancy (RT_TRIS_WAVES_DEFER) */
+                int bd = 0;
+                const int rd = grid_blocks(c, trav, c->counting, true, &bd);
+                if (rd != RT_OK) return rd;
+                blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)bd, (items + RT_BLOCK - 1) / RT_BLOCK));
             }
         }
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));

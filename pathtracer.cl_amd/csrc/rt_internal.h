@@ -36,6 +36,12 @@
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif
+#ifndef RT_TRIS_WAVES_DEFER
+/* the deferred-shadow form runs tiles, whose time is the serial chains of their box pixels:
+   4 waves per SIMD leave it 120 VGPRs and no spill reloads in the path advance (8-way tiles
+   36.5 -> 33.2 ms; a whole frame, throughput-bound, prefers 5: 129.2 vs 131.3 ms) */
+#define RT_TRIS_WAVES_DEFER 4
+#endif
 #ifndef RT_SHADOW_REDO
 #define RT_SHADOW_REDO 1 /* k_tris: shadow rays answered without traversal are consumed in the same D pass (-3.9 %) */
 #endif
@@ -197,6 +203,6 @@ int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, v
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,
                         uint32_t *buf, bool unpack, void *stream);
 /* Persistent-grid size for the triangle kernel on this device. */
-int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks);
+int rt_tris_grid_blocks(int device, int trav, bool count, bool defer, int *blocks);
 
 #endif /* RT_INTERNAL_H */

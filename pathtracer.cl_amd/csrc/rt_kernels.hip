@@ -587,7 +587,7 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         wave's longest query ends.  LINEAR: each query runs to completion inside
         the iteration (the reference loop, wave-uniform). */
 template <int TRAV, bool COUNT, bool DEFER>
-__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
+__global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
     constexpr bool RESUME = TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
@@ -1754,16 +1754,22 @@ int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris,
     return (int)hipGetLastError();
 }
 
-int rt_tris_grid_blocks(int device, int trav, bool count, int *blocks)
+int rt_tris_grid_blocks(int device, int trav, bool count, bool defer, int *blocks)
 {
     int per_cu = 0;
     int e;
     if (trav == RT_TRAV_LINEAR)
         e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true, false>, &per_cu)
                   : occupancy(k_tris<RT_TRAV_LINEAR, false, false>, &per_cu);
-    else if (trav == RT_TRAV_BVH4Q) /* the deferred form has the same launch bounds */
+    else if (trav == RT_TRAV_BVH4Q && defer)
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true, true>, &per_cu)
+                  : occupancy(k_tris<RT_TRAV_BVH4Q, false, true>, &per_cu);
+    else if (trav == RT_TRAV_BVH4Q)
         e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true, false>, &per_cu)
                   : occupancy(k_tris<RT_TRAV_BVH4Q, false, false>, &per_cu);
+    else if (defer)
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true, true>, &per_cu)
+                  : occupancy(k_tris<RT_TRAV_BVH4, false, true>, &per_cu);
     else
         e = count ? occupancy(k_tris<RT_TRAV_BVH4, true, false>, &per_cu)
                   : occupancy(k_tris<RT_TRAV_BVH4, false, false>, &per_cu);

@@ -44,11 +44,19 @@ def main():
         s = np.fromfile(dump, np.uint32).reshape(rows * W, 8).astype(np.int64)
         dur = ((s[:, 1] - s[:, 0]) & 0xFFFFFFFF) / 1e5
         top = np.argsort(dur)[-4:][::-1]
+        t0 = s[:, 0].min()
+        end = ((s[:, 1] - t0) & 0xFFFFFFFF) / 1e5  # ms after the first pixel started
+        start = ((s[:, 0] - t0) & 0xFFFFFFFF) / 1e5
+        timeline = {f"end_p{q}": round(float(np.percentile(end, q)), 2) for q in (50, 90, 99, 99.9, 100)}
+        timeline["costliest_start_ms"] = [round(float(start[i]), 2) for i in top]
         print(json.dumps({name: {"kernel_ms": round(ms, 2), "pixels_deferred": cn["pixels_deferred"],
                                  "steps_per_query": round((cn["nodes_visited"] + cn["leaves_visited"]) /
                                                           max(cn["rays_closest"] + cn["rays_shadow"], 1), 2),
+                                 "timeline": timeline,
                                  "costliest": [{"px": [int(i % W), int(i // W)], "wall_ms": round(float(dur[i]), 2),
-                                                "queries": int(s[i, 2]), "steps": int(s[i, 3])} for i in top]}}),
+                                                "queries": int(s[i, 2]), "steps": int(s[i, 3]),
+                                                "shade_refill_step": [round(float(s[i, k]) / max(float(s[i, 4] + s[i, 5] + s[i, 6]), 1.0), 3) for k in (4, 5, 6)],
+                                                "iterations": int(s[i, 7])} for i in top]}}),
               flush=True)
 
 

@@ -37,7 +37,7 @@ def main():
             b = min(b, rt.lastKernelMs())
         return b
 
-    res = {"env": {k: os.environ.get(k) for k in ("RT_FETCH_FRAC", "RT_BOX_EXIT", "RT_FETCH_K", "RT_FETCH_K_BOX", "RT_DEFER", "RT_SPREAD", "RT_PIXEL_LISTS")}}
+    res = {"env": {k: os.environ.get(k) for k in ("RT_FETCH_FRAC", "RT_BOX_EXIT", "RT_FETCH_K", "RT_FETCH_K_BOX", "RT_DEFER", "RT_SPREAD", "RT_PIXEL_LISTS", "RT_GRID_PCT")}}
     seeds0 = None
     rt.rayTrace(out, W, H, 0, kernel=2)
     seeds0 = rt.getSeeds()

@@ -1039,6 +1039,20 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         e = lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr, c->d_lists,
                                           st)
                   : 0;
+        if (!e && lists && getenv("RT_LIST_STATS")) { /* diagnostics: candidate list lengths */
+            std::vector<uint8_t> h((size_t)W * hl);
+            HIPCHK(c, hipMemcpyAsync(h.data(), c->d_lists, h.size(), hipMemcpyDeviceToHost, st));
+            HIPCHK(c, hipStreamSynchronize(st));
+            uint64_t b[6] = {}, sum = 0, nl = 0;
+            for (uint8_t v : h) {
+                b[v == 0 ? 0 : v <= 8 ? 1 : v <= 16 ? 2 : v <= 24 ? 3 : v <= 32 ? 4 : 5]++;
+                if (v <= RT_LIST_MAX) sum += v, nl++;
+            }
+            fprintf(stderr, "lists: 0:%llu 1-8:%llu 9-16:%llu 17-24:%llu 25-32:%llu none:%llu mean %.2f\n",
+                    (unsigned long long)b[0], (unsigned long long)b[1], (unsigned long long)b[2],
+                    (unsigned long long)b[3], (unsigned long long)b[4], (unsigned long long)b[5],
+                    nl ? (double)sum / (double)nl : 0.0);
+        }
         if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
         if (!e && a.n_defer) e = rt_launch_defer(a, c->counting, blocks, st);
         c->last_deferred = a.n_defer;

@@ -284,6 +284,9 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 }
             }
         }
+        /* a camera candidate list (k_pixel_lists) is sorted, r1.w = the next candidate's
+           earliest accept t: past the best hit, nothing later can be accepted (tree leaves: 0) */
+        if (!any_hit && s.best_t < __uint_as_float(q1.w)) return true;
         if (enc & 7u) { /* next triangle of this leaf */
             s.node = ~(int)((((enc >> 3) + 1u) << 3) | ((enc & 7u) - 1u));
             return false;
@@ -980,13 +983,13 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                         } else if (pc <= RT_LIST_MAX) {
                             /* the candidates as virtual leaves of up to 8: the first is stepped
                                now, the others wait on the (empty) stack */
+                            /* pushed last block first: the blocks pop in list order (the
+                               sorted list's early end relies on it) */
                             const uint32_t k0 = pc < 8u ? pc : 8u;
                             ts.node = ~(int)((first << 3) | (k0 - 1u));
-                            for (uint32_t rem = pc - k0; rem > 0;) {
-                                first += 8u;
-                                const uint32_t k = rem < 8u ? rem : 8u;
-                                stk.push(~(int)((first << 3) | (k - 1u)));
-                                rem -= k;
+                            for (uint32_t b = (pc - 1u) >> 3; b > 0; --b) {
+                                const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
+                                stk.push(~(int)(((first + 8u * b) << 3) | (k - 1u)));
                             }
                         }
                     }
@@ -1500,7 +1503,8 @@ __global__ __launch_bounds__(64) void k_defer_finish(RtTriLaunch a)
    records, so the same closest hit), and an empty list answers "no mesh hit" outright.  Pixels
    with more candidates (or a stack overflow) keep the BVH. */
 __device__ __forceinline__ bool frustum_slab(const double olo[3], const double ohi[3], const double dlo[3],
-                                             const double dhi[3], const double lo[3], const double hi[3], double tmax)
+                                             const double dhi[3], const double lo[3], const double hi[3], double tmax,
+                                             double *tin_out = nullptr)
 {
     /* rays o + t d with o in [olo, ohi], d in [dlo, dhi]: per axis (P - o) / d is monotonic in
        o and in d (d of one sign), so its range is spanned by the four corner quotients */
@@ -1523,6 +1527,7 @@ __device__ __forceinline__ bool frustum_slab(const double olo[3], const double o
         tout = fmin(tout, fmax(fmax(f1, f2), fmax(f3, f4)));
     }
     tin = fmax(tin, -1e-3); /* accepted hits have t > tmin > 0 */
+    if (tin_out) *tin_out = tin;
     return tin <= tout && tin <= tmax;
 }
 
@@ -1598,6 +1603,25 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
     uint32_t n = 0;
     const bool ok = frustum_list(nodes4, q4, tris, o, o, dlo, dhi, l1, 1e300, lst, RT_LIST_MAX, n);
     counts[p] = ok ? (uint8_t)n : (uint8_t)RT_LIST_NONE;
+    if (!ok || n < 2) {
+        if (ok && n == 1) lst[1].w = kInf;
+        return;
+    }
+    /* Sorted by earliest accept t; each record's r1.w then carries the NEXT record's bound
+       (+inf on the last): a closest-hit query whose best t is already below it has its answer
+       (trav_step_q ends the list there — the accept rule needs t < best_t, or t == best_t). */
+    float key[RT_LIST_MAX];
+    for (uint32_t i = 0; i < n; ++i) key[i] = lst[3 * i + 1].w;
+    float4 buf[3 * RT_LIST_MAX];
+    for (uint32_t i = 0; i < 3 * n; ++i) buf[i] = lst[i];
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t r = 0;
+        for (uint32_t j = 0; j < n; ++j) r += (key[j] < key[i] || (key[j] == key[i] && j < i)) ? 1u : 0u;
+        lst[3 * r] = buf[3 * i];
+        lst[3 * r + 1] = buf[3 * i + 1];
+        lst[3 * r + 2] = buf[3 * i + 2];
+    }
+    for (uint32_t r = 0; r < n; ++r) lst[3 * r + 1].w = r + 1 < n ? lst[3 * (r + 1) + 1].w : kInf;
 }
 
 /* Conservative traversal for k_pixel_lists: every triangle some ray o + t d (o in [olo, ohi],
@@ -1641,9 +1665,9 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
             for (int j = 0; j < cnt; ++j) {
                 const int s = first + j;
                 const float4 r0 = tris[3 * s], r1 = tris[3 * s + 1], r2 = tris[3 * s + 2];
-                double lo[3], hi[3], nmax;
+                double lo[3], hi[3], nmax, tin;
                 tri_padded_box(r0, r1, r2, lo, hi, nmax);
-                if (!frustum_slab(olo, ohi, dlo, dhi, lo, hi, tmax)) continue;
+                if (!frustum_slab(olo, ohi, dlo, dhi, lo, hi, tmax, &tin)) continue;
                 const double e1[3] = {r1.x, r1.y, r1.z}, e2[3] = {r2.x, r2.y, r2.z};
                 const double nv[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
                                       e2[0] * e1[1] - e2[1] * e1[0]};
@@ -1653,8 +1677,19 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                     ok = false;
                     break;
                 }
+                /* the earliest t any ray could accept this triangle at: the box entry less the
+                   error of the float t (relative ~gamma |e1| |e2| |d| / |det|, |det| >= 1e-4;
+                   30x margin), at the farthest t the box allows; kept in the spare r1.w */
+                double tf2 = 0.0;
+                for (int k = 0; k < 3; ++k) {
+                    const double u = fmax(fabs(lo[k] - olo[k]), fabs(hi[k] - olo[k]));
+                    tf2 += u * u;
+                }
+                const double le1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+                const double le2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+                const double terr = sqrt(tf2) * (2e-6 * le1 * le2 * l1 / 1e-4 + 1e-6) * l1 + 1e-5;
                 lst[3 * n] = r0;
-                lst[3 * n + 1] = r1;
+                lst[3 * n + 1] = make_float4(r1.x, r1.y, r1.z, __double2float_rd(tin - terr));
                 lst[3 * n + 2] = r2;
                 ++n;
             }

@@ -36,6 +36,7 @@ static long g_node_steps, g_tri_steps; /* of all queries */
 static long g_near[2], g_far[2];         /* shadow-query steps entered within / beyond t = 0.05 (node, tri) */
 static bool g_track;
 static bool g_from_mesh; /* the shadow query leaves a mesh hit */
+static float g_tmin_shadow = -1e-3f; /* experiment: node-cull tmin of shadow rays leaving the mesh */
 static double g_occ[2], g_occ_steps[2]; /* camera-hit shadow queries: unoccluded / occluded, and their steps */
 static int g_order = 0; /* 0 sorted push, 1 nearest first only, 2 sorted with any-hit origin boxes last, 3 and those by segment length, 5 = 3 for shadow rays leaving the mesh else 2 (k_tris) */
 /* per 4-wide node: box of the unnormalised normals e2 x e1 of its subtree's triangles (det cull) */
@@ -149,7 +150,8 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
                 float tx0 = (f[0 + i] - o.x) * inv.x, tx1 = (f[4 + i] - o.x) * inv.x;
                 float ty0 = (f[8 + i] - o.y) * inv.y, ty1 = (f[12 + i] - o.y) * inv.y;
                 float tz0 = (f[16 + i] - o.z) * inv.z, tz1 = (f[20 + i] - o.z) * inv.z;
-                float tn = std::max(std::max(std::min(tx0, tx1), std::min(ty0, ty1)), std::max(std::min(tz0, tz1), -1e-3f));
+                float tn = std::max(std::max(std::min(tx0, tx1), std::min(ty0, ty1)),
+                                    std::max(std::min(tz0, tz1), any && g_from_mesh ? g_tmin_shadow : -1e-3f));
                 float tf = std::min(std::min(std::max(tx0, tx1), std::max(ty0, ty1)),
                                     std::min(std::max(tz0, tz1), best * 1.0009765625f + 1e-4f));
                 if (!(tn <= tf)) continue;
@@ -254,6 +256,7 @@ int main(int argc, char **argv)
     build_nbox(0);
     g_det_cull = argc > 4 ? atoi(argv[4]) : 0;
     g_order = argc > 5 ? atoi(argv[5]) : 0;
+    if (argc > 6) g_tmin_shadow = (float)atof(argv[6]);
     float cam[16];
     rt_camera_spherical(0, -4, 0, 40, 105, 5, 53, W, reinterpret_cast<rt_camera *>(cam));
     const V view{cam[0], cam[1], cam[2]}, up{cam[4], cam[5], cam[6]}, right{cam[8], cam[9], cam[10]},

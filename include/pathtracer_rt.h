@@ -190,6 +190,10 @@ int rt_get_counters(const rt_ctx *ctx, rt_counters *out); /* of the last complet
 int rt_set_counting(rt_ctx *ctx, int enable);             /* count nodes/tris in the next renders */
 /* Device time of the last render's kernel (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(const rt_ctx *ctx, float *ms);
+/* The same time split at the start of the main path kernel: the camera-ray candidate-list
+   pre-pass of a triangle render (0 without one), then k_tris (+ the deferred-shadow
+   kernels), ms. */
+int rt_last_kernel_split_ms(const rt_ctx *ctx, float *prepass_ms, float *main_ms);
 
 /* ---- ray queries for hit-index parity (rtcommon.h:39-52 / :59-68 semantics).
    Host arrays; any_hit=0: out_idx = closest triangle (-1 none), out_t = its t;

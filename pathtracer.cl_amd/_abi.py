@@ -143,6 +143,7 @@ SIGNATURES = {
     "rt_get_counters": (_i32, [_vp, ctypes.POINTER(RtCounters)]),
     "rt_set_counting": (_i32, [_vp, _i32]),
     "rt_last_kernel_ms": (_i32, [_vp, ctypes.POINTER(_f32)]),
+    "rt_last_kernel_split_ms": (_i32, [_vp, ctypes.POINTER(_f32), ctypes.POINTER(_f32)]),
     "rt_trace_rays": (_i32, [_vp, _vp, _u32, _i32, _vp, _vp]),
     "rt_mesh_vertex_count": (_u32, [_u32]),
     "rt_make_mesh": (_i32, [_u32, _f32, _f32, _f32, _f32, _vp, _vp]),

@@ -68,7 +68,7 @@ constexpr double kPi = 3.14159265358979323846; /* M_PI */
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evm = nullptr; /* evm: the main kernel's start */
     std::string err;
 
     /* scene */
@@ -85,7 +85,8 @@ struct rt_ctx {
     size_t tris_cap = 0;       /* triangle records d_tris holds (mesh + camera-ray candidate lists) */
     uint8_t *d_lists = nullptr; /* candidate count per pixel (k_pixel_lists) */
     size_t lists_bytes = 0;
-    bool pixel_lists = true;   /* RT_PIXEL_LISTS=0: camera rays always traverse the BVH */
+    int pixel_lists = -1; /* RT_PIXEL_LISTS: 0 off, 1 on, unset: on for sampleRate >= 4 (the pre-pass
+                             costs about a traversal per pixel: a 1-spp frame does not repay it) */
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
@@ -577,10 +578,11 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_FETCH_FRAC")) c->fetch_frac = (uint32_t)std::max(0, std::min(64, atoi(v)));
     if (const char *v = getenv("RT_BOX_EXIT")) c->box_exit = atoi(v) != 0;
     if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0; /* A/B knob */
-    if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0; /* A/B knob */
+    if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0; /* A/B knob */
     if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->evm) != hipSuccess ||
         hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_HIP;
@@ -618,6 +620,7 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->evm) (void)hipEventDestroy(c->evm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
@@ -1021,7 +1024,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         const uint64_t kept = c->n_tris;
         a.list_base = (uint32_t)kept;
         const uint64_t list_recs = (uint64_t)W * hl * RT_LIST_MAX;
-        const bool lists = c->pixel_lists && bvh4 && kept + list_recs < (1ull << 28);
+        const bool lists = (c->pixel_lists == 1 || (c->pixel_lists < 0 && c->sample_rate >= 4)) && bvh4 &&
+                           kept + list_recs < (1ull << 28);
         if (lists) {
             const int r = ensure_tris_capacity(c, (size_t)(kept + list_recs), kept, st);
             if (r != RT_OK) return r;
@@ -1039,6 +1043,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         e = lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr, c->d_lists,
                                           st)
                   : 0;
+        HIPCHK(c, hipEventRecord(c->evm, st));
         if (!e && lists && getenv("RT_LIST_STATS")) { /* diagnostics: candidate list lengths */
             std::vector<uint8_t> h((size_t)W * hl);
             HIPCHK(c, hipMemcpyAsync(h.data(), c->d_lists, h.size(), hipMemcpyDeviceToHost, st));
@@ -1087,6 +1092,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.rank = rk;
         a.counters = c->d_counters;
         HIPCHK(c, hipEventRecord(c->ev0, st));
+        HIPCHK(c, hipEventRecord(c->evm, st));
         e = rt_launch_spheres(a, kernel == RT_KERNEL_SPHERES_SS, st);
         HIPCHK(c, hipEventRecord(c->ev1, st));
     }
@@ -1203,6 +1209,15 @@ int rt_set_counting(rt_ctx *c, int enable)
     return RT_OK;
 }
 
+int rt_last_kernel_split_ms(const rt_ctx *c, float *prepass_ms, float *main_ms)
+{
+    if (!c || !prepass_ms || !main_ms) return RT_ERR_ARG;
+    if (!c->have_timing) return RT_ERR_STATE;
+    if (hipEventSynchronize(c->ev1) != hipSuccess) return RT_ERR_HIP;
+    if (hipEventElapsedTime(prepass_ms, c->ev0, c->evm) != hipSuccess) return RT_ERR_HIP;
+    return hipEventElapsedTime(main_ms, c->evm, c->ev1) == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
 int rt_last_kernel_ms(const rt_ctx *c, float *ms)
 {
     if (!c || !ms) return RT_ERR_ARG;
@@ -1238,6 +1253,7 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
         }
     }
     if (e == hipSuccess) e = hipEventRecord(c->ev0, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(c->evm, c->stream);
     if (e == hipSuccess) {
         /* The tree leaves out triangles no UNIT-length ray can hit (rt_bvh.cpp never_hit); the
            kernels only trace unit directions, but a caller's rays may be longer: then the

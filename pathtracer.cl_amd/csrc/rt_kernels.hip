@@ -1502,33 +1502,53 @@ __global__ __launch_bounds__(64) void k_defer_finish(RtTriLaunch a)
    query by testing only them (a virtual leaf: the same tests and accept rule on the same
    records, so the same closest hit), and an empty list answers "no mesh hit" outright.  Pixels
    with more candidates (or a stack overflow) keep the BVH. */
-__device__ __forceinline__ bool frustum_slab(const double olo[3], const double ohi[3], const double dlo[3],
-                                             const double dhi[3], const double lo[3], const double hi[3], double tmax,
+struct Frustum {
+    double olo[3], ohi[3]; /* ray origins */
+    double dlo[3], dhi[3]; /* ray directions (component-wise interval) */
+    double ilo[3], ihi[3]; /* 1 / dlo, 1 / dhi (axes where d keeps one sign) */
+    double l1;             /* max |d|_1 */
+    double tmax;           /* farthest t of interest */
+};
+
+__device__ __forceinline__ void frustum_init(Frustum &f)
+{
+    f.l1 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        f.ilo[k] = 1.0 / f.dlo[k];
+        f.ihi[k] = 1.0 / f.dhi[k];
+        f.l1 += fmax(fabs(f.dlo[k]), fabs(f.dhi[k]));
+    }
+}
+
+__device__ __forceinline__ bool frustum_slab(const Frustum &f, const double lo[3], const double hi[3],
                                              double *tin_out = nullptr)
 {
     /* rays o + t d with o in [olo, ohi], d in [dlo, dhi]: per axis (P - o) / d is monotonic in
-       o and in d (d of one sign), so its range is spanned by the four corner quotients */
+       o and in d (d of one sign), so its range is spanned by the four corner quotients (as
+       products with the reciprocals: a relative 1e-16 against boxes padded by 1e-6 and more) */
+    const double *olo = f.olo, *ohi = f.ohi;
     double tin = -1e300, tout = 1e300;
     for (int k = 0; k < 3; ++k) {
-        const double a = dlo[k], b = dhi[k];
+        const double a = f.dlo[k], b = f.dhi[k];
         if (!(a > 0.0 || b < 0.0)) {
             /* d straddles 0 on this axis: at t >= 0 the rays' coordinate spans
                [olo + t a, ohi + t b], which must reach [lo, hi] (a lower bound on t) */
-            if (a < 0.0) tin = fmax(tin, (hi[k] - olo[k]) / a);
+            if (a < 0.0) tin = fmax(tin, (hi[k] - olo[k]) * f.ilo[k]);
             else if (olo[k] > hi[k]) return false;
-            if (b > 0.0) tin = fmax(tin, (lo[k] - ohi[k]) / b);
+            if (b > 0.0) tin = fmax(tin, (lo[k] - ohi[k]) * f.ihi[k]);
             else if (ohi[k] < lo[k]) return false;
             continue;
         }
         const double ne = a > 0.0 ? lo[k] : hi[k], fa = a > 0.0 ? hi[k] : lo[k];
-        const double n1 = (ne - olo[k]) / a, n2 = (ne - olo[k]) / b, n3 = (ne - ohi[k]) / a, n4 = (ne - ohi[k]) / b;
-        const double f1 = (fa - olo[k]) / a, f2 = (fa - olo[k]) / b, f3 = (fa - ohi[k]) / a, f4 = (fa - ohi[k]) / b;
+        const double ia = f.ilo[k], ib = f.ihi[k];
+        const double n1 = (ne - olo[k]) * ia, n2 = (ne - olo[k]) * ib, n3 = (ne - ohi[k]) * ia, n4 = (ne - ohi[k]) * ib;
+        const double f1 = (fa - olo[k]) * ia, f2 = (fa - olo[k]) * ib, f3 = (fa - ohi[k]) * ia, f4 = (fa - ohi[k]) * ib;
         tin = fmax(tin, fmin(fmin(n1, n2), fmin(n3, n4)));
         tout = fmin(tout, fmax(fmax(f1, f2), fmax(f3, f4)));
     }
     tin = fmax(tin, -1e-3); /* accepted hits have t > tmin > 0 */
     if (tin_out) *tin_out = tin;
-    return tin <= tout && tin <= tmax;
+    return tin <= tout && tin <= f.tmax;
 }
 
 /* max over the direction box of |d . n| for n in [nlo, nhi] */
@@ -1570,9 +1590,8 @@ __device__ __forceinline__ void tri_padded_box(float4 r0, float4 r1, float4 r2, 
 }
 
 __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *__restrict__ q4,
-                             const float4 *__restrict__ tris, const double olo[3], const double ohi[3],
-                             const double dlo[3], const double dhi[3], double l1, double tmax, float4 *lst, uint32_t cap,
-                             uint32_t &n);
+                             const float4 *__restrict__ tris, const Frustum &f, int *slots, float *keys,
+                             uint32_t cap, uint32_t &n);
 
 __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const float *__restrict__ nodes4,
                                                           const uint32_t *__restrict__ q4, uint8_t *__restrict__ counts)
@@ -1591,47 +1610,51 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
             dhi[k] = fmax(dhi[k], dv[k]);
         }
     }
-    double l1 = 0.0;
+    Frustum f;
     for (int k = 0; k < 3; ++k) {
-        dlo[k] -= 1e-5;
-        dhi[k] += 1e-5;
-        l1 += fmax(fabs(dlo[k]), fabs(dhi[k]));
+        f.dlo[k] = dlo[k] - 1e-5;
+        f.dhi[k] = dhi[k] + 1e-5;
+        f.olo[k] = f.ohi[k] = k == 0 ? a.cam.position.x : k == 1 ? a.cam.position.y : a.cam.position.z;
     }
-    const double o[3] = {a.cam.position.x, a.cam.position.y, a.cam.position.z};
+    f.tmax = 1e300;
+    frustum_init(f);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
     float4 *__restrict__ lst = const_cast<float4 *>(tris) + 3ull * (a.list_base + (size_t)p * RT_LIST_MAX);
-    uint32_t n = 0;
-    const bool ok = frustum_list(nodes4, q4, tris, o, o, dlo, dhi, l1, 1e300, lst, RT_LIST_MAX, n);
-    counts[p] = ok ? (uint8_t)n : (uint8_t)RT_LIST_NONE;
-    if (!ok || n < 2) {
-        if (ok && n == 1) lst[1].w = kInf;
-        return;
-    }
-    /* Sorted by earliest accept t; each record's r1.w then carries the NEXT record's bound
-       (+inf on the last): a closest-hit query whose best t is already below it has its answer
-       (trav_step_q ends the list there — the accept rule needs t < best_t, or t == best_t). */
+    int slot[RT_LIST_MAX];
     float key[RT_LIST_MAX];
-    for (uint32_t i = 0; i < n; ++i) key[i] = lst[3 * i + 1].w;
-    float4 buf[3 * RT_LIST_MAX];
-    for (uint32_t i = 0; i < 3 * n; ++i) buf[i] = lst[i];
+    uint32_t n = 0;
+    const bool ok = frustum_list(nodes4, q4, tris, f, slot, key, RT_LIST_MAX, n);
+    counts[p] = ok ? (uint8_t)n : (uint8_t)RT_LIST_NONE;
+    if (!ok) return;
+    /* The records in order of their earliest accept t, each one's r1.w carrying the NEXT
+       record's bound (+inf on the last): a closest-hit query whose best t is already below
+       it has its answer (trav_step_q ends the list there — the accept rule needs t < best_t,
+       or t == best_t). */
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t r = 0;
-        for (uint32_t j = 0; j < n; ++j) r += (key[j] < key[i] || (key[j] == key[i] && j < i)) ? 1u : 0u;
-        lst[3 * r] = buf[3 * i];
-        lst[3 * r + 1] = buf[3 * i + 1];
-        lst[3 * r + 2] = buf[3 * i + 2];
+        float next = kInf;
+        for (uint32_t j = 0; j < n; ++j) {
+            const bool before = key[j] < key[i] || (key[j] == key[i] && j < i);
+            r += before ? 1u : 0u;
+            if (!before && j != i) next = fminf(next, key[j]);
+        }
+        const int s = slot[i];
+        const float4 e1 = tris[3 * s + 1];
+        lst[3 * r] = tris[3 * s];
+        lst[3 * r + 1] = make_float4(e1.x, e1.y, e1.z, next);
+        lst[3 * r + 2] = tris[3 * s + 2];
     }
-    for (uint32_t r = 0; r < n; ++r) lst[3 * r + 1].w = r + 1 < n ? lst[3 * (r + 1) + 1].w : kInf;
 }
 
-/* Conservative traversal for k_pixel_lists: every triangle some ray o + t d (o in [olo, ohi],
-   d in [dlo, dhi], t <= tmax) could accept under intersects_triangle's tests is copied to
-   `lst` (`cap` at most: false on overflow). */
+/* Conservative traversal for k_pixel_lists: every triangle some ray o + t d of the frustum
+   could accept under intersects_triangle's tests is listed (`cap` at most: false on
+   overflow): its slot, and the earliest t of such an accept. */
 __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *__restrict__ q4,
-                             const float4 *__restrict__ tris, const double olo[3], const double ohi[3],
-                             const double dlo[3], const double dhi[3], double l1, double tmax, float4 *lst, uint32_t cap,
-                             uint32_t &n)
+                             const float4 *__restrict__ tris, const Frustum &fr, int *slots, float *keys,
+                             uint32_t cap, uint32_t &n)
 {
+    const double *dlo = fr.dlo, *dhi = fr.dhi, *olo = fr.olo;
+    const double l1 = fr.l1;
     int stack[64];
     int sp = 0, node = 0;
     n = 0;
@@ -1642,7 +1665,7 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
             const int c = __float_as_int(f[24 + k]);
             if (c == RT_EMPTY_CHILD) continue;
             const double lo[3] = {f[0 + k], f[8 + k], f[16 + k]}, hi[3] = {f[4 + k], f[12 + k], f[20 + k]};
-            if (!frustum_slab(olo, ohi, dlo, dhi, lo, hi, tmax)) continue;
+            if (!frustum_slab(fr, lo, hi)) continue;
             if (c >= 0) {
                 if (q4) { /* the child's normal box (determinant cull) */
                     const uint32_t wl = q4[(size_t)RT_QNODE_DWORDS * (uint32_t)c + 10];
@@ -1667,7 +1690,7 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                 const float4 r0 = tris[3 * s], r1 = tris[3 * s + 1], r2 = tris[3 * s + 2];
                 double lo[3], hi[3], nmax, tin;
                 tri_padded_box(r0, r1, r2, lo, hi, nmax);
-                if (!frustum_slab(olo, ohi, dlo, dhi, lo, hi, tmax, &tin)) continue;
+                if (!frustum_slab(fr, lo, hi, &tin)) continue;
                 const double e1[3] = {r1.x, r1.y, r1.z}, e2[3] = {r2.x, r2.y, r2.z};
                 const double nv[3] = {e2[1] * e1[2] - e2[2] * e1[1], e2[2] * e1[0] - e2[0] * e1[2],
                                       e2[0] * e1[1] - e2[1] * e1[0]};
@@ -1688,9 +1711,8 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                 const double le1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
                 const double le2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
                 const double terr = sqrt(tf2) * (2e-6 * le1 * le2 * l1 / 1e-4 + 1e-6) * l1 + 1e-5;
-                lst[3 * n] = r0;
-                lst[3 * n + 1] = make_float4(r1.x, r1.y, r1.z, __double2float_rd(tin - terr));
-                lst[3 * n + 2] = r2;
+                slots[n] = s;
+                keys[n] = __double2float_rd(tin - terr);
                 ++n;
             }
         }

@@ -248,6 +248,13 @@ class RayTracer:
         self._check(self._lib.rt_last_kernel_ms(self._h, ctypes.byref(ms)), "rt_last_kernel_ms")
         return ms.value
 
+    def lastKernelSplitMs(self) -> tuple[float, float]:
+        """(candidate-list pre-pass, main kernel) device times of the last render, ms."""
+        pre, main = ctypes.c_float(), ctypes.c_float()
+        self._check(self._lib.rt_last_kernel_split_ms(self._h, ctypes.byref(pre), ctypes.byref(main)),
+                    "rt_last_kernel_split_ms")
+        return pre.value, main.value
+
     def traceRays(self, rays: np.ndarray, any_hit: bool = False) -> tuple[np.ndarray, np.ndarray]:
         r = np.ascontiguousarray(rays, _abi.RAY_DTYPE)
         idx = np.empty(r.size, np.int32)

@@ -808,6 +808,36 @@ def test_ply_mesh_cli_and_oracle(tracer, pt, oracle, tmp_path):
     np.testing.assert_array_equal(bits(got_cli), bits(exp))
 
 
+@pytest.mark.parametrize("n_tris,sr", [(2000, 1), (20_000, 2)])
+def test_pixel_candidate_lists_vs_oracle(pt, oracle, monkeypatch, n_tris, sr):
+    """Camera rays answered from the per-pixel candidate lists (k_pixel_lists: sorted, the
+    early end on the next candidate's earliest accept t, blocks popped in list order) equal
+    the oracle's linear loop bit for bit, lists forced on (RT_PIXEL_LISTS=1) at sample rates
+    the automatic rule leaves them off for, and off; meshes whose pixels hold 1-32 candidates
+    (the 2,000-triangle mesh: large triangles, many lists over 8)."""
+    sc = pt.scenes
+    W, H = 64, 48
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(n_tris)
+    seeds = sc.default_seeds(Wp, Hp, skip=3)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    exp = np.zeros(W * H * 4, np.float32)
+    oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, sr, 6, 0, seeds.copy(), verts, idx)  # advances its seeds
+    for mode in ("1", "0"):
+        monkeypatch.setenv("RT_PIXEL_LISTS", mode)
+        rt = pt.RayTracer(0)  # read when the context is created
+        rt.setSpheres(sc.ply_scene())
+        rt.setCamera(cam)
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        got = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(got, W, H, 0, kernel=2)
+        rt.close()
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"RT_PIXEL_LISTS={mode}")
+
+
 # ---- GPU BVH builder (csrc/rt_build_gpu.hip) ----------------------------------------------
 
 @pytest.mark.parametrize("trav", ["bvh", "bvh4f"])
@@ -988,7 +1018,8 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     probe density are scheduling only: a frame with box and mesh pixels, 16 spp, renders to
     the same bits and seeds with the queue row-major (RT_SCHEDULE=0), with the default
     schedule, with other probe / key settings, and with the box pixels' shadow rays traced
-    inline (RT_DEFER=0) or deferred for only the few box pixels 1 MB of slots holds."""
+    inline (RT_DEFER=0) or deferred for only the few box pixels 1 MB of slots holds, and with
+    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0)."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
@@ -996,8 +1027,8 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     seeds = sc.default_seeds(Wp, Hp, skip=7)
     frames = []
     for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_PROBE_N": "1", "RT_LPT_MAX": "0"}, {"RT_PROBE_N": "3"},
-                {"RT_DEFER": "0"}, {"RT_DEFER": "1", "RT_DEFER_MB": "1"}):
-        for k in ("RT_SCHEDULE", "RT_PROBE_N", "RT_LPT_MAX", "RT_DEFER", "RT_DEFER_MB"):
+                {"RT_DEFER": "0"}, {"RT_DEFER": "1", "RT_DEFER_MB": "1"}, {"RT_PIXEL_LISTS": "0"}):
+        for k in ("RT_SCHEDULE", "RT_PROBE_N", "RT_LPT_MAX", "RT_DEFER", "RT_DEFER_MB", "RT_PIXEL_LISTS"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

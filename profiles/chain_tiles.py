@@ -32,7 +32,7 @@ def main():
     rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS["dragon"]))
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     rt.rayTrace(out, W, H, 0, kernel=2)
-    for name, tile in (("full", None), ("n8_r0", (8, 8, 0)), ("n4_r2", (8, 4, 2))):
+    for name, tile in (("full", None), ("n8_r0", (8, 8, 0)), ("n4_r2", (8, 4, 2)), ("row81", (1, H, 81))):
         rows = H if tile is None else len([y for y in range(H) if (y // tile[0]) % tile[1] == tile[2]])
         rt.setCounting(True)
         rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)

@@ -42,6 +42,11 @@ def main():
     rt.rayTrace(out, W, H, 0, kernel=2)
     seeds0 = rt.getSeeds()
     Wp, Hp = sc.padded_dims(W, H)
+    pre = []
+    for _ in range(5):
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        pre.append(rt.lastKernelSplitMs()[0])
+    res["full_prepass_ms"] = round(sorted(pre)[2], 3)
     res["full_ms"] = round(best(None, 3), 2)
     res["row81_ms"] = round(best((1, H, 81)), 2)
     for n in (2, 4, 8):

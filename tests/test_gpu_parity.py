@@ -838,6 +838,33 @@ def test_pixel_candidate_lists_vs_oracle(pt, oracle, monkeypatch, n_tris, sr):
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"RT_PIXEL_LISTS={mode}")
 
 
+def test_kernel_time_split(pt, monkeypatch):
+    """rt_last_kernel_split_ms: a many-sample frame's device time splits into the candidate-list
+    pre-pass and the main kernel, the two adding up to rt_last_kernel_ms; without lists
+    (RT_PIXEL_LISTS=0) the pre-pass part is zero."""
+    sc = pt.scenes
+    W, H = 128, 96
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    for mode, has_pre in (("1", True), ("0", False)):
+        monkeypatch.setenv("RT_PIXEL_LISTS", mode)
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        c = sc.PLY_CAMERA
+        rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+        rt.setSampleRate(4)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, sc.default_seeds(Wp, Hp))
+        out = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        total = rt.lastKernelMs()
+        pre, main = rt.lastKernelSplitMs()
+        rt.close()
+        assert main > 0.0 and abs(pre + main - total) <= 0.01 * total + 1e-3, (pre, main, total)
+        assert (pre > 0.0) if has_pre else (pre < 0.05 * total), (mode, pre, total)
+
+
 # ---- GPU BVH builder (csrc/rt_build_gpu.hip) ----------------------------------------------
 
 @pytest.mark.parametrize("trav", ["bvh", "bvh4f"])

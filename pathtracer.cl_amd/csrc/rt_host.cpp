@@ -391,7 +391,10 @@ int classify_pixels(rt_ctx *c, const std::vector<uint32_t> &f, uint32_t W, uint3
        tile with few pixels per lane) of a many-sample frame, not on a full frame (dragon
        1920x1080: 161.7 -> 173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) nor on short
        chains (bunny class 1024^2 at 1 spp: 0.95 -> 1.35 ms, r02u) */
-    const bool use = c->defer == 1 || (c->defer < 0 && npx < 4 * lanes && c->sample_rate >= 4);
+    /* (r02z, with the candidate lists: the 2-way dragon tile, 1.04M pixels, 65.5 ms deferred
+       against 60.7 inline; the 4-way 39 vs 46 ms, the 8-way 30 vs 44 ms: the line sits below
+       two pixels per resident lane) */
+    const bool use = c->defer == 1 || (c->defer < 0 && npx < 2 * lanes && c->sample_rate >= 4);
     const uint32_t pn2 = c->probe_n * c->probe_n;
     const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
     const uint64_t nl = c->lights.size();

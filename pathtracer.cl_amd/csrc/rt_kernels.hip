@@ -595,6 +595,14 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
     constexpr bool RESUME = TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     __shared__ float s_light[kMaxLights * 8];
+    /* the pixel sum and the path throughput, touched once per sample / segment, live in LDS
+       (6 floats per lane) instead of six registers across the stepping loop */
+    __shared__ float s_state[6 * RT_BLOCK];
+    float *const st_acc = s_state + threadIdx.x, *const st_prop = s_state + 3 * RT_BLOCK + threadIdx.x;
+#define ACC_GET(k) st_acc[(k) * RT_BLOCK]
+#define ACC_SET(k, v) (st_acc[(k) * RT_BLOCK] = (v))
+#define PROP_GET(k) st_prop[(k) * RT_BLOCK]
+#define PROP_SET(k, v) (st_prop[(k) * RT_BLOCK] = (v))
 
     /* emissive spheres: center.xyz, radius, emission.xyz (materials.h:232, rtcommon.h:97-99) */
     const uint32_t n_lights = a.n_lights < (uint32_t)kMaxLights ? a.n_lights : (uint32_t)kMaxLights;
@@ -635,9 +643,7 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
     int mode = M_IDLE;
     uint32_t x = 0, yl = 0; /* pixel column and local row (global row / seed slot derived) */
     Seed seed = {0u, 0u};
-    float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f; /* pixel sum over samples (raytracer.cl:228-230) */
     float col_x = 0.0f, col_y = 0.0f, col_z = 0.0f; /* this path's radiance (trace_path_tri's pixelColor) */
-    V3 prop = v3(1.0f, 1.0f, 1.0f);
     uint32_t sample = 0, depth = 0, light = 0;
     /* the query ray: a path segment (closest hit) or a shadow ray from the offset hit
        point (any hit) — one register set for both, the phases never overlap */
@@ -727,6 +733,7 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
             bool bounce = false;
             if (seg_done) {
                 const float scale = 1.0f * RT_M_1_PI_F;
+                V3 prop = v3(PROP_GET(0), PROP_GET(1), PROP_GET(2));
                 if (tri_hit) { /* rtcommon.h:411-421: no bounce off triangles */
                     col_x += prop.x * direct.x * scale * 0.7f;
                     col_y += prop.y * direct.y * scale * 0.7f;
@@ -739,6 +746,9 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                     col_x += prop.x * direct.x * scale;
                     col_y += prop.y * direct.y * scale;
                     col_z += prop.z * direct.z * scale;
+                    PROP_SET(0, prop.x);
+                    PROP_SET(1, prop.y);
+                    PROP_SET(2, prop.z);
                     qo = hp;
                     bounce = true;
                 }
@@ -787,14 +797,15 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                 }
             }
             if (sample_done) {
-                acc_x += col_x;
-                acc_y += col_y;
-                acc_z += col_z;
+                ACC_SET(0, ACC_GET(0) + col_x);
+                ACC_SET(1, ACC_GET(1) + col_y);
+                ACC_SET(2, ACC_GET(2) + col_z);
                 ++sample;
                 mode = M_NEWSAMPLE;
                 if (sample >= spp) { /* raytracer.cl:234-242 */
                     if (!DEFER || pclass < 0) { /* a deferred pixel's colour is written by k_defer_finish */
                         const float n = (float)spp;
+                        const float acc_x = ACC_GET(0), acc_y = ACC_GET(1), acc_z = ACC_GET(2);
                         float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
                         float4 *dst = out + ((size_t)yl * a.W + x);
                         if (a.progressive > 0) {
@@ -908,7 +919,10 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                             pix_q = pix_steps = 0;
                             pix_d = pix_ab = pix_c = pix_it = 0;
                         }
-                        acc_x = acc_y = acc_z = 0.0f;
+                        ACC_SET(0, 0.0f);
+                        ACC_SET(1, 0.0f);
+                        ACC_SET(2, 0.0f);
+                        const float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
                         sample = 0;
                         /* some of the probe's rays missed the mesh: box paths, long chains */
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
@@ -943,7 +957,9 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
             const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
             qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
             qd = camera_dir(a.cam, fa - hw, fb - hh);
-            prop = v3(1.0f, 1.0f, 1.0f);
+            PROP_SET(0, 1.0f);
+            PROP_SET(1, 1.0f);
+            PROP_SET(2, 1.0f);
             col_x = col_y = col_z = 0.0f;
             depth = 0;
             mode = M_CLOSEST;
@@ -1061,6 +1077,10 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
     if (COUNT) cnt[7] = wave_clock() - t_k0;
     flush_counters(a.counters, cnt, COUNT);
 }
+#undef ACC_GET
+#undef ACC_SET
+#undef PROP_GET
+#undef PROP_SET
 
 /* ======================================================================== */
 /* Sphere kernel: raytrace (SS = false) / raytrace_ss (SS = true)            */

@@ -823,19 +823,20 @@ def test_pixel_candidate_lists_vs_oracle(pt, oracle, monkeypatch, n_tris, sr):
     cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
     exp = np.zeros(W * H * 4, np.float32)
     oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, sr, 6, 0, seeds.copy(), verts, idx)  # advances its seeds
-    for mode in ("1", "0"):
+    for mode, builder in (("1", "host"), ("1", "gpu"), ("0", "host")):
         monkeypatch.setenv("RT_PIXEL_LISTS", mode)
         rt = pt.RayTracer(0)  # read when the context is created
         rt.setSpheres(sc.ply_scene())
         rt.setCamera(cam)
         rt.setSampleRate(sr)
         rt.setMaxPathDepth(6)
+        rt.setBuilder(builder)  # the GPU-built tree: never-culling normal boxes
         rt.setMesh(verts, idx)
         rt.setSeeds(Wp, Hp, seeds)
         got = np.zeros(W * H * 4, np.float32)
         rt.rayTrace(got, W, H, 0, kernel=2)
         rt.close()
-        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"RT_PIXEL_LISTS={mode}")
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"RT_PIXEL_LISTS={mode} {builder}")
 
 
 def test_kernel_time_split(pt, monkeypatch):

@@ -98,8 +98,12 @@ static bool mt(const float *tr, V o, V d, float &t)
 }
 
 /* nearest-first DFS, one record (node or triangle) per step: k_tris's step count */
+static const float *g_bin; /* the host's binary tree (16 floats per node) */
+static int g_wide = 0;      /* > 0: traverse an n-wide collapse of it (query_wide) */
+static long query_wide(V o, V d, float tmax, bool any, float &t_hit, int &hit);
 static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
 {
+    if (g_wide) return query_wide(o, d, tmax, any, t_hit, hit);
     V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
     struct It {
         int c;
@@ -211,6 +215,91 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
     return steps;
 }
 
+/* An n-wide tree collapsed on the fly from the host's binary tree (largest-area inner child
+   expanded first, as rt_bvh.cpp collapses to 4-wide), one step per wide node and per triangle:
+   how many steps an 8-wide layout would save (g_wide = 4 / 8; no determinant cull). */
+static long query_wide(V o, V d, float tmax, bool any, float &t_hit, int &hit)
+{
+    struct E {
+        float lo[3], hi[3];
+        int code;
+    };
+    auto child = [](int node, int side) {
+        const float *n = g_bin + 16 * node;
+        E e;
+        const int b = side ? 4 : 0;
+        e.lo[0] = n[b + 0]; e.hi[0] = n[b + 1]; e.lo[1] = n[b + 2]; e.hi[1] = n[b + 3];
+        e.lo[2] = n[8 + 2 * side]; e.hi[2] = n[9 + 2 * side];
+        memcpy(&e.code, &n[12 + side], 4);
+        return e;
+    };
+    auto area = [](const E &e) {
+        const float x = e.hi[0] - e.lo[0], y = e.hi[1] - e.lo[1], z = e.hi[2] - e.lo[2];
+        return x * y + y * z + z * x;
+    };
+    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    struct It {
+        int c; /* binary node whose children form a wide node (>= 0) or a leaf code (< 0) */
+        float key;
+    };
+    std::vector<It> st{{0, 0.0f}};
+    float best = tmax;
+    hit = -1;
+    long steps = 0;
+    while (!st.empty()) {
+        It it = st.back();
+        st.pop_back();
+        if (it.c >= 0) {
+            ++steps;
+            std::vector<E> k{child(it.c, 0), child(it.c, 1)};
+            while ((int)k.size() < g_wide) {
+                int bi = -1;
+                float ba = -1.0f;
+                for (int i = 0; i < (int)k.size(); ++i)
+                    if (k[i].code >= 0 && area(k[i]) > ba) ba = area(k[i]), bi = i;
+                if (bi < 0) break;
+                const int e = k[bi].code;
+                k[bi] = child(e, 0);
+                k.push_back(child(e, 1));
+            }
+            std::vector<It> buf;
+            for (const E &e : k) {
+                float tx0 = (e.lo[0] - o.x) * inv.x, tx1 = (e.hi[0] - o.x) * inv.x;
+                float ty0 = (e.lo[1] - o.y) * inv.y, ty1 = (e.hi[1] - o.y) * inv.y;
+                float tz0 = (e.lo[2] - o.z) * inv.z, tz1 = (e.hi[2] - o.z) * inv.z;
+                float tn = std::max(std::max(std::min(tx0, tx1), std::min(ty0, ty1)), std::max(std::min(tz0, tz1), -1e-3f));
+                float tf = std::min(std::min(std::max(tx0, tx1), std::max(ty0, ty1)),
+                                    std::min(std::max(tz0, tz1), best * 1.0009765625f + 1e-4f));
+                if (!(tn <= tf)) continue;
+                float key = tn;
+                if (any && g_order >= 2) key = (g_order == 3 || (g_order == 5 && g_from_mesh) ? tn - tf : tn) + (tn <= 0.0f ? 1e4f : 0.0f);
+                buf.push_back({e.code, key});
+            }
+            std::sort(buf.begin(), buf.end(), [](const It &a, const It &b) { return a.key > b.key; });
+            for (const It &b : buf) st.push_back(b);
+        } else {
+            int enc = ~it.c, first = enc >> 3, cnt = (enc & 7) + 1;
+            for (int j = 0; j < cnt; ++j) {
+                ++steps;
+                float t;
+                if (mt(g_tris + 12 * (first + j), o, d, t)) {
+                    if (any) {
+                        if (t > 1e-4f && t < tmax) {
+                            hit = first + j;
+                            return steps;
+                        }
+                    } else if (!(t < 1e-4f) && t < best) {
+                        best = t;
+                        hit = first + j;
+                    }
+                }
+            }
+        }
+    }
+    t_hit = best;
+    return steps;
+}
+
 static float box_hit(V o, V d, V &n)
 {
     const float s[3] = {6.0f, 5.0f, 6.0f};
@@ -257,6 +346,8 @@ int main(int argc, char **argv)
     g_det_cull = argc > 4 ? atoi(argv[4]) : 0;
     g_order = argc > 5 ? atoi(argv[5]) : 0;
     if (argc > 6) g_tmin_shadow = (float)atof(argv[6]);
+    if (argc > 7) g_wide = atoi(argv[7]);
+    g_bin = bvh.nodes.data();
     float cam[16];
     rt_camera_spherical(0, -4, 0, 40, 105, 5, 53, W, reinterpret_cast<rt_camera *>(cam));
     const V view{cam[0], cam[1], cam[2]}, up{cam[4], cam[5], cam[6]}, right{cam[8], cam[9], cam[10]},

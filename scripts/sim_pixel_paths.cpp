@@ -251,6 +251,7 @@ static long query_wide(V o, V d, float tmax, bool any, float &t_hit, int &hit)
         st.pop_back();
         if (it.c >= 0) {
             ++steps;
+            ++g_node_steps;
             std::vector<E> k{child(it.c, 0), child(it.c, 1)};
             while ((int)k.size() < g_wide) {
                 int bi = -1;
@@ -281,6 +282,7 @@ static long query_wide(V o, V d, float tmax, bool any, float &t_hit, int &hit)
             int enc = ~it.c, first = enc >> 3, cnt = (enc & 7) + 1;
             for (int j = 0; j < cnt; ++j) {
                 ++steps;
+                ++g_tri_steps;
                 float t;
                 if (mt(g_tris + 12 * (first + j), o, d, t)) {
                     if (any) {

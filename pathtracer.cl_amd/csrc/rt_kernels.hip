@@ -1606,13 +1606,19 @@ __device__ __forceinline__ void tri_padded_box(float4 r0, float4 r1, float4 r2, 
                 fmax(fabs(e2[2] * e1[0] - e2[0] * e1[2]), fabs(e2[0] * e1[1] - e2[1] * e1[0])));
 }
 
+/* the pre-pass's per-lane traversal stack, in LDS (it was 256 B of scratch per lane): 48 entries
+   cover a 4-wide tree of depth 15 (the dragon needs 35); deeper, the pixel takes the tree */
+constexpr int kFrustumStack = 48;
+
 __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *__restrict__ q4,
-                             const float4 *__restrict__ tris, const Frustum &f, int *slots, float *keys, uint32_t cap, uint32_t &n);
+                             const float4 *__restrict__ tris, const Frustum &f, int *slots, float *keys, uint32_t cap,
+                             uint32_t &n, lds_int *stack);
 
 __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const float *__restrict__ nodes4,
                                                           const uint32_t *__restrict__ q4, uint8_t *__restrict__ counts)
 {
     /* one wave per 8 x 8 pixel tile: neighbouring frusta walk the same nodes */
+    __shared__ int s_fstack[kFrustumStack * RT_BLOCK];
     const uint32_t item = blockIdx.x * RT_BLOCK + threadIdx.x, tiles_x = (a.W + 7u) / 8u;
     const uint32_t tile = item >> 6, in = item & 63u;
     const uint32_t x = (tile % tiles_x) * 8u + (in & 7u), yl = (tile / tiles_x) * 8u + (in >> 3);
@@ -1641,7 +1647,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
     int slot[RT_LIST_MAX];
     float key[RT_LIST_MAX];
     uint32_t n = 0;
-    const bool ok = frustum_list(nodes4, q4, tris, f, slot, key, RT_LIST_MAX, n);
+    const bool ok = frustum_list(nodes4, q4, tris, f, slot, key, RT_LIST_MAX, n,
+                                 (lds_int *)(s_fstack + threadIdx.x));
     counts[p] = ok ? (uint8_t)n : (uint8_t)RT_LIST_NONE;
     if (!ok) return;
     /* The records in order of their earliest accept t, each one's r1.w carrying the NEXT
@@ -1671,11 +1678,10 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
    itself at 109 instead of 164 VGPRs.) */
 __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *__restrict__ q4,
                              const float4 *__restrict__ tris, const Frustum &fr, int *slots, float *keys, uint32_t cap,
-                             uint32_t &n)
+                             uint32_t &n, lds_int *stack)
 {
     const double *dlo = fr.dlo, *dhi = fr.dhi, *olo = fr.o;
     const double l1 = fr.l1;
-    int stack[64];
     int sp = 0, node = 0;
     n = 0;
     bool ok = true;
@@ -1697,11 +1703,11 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                                            ((int)((wh >> 16) & 255u) - 128) * sc};
                     if (frustum_det(dlo, dhi, nlo, nhi) * 1.02 + 5e-7 * l1 < 1e-4) continue;
                 }
-                if (sp >= 64) {
+                if (sp >= kFrustumStack) {
                     ok = false;
                     break;
                 }
-                stack[sp++] = c;
+                stack[RT_BLOCK * sp++] = c;
                 continue;
             }
             const int enc = ~c, first = enc >> 3, cnt = (enc & 7) + 1;
@@ -1737,7 +1743,7 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
             }
         }
         if (!ok || sp == 0) break;
-        node = stack[--sp];
+        node = stack[RT_BLOCK * --sp];
     }
     return ok;
 }

@@ -66,3 +66,20 @@ def test_reference_plymain_replay_equals_oracle(tracer, pt, oracle, tmp_path):
     for p in range(frames):
         oracle.render_spheres(exp, cam, sc.ply_scene(), W, H, Wp, Hp, 1, 6, p, sd)
     np.testing.assert_array_equal(bits(got), bits(exp))
+
+
+def test_gl_pbo_adapter_builds_and_fails_loudly_without_gpu(pt):
+    """f3, the display side of GlutCLWindow::rayTrace (GlutCLWindow.cpp:190-227):
+    include/GlPboTargetHIP.hpp (PBO shared through hipGraphicsGLRegisterBuffer, or the
+    glMapBuffer + rt_read readback) compiles and links against libGL, the HIP runtime and
+    librtmi.  No GL context exists here or on the GPU box, so its two paths are not run;
+    without a GPU the program fails at rt_create (no CPU fallback)."""
+    subprocess.run(["make", "-s", "-B", "-C", str(ROOT / "tests" / "cpp"), "gl_pbo_target"], check=True, timeout=300)
+    exe = ROOT / "tests" / "cpp" / "gl_pbo_target"
+    assert exe.exists()
+    from conftest import gpu_available
+
+    if gpu_available():
+        pytest.skip("a GPU is visible: nothing to check without a GL context")
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3 and "rt_create" in r.stderr

@@ -5,7 +5,12 @@ Workload (BASELINE.json configs[3], the metric's config): 871,41
 synthetic mesh (dragon class), 1920x1080, sampleRate 16 (256 spp, one launch,
 progression 0), maxDepth 6, plymain.cpp lights and camera, BVH traversal.
 One step = one full frame: every rank renders its interleaved row stripes (rt_tile) and,
-for N > 1, the frame is gathered to rank 0 over RCCL (torch.distributed "nccl").
+for N > 1, the frame is gathered to rank 0 over RCCL — by librtmi's own communicator
+(rt_comm_render: seed-row halo, grouped ncclSend/ncclRecv, device-side assembly; the
+default, `--comm native`) or by torch.distributed (`--comm torch`, also the gloo rehearsal).
+At N > 1 the line carries `gathered_bit_exact`: the frame gathered through the same path from
+fixed seeds, compared on rank 0 with a single-GPU render of the same seeds (and every rank's
+seed rows with the single render's).
 A ray = one closest-hit or one any-hit (shadow) query, counted on the device.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -268,6 +273,18 @@ def main():
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays = int(r.item())
 
+    info = rt.renderInfo()
+    # a frame right after a camera change (the reference restarts refinement on every arrow
+    # key or drag, GlutCLWindow.cpp:229-279): wall clock including the host work of the new
+    # schedule (cost probe, LPT order, pixel classes), against the next frame with the camera
+    # unchanged
+    cold = interactive_cost(rt, step, cam_setup, azimuth, device, dist)
+
+    sharded = None
+    if n_ranks > 1:
+        sharded = verify_sharded(rt, pt, sc, ptdist, comm, dist, W, H, Wp, Hp, kernel, args.stripe, n_ranks, rank,
+                                 device, out, frame_full if comm is not None else None)
+
     if rank != 0:
         if comm is not None:
             comm.close()
@@ -330,6 +347,14 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
+    if kernel == pt.RayTracer.KERNEL_TRIS:
+        line["config"]["candidate_lists"] = {"on": bool(info["lists"]), "capacity_records": int(info["list_capacity"]),
+                                             "records": int(info["list_records"]),
+                                             "pixels_on_tree": int(info["list_pixels_tree"])}
+        line["config"]["pixels_deferred"] = int(info["pixels_deferred"])
+    line.update(cold)
+    if sharded is not None:
+        line.update(sharded)
     if cpu is not None and "gpu_vs_reference_bit_exact" in cpu:
         line["gpu_vs_reference_bit_exact"] = cpu["gpu_vs_reference_bit_exact"]
         line["gpu_vs_reference_pixels"] = cpu["gpu_vs_reference_pixels"]
@@ -340,6 +365,78 @@ def main():
         comm.close()
     if dist:
         dist.destroy_process_group()
+
+
+def interactive_cost(rt, step, cam_setup, azimuth, device, dist):
+    """Wall time of a step right after a 3-degree camera move (one arrow key) and of the next
+    step, same camera; max over ranks.  Restores the camera afterwards."""
+    import torch
+
+    def timed():
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3
+
+    res = {}
+    for k, az in (("cold", azimuth + 3.0), ("restore", azimuth)):
+        rt.setCameraSpherical(cam_setup["target"], cam_setup["elevation"], az, cam_setup["distance"])
+        c_ms = timed()
+        w_ms = timed()
+        if k == "cold":
+            res = {"cold_frame_ms": c_ms, "warm_frame_ms": w_ms, "schedule_host_ms": rt.renderInfo()["schedule_host_ms"]}
+    if dist:
+        t = torch.tensor([res["cold_frame_ms"], res["warm_frame_ms"]], dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        res["cold_frame_ms"], res["warm_frame_ms"] = float(t[0]), float(t[1])
+    return {k: round(v, 3) for k, v in res.items()}
+
+
+def verify_sharded(rt, pt, sc, ptdist, comm, dist, W, H, Wp, Hp, kernel, stripe, n_ranks, rank, device, out,
+                   frame_full):
+    """The N > 1 line checks itself (collective; untimed, after the timed steps): every rank
+    takes the same seed planes (the glibc rand() stream from its start), renders its stripes and
+    the frame is gathered through the same path as the timed step (rt_comm_render, or the
+    torch.distributed gather); rank 0 then renders the whole frame from the same seeds on its own
+    GPU and compares the two bit for bit, and every rank's seed rows (gathered to rank 0) with
+    the single render's.  Returns the fields for the line on rank 0."""
+    import torch
+
+    s0 = sc.default_seeds(Wp, Hp)
+    rt.setSeeds(Wp, Hp, s0)
+    if comm is not None:
+        comm.reset_halo()
+        comm.render(rt, frame_full, W, H, 0, kernel, stripe=stripe)
+        gathered = frame_full.cpu().numpy().reshape(-1) if rank == 0 else None
+        ranks = comm.count()
+    else:
+        rt.rayTrace(out, W, H, 0, kernel=kernel, tile=(stripe, n_ranks, rank))
+        g = ptdist.gather_frame(out, H, W, stripe)
+        gathered = g.cpu().numpy().reshape(-1) if rank == 0 else None
+        ranks = dist.get_world_size()
+    seeds = torch.from_numpy(rt.getSeeds().view(np.int32).copy())
+    if dist.get_backend() == "nccl":
+        seeds = seeds.to(f"cuda:{device}")
+    bucket = [torch.empty_like(seeds) for _ in range(n_ranks)] if rank == 0 else None
+    dist.gather(seeds, bucket, dst=0)
+    if rank != 0:
+        return None
+    rt.setSeeds(Wp, Hp, s0)
+    full = np.zeros(W * H * 4, np.float32)
+    rt.rayTrace(full, W, H, 0, kernel=kernel)
+    single = rt.getSeeds()
+    seeds_ok = True
+    plane = Wp * Hp
+    for r in range(n_ranks):
+        got = bucket[r].cpu().numpy().view(np.uint32)
+        rows = ptdist.tile_rows(H, stripe, n_ranks, r)
+        sl = (rows[:, None] * Wp + np.arange(W)[None, :]).reshape(-1)
+        seeds_ok &= bool(np.array_equal(got[sl], single[sl]) and np.array_equal(got[plane + sl], single[plane + sl]))
+    return {"gathered_bit_exact": bool(np.array_equal(gathered.view(np.uint32), full.view(np.uint32))),
+            "gathered_seeds_bit_exact": bool(seeds_ok), "ranks": int(ranks),
+            "gathered_check": "frame from the initial glibc rand() seeds gathered through the timed path == "
+                              "rank 0's single-GPU render of the same seeds (bits), seed rows per rank likewise"}
 
 
 def critical_chain(rt, pt, W, H, Wp, Hp, seeds0, kernel):

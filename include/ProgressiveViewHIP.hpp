@@ -9,13 +9,17 @@
  *   display()        glutDisplayCallback (:136-188): after a (re)allocation render with
  *                    progression 0, else refine while progression < maxProgression
  *                    (progression++), then the non-sharing readback (:214-225) into
- *                    pixels(); returns true when another redisplay should be posted;
+ *                    pixels(); returns true when another redisplay should be posted
+ *                    (glutPostRedisplay, :149-150, :157); rendered() tells whether it traced;
  *   reshape(w, h)    glutReshapeCallback (:113-134): new buffer at the next display;
  *   specialKey(k)    glutSpecialKeypressCallback (:228-262): arrows orbit the camera by
  *                    3 degrees (azimuth mod 360, elevation clamped to [10, 90]) about
  *                    (0, -4, 0), then restart();
  *   motion(dx, dy)   glutMotionCallback (:270-281): drag orbits by (dx, dy) degrees;
- *   restart()        (:295-301): progression back to 0.
+ *   restart()        (:294-301): progression back to 0.  Returns true when a redisplay must
+ *                    be posted: refinement had finished (progression >= maxProgression), so
+ *                    no display is pending — without it the window would stay frozen on the
+ *                    old view.  specialKey and motion return restart()'s answer.
  *
  * The orbit state starts at GlutCLWindow's constructor values (azimuth 105, elevation
  * 40, distance 5, :24-28), independent of the camera the application set — as in the
@@ -50,6 +54,7 @@ public:
     bool display()
     {
         bool again = false;
+        rendered_ = false;
         if (realloc_) {
             allocate();
             progression_ = 0;
@@ -71,7 +76,7 @@ public:
         realloc_ = true;
     }
 
-    void specialKey(Key k)
+    bool specialKey(Key k)
     {
         switch (k) {
         case KEY_LEFT: azimuth_ = std::fmod(azimuth_ + 3.0f, 360.0f); break;
@@ -80,21 +85,28 @@ public:
         case KEY_DOWN: elevation_ = std::fmax(elevation_ - 3.0f, 10.0f); break;
         }
         orbit();
-        restart();
+        return restart();
     }
 
-    void motion(int dx, int dy)
+    bool motion(int dx, int dy)
     {
         azimuth_ = std::fmod(azimuth_ + (float)dx, 360.0f);
         elevation_ = std::fmax(std::fmin(elevation_ + (float)dy, 90.0f), 10.0f);
         orbit();
-        restart();
+        return restart();
     }
 
-    void restart() { progression_ = 0; }
+    bool restart()
+    {
+        const bool post = progression_ >= maxProgression_;
+        progression_ = 0;
+        return post;
+    }
 
     const std::vector<float> &pixels() const { return pbo_; }
     unsigned progression() const { return progression_; }
+    unsigned maxProgression() const { return maxProgression_; }
+    bool rendered() const { return rendered_; }
     float azimuth() const { return azimuth_; }
     float elevation() const { return elevation_; }
     float distance() const { return distance_; }
@@ -123,6 +135,7 @@ private:
     {
         rt_.rayTrace(dev_, width_, height_, progression_, kernel_, true);
         rt_.read(pbo_.data(), pbo_.size()); /* the non-sharing readback into the PBO */
+        rendered_ = true;
     }
 
     RayTracerHIP &rt_;
@@ -130,7 +143,7 @@ private:
     int kernel_;
     float *dev_ = nullptr;
     std::vector<float> pbo_;
-    bool realloc_ = true;
+    bool realloc_ = true, rendered_ = false;
     unsigned progression_ = 0, maxProgression_ = 10000;
     float azimuth_ = 105.0f, elevation_ = 40.0f, distance_ = 5.0f;
 };

@@ -195,6 +195,25 @@ int rt_last_kernel_ms(const rt_ctx *ctx, float *ms);
    kernels), ms. */
 int rt_last_kernel_split_ms(const rt_ctx *ctx, float *prepass_ms, float *main_ms);
 
+/* What the last render did beyond the reference's launch (the triangle kernel's own
+   machinery; none of it changes a result bit). */
+typedef struct rt_render_info {
+    uint32_t kernel;           /* RT_KERNEL_* of the last render */
+    uint32_t traversal;        /* internal traversal kind of a triangle render */
+    uint32_t grid_blocks;      /* persistent grid of the main kernel */
+    uint32_t lists;            /* 1: camera-ray candidate lists were built and used */
+    uint64_t list_capacity;    /* list-area records (48 B each) reserved for the render */
+    uint64_t list_records;     /* records the pixels' lists took (read on the first call) */
+    uint32_t list_pixels_tree; /* pixels without a list (over RT_LIST_MAX candidates, a deep
+                                  frustum stack, or the area full): their camera rays took the tree */
+    uint32_t pixels_deferred;  /* box pixels whose shadow rays were deferred */
+    uint32_t schedule_rebuilt; /* 1: the cost probe, LPT order and pixel classes were recomputed
+                                  (camera, mesh, frame, tile or parameters changed) */
+    uint32_t reserved;
+    double schedule_host_ms;   /* host time spent enqueueing / sizing the schedule this render */
+} rt_render_info;
+int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
+
 /* ---- ray queries for hit-index parity (rtcommon.h:39-52 / :59-68 semantics).
    Host arrays; any_hit=0: out_idx = closest triangle (-1 none), out_t = its t;
    any_hit=1: out_idx = 1 if occluded in (tmin, tmax). ---- */
@@ -238,6 +257,8 @@ int rt_comm_get_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
 int rt_comm_create(const uint8_t id[RT_COMM_ID_BYTES], int n_ranks, int rank, int device, rt_comm **out);
 int rt_comm_destroy(rt_comm *comm);
 const char *rt_comm_last_error(const rt_comm *comm);
+/* ncclCommCount (rccl.h:378): ranks in the communicator as RCCL sees them. */
+int rt_comm_count(const rt_comm *comm, int *n_ranks);
 /* Frame assembly (collective): every rank passes its compact tile (device pointer,
    rt_tile_rows(H, {stripe, n_ranks, rank}) rows of W RGBA32F pixels); `root` receives
    them with grouped ncclSend/ncclRecv (one point-to-point xGMI transfer per sender)
@@ -255,9 +276,20 @@ int rt_assemble_tiles(const float *const *tiles_dev, uint32_t n_ranks, uint32_t 
    writer.  Capacity of the three output arrays: height entries. */
 int rt_seed_halo_plan(int32_t *writer, uint32_t height, uint32_t hpad, uint32_t stripe_rows, uint32_t n_ranks,
                       uint32_t progressive, uint32_t *src, uint32_t *dst, uint32_t *rows, uint32_t *n_moves);
+/* One rank's side of a halo plan (host only): the rows `me` sends to each peer and receives
+   from each peer, as one packed block per peer in peer order — send_rows holds the blocks to
+   peers 0, 1, ... back to back (send_counts[p] rows to peer p), likewise recv_rows /
+   recv_counts.  Row order within a block is the plan's, so peer p's send block to `me` and
+   my receive block from p list the same rows in the same order (the packed buffers match
+   word for word).  Capacity of send_rows / recv_rows: n_moves; of the counts: n_ranks. */
+int rt_seed_halo_peer_blocks(const uint32_t *src, const uint32_t *dst, const uint32_t *rows, uint32_t n_moves,
+                             uint32_t n_ranks, uint32_t me, uint32_t *send_rows, uint32_t *send_counts,
+                             uint32_t *recv_rows, uint32_t *recv_counts);
 /* One sharded rayTrace (collective): rank renders its stripes into a tile buffer the
-   communicator keeps (progression mixes into it across frames), exchanges the seed-row
-   halo first for RT_KERNEL_SPHERES (grouped ncclSend/ncclRecv of packed rows), then
+   communicator keeps (progression mixes into it across frames), first brings the seed rows
+   it reads up to date from their last writers (the seed-row halo: grouped ncclSend/ncclRecv
+   of packed rows; raytrace shifts rows by the progression, the other kernels read row y,
+   which after progressive sphere frames another rank may have written last), then
    gathers the frame to `root` (frame_dev: device, W*H*4 floats on root).  Bit-identical
    to rt_render of the whole frame on one GPU.  Call rt_comm_reset_halo after replacing
    a context's seeds (rt_set_seeds). */

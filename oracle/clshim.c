@@ -14,11 +14,31 @@
  * reference's algorithm lives here.
  *
  * Symbols use the Itanium-mangled names clang emits for OpenCL overloads.
+ *
+ * Built with -DCLSHIM_LIBM (oracle/Makefile `ref_libm` -> oracle/_ref_libm/) the
+ * transcendentals come from glibc's libm instead (sinf, cosf, expf, logf, powf: another
+ * conforming OpenCL builtin library).  That second build of the unchanged reference
+ * measures how much the result depends on the builtin library the pinned model fixes
+ * (oracle/libm_sensitivity.py).
  */
 #include <stddef.h>
 #include <stdint.h>
 
 #include "rt_math.h"
+#ifdef CLSHIM_LIBM
+#include <math.h>
+#define SHIM_SIN(x) sinf(x)
+#define SHIM_COS(x) cosf(x)
+#define SHIM_EXP(x) expf(x)
+#define SHIM_LOG(x) logf(x)
+#define SHIM_POW(x, y) powf(x, y)
+#else
+#define SHIM_SIN(x) rt_sinf(x)
+#define SHIM_COS(x) rt_cosf(x)
+#define SHIM_EXP(x) rt_expf(x)
+#define SHIM_LOG(x) rt_logf(x)
+#define SHIM_POW(x, y) rt_powf(x, y)
+#endif
 
 typedef float float4 __attribute__((ext_vector_type(4)));
 
@@ -34,15 +54,15 @@ size_t cl_get_global_size(unsigned d) CLSYM("_Z15get_global_sizej");
 size_t cl_get_global_size(unsigned d) { return d < 3 ? clshim_gsz[d] : 1; }
 
 float cl_cos(float x) CLSYM("_Z3cosf");
-float cl_cos(float x) { return rt_cosf(x); }
+float cl_cos(float x) { return SHIM_COS(x); }
 float cl_sin(float x) CLSYM("_Z3sinf");
-float cl_sin(float x) { return rt_sinf(x); }
+float cl_sin(float x) { return SHIM_SIN(x); }
 float cl_exp(float x) CLSYM("_Z3expf");
-float cl_exp(float x) { return rt_expf(x); }
+float cl_exp(float x) { return SHIM_EXP(x); }
 float cl_log(float x) CLSYM("_Z3logf");
-float cl_log(float x) { return rt_logf(x); }
+float cl_log(float x) { return SHIM_LOG(x); }
 float cl_pow(float x, float y) CLSYM("_Z3powff");
-float cl_pow(float x, float y) { return rt_powf(x, y); }
+float cl_pow(float x, float y) { return SHIM_POW(x, y); }
 float cl_sqrt(float x) CLSYM("_Z4sqrtf");
 float cl_sqrt(float x) { return rt_sqrtf(x); }
 float cl_rsqrt(float x) CLSYM("_Z5rsqrtf");

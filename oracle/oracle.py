@@ -20,6 +20,7 @@ import numpy as np
 ORACLE_DIR = Path(__file__).resolve().parent
 LIBORACLE = ORACLE_DIR / "liboracle.so"
 LIBREF = ORACLE_DIR / "_ref" / "libptref.so"
+LIBREF_LIBM = ORACLE_DIR / "_ref_libm" / "libptref.so"  # the same reference, glibc transcendentals
 REFERENCE_ROOT = Path("/root/reference")
 
 KERNEL_SPHERES, KERNEL_SPHERES_SS, KERNEL_TRIS = 0, 1, 2
@@ -61,6 +62,8 @@ class Oracle:
             fn.restype = ctypes.c_float
         L.or_math_pow.argtypes = [ctypes.c_float, ctypes.c_float]
         L.or_math_pow.restype = ctypes.c_float
+        L.or_math_vec.argtypes = [i32, vp, vp, vp, ctypes.c_size_t]
+        L.or_math_vec.restype = None
 
     def render_spheres(self, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds,
                        single_sample=False, nthreads=None):
@@ -84,6 +87,16 @@ class Oracle:
         assert st == 0
         return c.closest, c.shadow
 
+    MATH_FN = {"sin": 0, "cos": 1, "exp": 2, "log": 3, "pow": 4, "sincos_s": 5, "sincos_c": 6}
+
+    def math(self, fn: str, x: np.ndarray, y: float = 0.0) -> np.ndarray:
+        """The pinned builtin `fn` (include/rt_math.h) over every element of x (pow: x ** y)."""
+        x = np.ascontiguousarray(x, np.float32)
+        yy = np.array([y], np.float32)
+        out = np.empty_like(x)
+        self.lib.or_math_vec(self.MATH_FN[fn], _p(x), _p(yy), _p(out), x.size)
+        return out
+
     def closest_hits(self, rays, verts, idx):
         n = len(rays)
         oi = np.empty(n, np.int32)
@@ -101,12 +114,13 @@ class Oracle:
 class Reference:
     """The reference kernel itself (clrt/ocl/raytracer.cl compiled for x86-64) + KAT wrappers."""
 
-    def __init__(self, build_if_missing: bool = True):
-        if not LIBREF.exists() and build_if_missing:
+    def __init__(self, build_if_missing: bool = True, path: os.PathLike | None = None):
+        lib = Path(path) if path else LIBREF
+        if not lib.exists() and build_if_missing:
             build(ref=True)
-        if not LIBREF.exists():
-            raise FileNotFoundError(f"{LIBREF} (needs /root/reference to build)")
-        self.lib = ctypes.CDLL(str(LIBREF))
+        if not lib.exists():
+            raise FileNotFoundError(f"{lib} (needs /root/reference to build)")
+        self.lib = ctypes.CDLL(str(lib))
         L = self.lib
         vp, u32, i32, f32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float
         L.ref_launch_kernel.argtypes = [i32, vp, vp, vp, u32, u32, u32, u32, u32, u32, u32, u32, vp, vp, vp, u32, i32]

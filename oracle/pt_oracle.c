@@ -884,6 +884,25 @@ OR_API float or_math_exp(float x) { return rt_expf(x); }
 OR_API float or_math_log(float x) { return rt_logf(x); }
 OR_API float or_math_pow(float x, float y) { return rt_powf(x, y); }
 
+/* Vectorised: the pinned builtins over whole argument ranges (tests/test_oracle_golden.py
+   test_math_model_sanity).  fn: 0 sin, 1 cos, 2 exp, 3 log, 4 pow(x, y[0]), 5 / 6 the sine /
+   cosine half of rt_sincosf (the triangle kernel's shared light / bounce direction). */
+OR_API void or_math_vec(int fn, const float *x, const float *y, float *out, size_t n)
+{
+    for (size_t i = 0; i < n; ++i) {
+        float s, c;
+        switch (fn) {
+        case 0: out[i] = rt_sinf(x[i]); break;
+        case 1: out[i] = rt_cosf(x[i]); break;
+        case 2: out[i] = rt_expf(x[i]); break;
+        case 3: out[i] = rt_logf(x[i]); break;
+        case 4: out[i] = rt_powf(x[i], y[0]); break;
+        case 5: rt_sincosf(x[i], &s, &c); out[i] = s; break;
+        default: rt_sincosf(x[i], &s, &c); out[i] = c; break;
+        }
+    }
+}
+
 /* Pointer-only wrappers for the per-function known-answer tests. */
 OR_API float or_kat_intersect_sphere(const rt_ray *r, const rt_vec3 *c, float radius)
 {

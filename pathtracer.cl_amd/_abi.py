@@ -109,6 +109,22 @@ class RtCounters(ctypes.Structure):
     ]
 
 
+class RtRenderInfo(ctypes.Structure):
+    _fields_ = [
+        ("kernel", ctypes.c_uint32),
+        ("traversal", ctypes.c_uint32),
+        ("grid_blocks", ctypes.c_uint32),
+        ("lists", ctypes.c_uint32),
+        ("list_capacity", ctypes.c_uint64),
+        ("list_records", ctypes.c_uint64),
+        ("list_pixels_tree", ctypes.c_uint32),
+        ("pixels_deferred", ctypes.c_uint32),
+        ("schedule_rebuilt", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("schedule_host_ms", ctypes.c_double),
+    ]
+
+
 # Every symbol the header declares, with its ctypes signature.
 _vp, _u32, _i32, _f32, _sz = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
 SIGNATURES = {
@@ -144,6 +160,7 @@ SIGNATURES = {
     "rt_set_counting": (_i32, [_vp, _i32]),
     "rt_last_kernel_ms": (_i32, [_vp, ctypes.POINTER(_f32)]),
     "rt_last_kernel_split_ms": (_i32, [_vp, ctypes.POINTER(_f32), ctypes.POINTER(_f32)]),
+    "rt_last_render_info": (_i32, [_vp, ctypes.POINTER(RtRenderInfo)]),
     "rt_trace_rays": (_i32, [_vp, _vp, _u32, _i32, _vp, _vp]),
     "rt_mesh_vertex_count": (_u32, [_u32]),
     "rt_make_mesh": (_i32, [_u32, _f32, _f32, _f32, _f32, _vp, _vp]),
@@ -158,9 +175,11 @@ SIGNATURES = {
     "rt_comm_create": (_i32, [_vp, _i32, _i32, _i32, ctypes.POINTER(_vp)]),
     "rt_comm_destroy": (_i32, [_vp]),
     "rt_comm_last_error": (ctypes.c_char_p, [_vp]),
+    "rt_comm_count": (_i32, [_vp, ctypes.POINTER(_i32)]),
     "rt_comm_gather_frame": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
     "rt_assemble_tiles": (_i32, [_vp, _u32, _u32, _u32, _u32, _vp, _i32]),
     "rt_seed_halo_plan": (_i32, [_vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _vp, ctypes.POINTER(_u32)]),
+    "rt_seed_halo_peer_blocks": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp]),
     "rt_comm_render": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32, _u32, _i32]),
     "rt_comm_reset_halo": (_i32, [_vp]),
 }

@@ -67,25 +67,11 @@ struct TmpNode {
 
 constexpr int kMaxBins = 64;
 
-/* SAH parameters: bins per axis and the cost of one node step relative to one
-   triangle test (RT_SAH_BINS / RT_SAH_TRAV override them for experiments). */
-int sah_bins()
-{
-    static const int b = [] {
-        const char *v = getenv("RT_SAH_BINS");
-        const int x = v ? atoi(v) : 32;
-        return std::min(std::max(x, 4), kMaxBins);
-    }();
-    return b;
-}
-float sah_trav()
-{
-    static const float c = [] {
-        const char *v = getenv("RT_SAH_TRAV");
-        return v ? (float)atof(v) : 1.0f;
-    }();
-    return c;
-}
+/* SAH parameters: bins per axis and the cost of one node step relative to one triangle
+   test (measured on the dragon frame: 16 / 64 bins -4 / -2.5 %, node cost 0.7 / 1.5 / 1.7
+   ±0.5 / -1 / -4 % against 32 and 1.0). */
+int sah_bins() { return 32; }
+float sah_trav() { return 1.0f; }
 
 struct Builder {
     const float *verts;

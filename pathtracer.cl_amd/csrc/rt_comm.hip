@@ -182,6 +182,12 @@ int rt_comm_destroy(rt_comm *m)
 
 const char *rt_comm_last_error(const rt_comm *m) { return m ? m->err.c_str() : "null communicator"; }
 
+int rt_comm_count(const rt_comm *m, int *n)
+{
+    if (!m || !n) return RT_ERR_ARG;
+    return ncclCommCount(m->nccl, n) == ncclSuccess ? RT_OK : RT_ERR_HIP;
+}
+
 int rt_assemble_tiles(const float *const *tiles, uint32_t n, uint32_t W, uint32_t H, uint32_t stripe, float *frame,
                       int device)
 {
@@ -261,6 +267,28 @@ int rt_seed_halo_plan(int32_t *writer, uint32_t H, uint32_t hpad, uint32_t strip
     return RT_OK;
 }
 
+int rt_seed_halo_peer_blocks(const uint32_t *src, const uint32_t *dst, const uint32_t *rows, uint32_t k, uint32_t n,
+                             uint32_t me, uint32_t *send_rows, uint32_t *send_counts, uint32_t *recv_rows,
+                             uint32_t *recv_counts)
+{
+    if (n == 0 || me >= n || !send_counts || !recv_counts || (k && (!src || !dst || !rows || !send_rows || !recv_rows)))
+        return RT_ERR_ARG;
+    std::vector<std::vector<uint32_t>> to(n), from(n);
+    for (uint32_t i = 0; i < k; ++i) {
+        if (src[i] >= n || dst[i] >= n) return RT_ERR_ARG;
+        if (src[i] == me) to[dst[i]].push_back(rows[i]);
+        if (dst[i] == me) from[src[i]].push_back(rows[i]);
+    }
+    size_t so = 0, ro = 0;
+    for (uint32_t p = 0; p < n; ++p) {
+        send_counts[p] = (uint32_t)to[p].size();
+        recv_counts[p] = (uint32_t)from[p].size();
+        for (uint32_t r : to[p]) send_rows[so++] = r;
+        for (uint32_t r : from[p]) recv_rows[ro++] = r;
+    }
+    return RT_OK;
+}
+
 int rt_comm_reset_halo(rt_comm *m)
 {
     if (!m) return RT_ERR_ARG;
@@ -285,63 +313,60 @@ int rt_comm_render(rt_comm *m, rt_ctx *c, float *frame, uint32_t W, uint32_t H, 
        seeds identically on every rank (rt_render), so nothing is stale */
     const bool fresh = m->writer.empty() || m->key_ctx != c || m->key_w != W || m->key_h != H ||
                        m->key_stripe != stripe;
+    /* the rows this frame reads: raytrace shifts them by the progression, the other kernels read
+       row y (raytracer.cl:20-30, :142-144, :207-209) */
+    const uint32_t shift = kernel == RT_KERNEL_SPHERES ? prog : 0u;
     int flags = RT_OUT_DEVICE;
-    if (kernel == RT_KERNEL_SPHERES && n > 1) {
-        flags |= RT_SEEDS_HALO;
-        if (!fresh) {
-            std::vector<uint32_t> src(H), dst(H), rows(H);
-            std::vector<int32_t> w = m->writer; /* committed after the render */
-            uint32_t k = 0;
-            if (rt_seed_halo_plan(w.data(), H, m->hpad, stripe, n, prog, src.data(), dst.data(), rows.data(), &k))
-                return fail(m, RT_ERR_STATE, "halo plan");
-            /* my sends and receives, one contiguous packed block per peer */
-            std::vector<std::vector<uint32_t>> to(n), from(n);
-            for (uint32_t i = 0; i < k; ++i) {
-                if (src[i] == me) to[dst[i]].push_back(rows[i]);
-                if (dst[i] == me) from[src[i]].push_back(rows[i]);
-            }
-            size_t ns = 0, nr = 0;
-            for (uint32_t p = 0; p < n; ++p) {
-                ns += to[p].size();
-                nr += from[p].size();
-            }
-            const size_t row_words = 2ull * m->wpad;
-            if (ns + nr) {
-                if (int e = grow(m, &m->halo_send, &m->halo_send_bytes, ns * row_words * 4)) return e;
-                if (int e = grow(m, &m->halo_recv, &m->halo_recv_bytes, nr * row_words * 4)) return e;
-                size_t off = 0;
-                for (uint32_t p = 0; p < n; ++p)
-                    if (!to[p].empty()) {
-                        const int e = rt_pack_seed_rows(c, to[p].data(), (uint32_t)to[p].size(), m->halo_send + off,
-                                                        RT_OUT_DEVICE);
-                        if (e) return fail(m, e, std::string("rt_pack_seed_rows: ") + rt_last_error(c));
-                        off += to[p].size() * row_words;
-                    }
-                NCCLC(m, ncclGroupStart());
-                size_t so = 0, ro = 0;
-                for (uint32_t p = 0; p < n; ++p) {
-                    if (!to[p].empty()) {
-                        NCCLC(m, ncclSend(m->halo_send + so, to[p].size() * row_words, ncclUint32, (int)p, m->nccl,
-                                          m->stream));
-                        so += to[p].size() * row_words;
-                    }
-                    if (!from[p].empty()) {
-                        NCCLC(m, ncclRecv(m->halo_recv + ro, from[p].size() * row_words, ncclUint32, (int)p, m->nccl,
-                                          m->stream));
-                        ro += from[p].size() * row_words;
-                    }
+    if (n > 1) flags |= RT_SEEDS_HALO;
+    if (n > 1 && !fresh) {
+        std::vector<uint32_t> src(H), dst(H), rows(H);
+        std::vector<int32_t> w = m->writer; /* committed after the render */
+        uint32_t k = 0;
+        if (rt_seed_halo_plan(w.data(), H, m->hpad, stripe, n, shift, src.data(), dst.data(), rows.data(), &k))
+            return fail(m, RT_ERR_STATE, "halo plan");
+        /* my sends and receives, one contiguous packed block per peer */
+        std::vector<uint32_t> to_rows(k), to_cnt(n), from_rows(k), from_cnt(n);
+        if (rt_seed_halo_peer_blocks(src.data(), dst.data(), rows.data(), k, n, me, to_rows.data(), to_cnt.data(),
+                                     from_rows.data(), from_cnt.data()))
+            return fail(m, RT_ERR_STATE, "halo peer blocks");
+        size_t ns = 0, nr = 0;
+        for (uint32_t p = 0; p < n; ++p) {
+            ns += to_cnt[p];
+            nr += from_cnt[p];
+        }
+        const size_t row_words = 2ull * m->wpad;
+        if (ns + nr) {
+            if (int e = grow(m, &m->halo_send, &m->halo_send_bytes, ns * row_words * 4)) return e;
+            if (int e = grow(m, &m->halo_recv, &m->halo_recv_bytes, nr * row_words * 4)) return e;
+            /* one packed block ([plane][row][x], rt_pack_seed_rows) per peer, back to back */
+            for (uint32_t p = 0, so = 0; p < n; so += to_cnt[p], ++p)
+                if (to_cnt[p]) {
+                    const int e = rt_pack_seed_rows(c, to_rows.data() + so, to_cnt[p], m->halo_send + so * row_words,
+                                                    RT_OUT_DEVICE);
+                    if (e) return fail(m, e, std::string("rt_pack_seed_rows: ") + rt_last_error(c));
                 }
-                NCCLC(m, ncclGroupEnd());
-                HIPC(m, hipStreamSynchronize(m->stream));
-                ro = 0;
-                for (uint32_t p = 0; p < n; ++p)
-                    if (!from[p].empty()) {
-                        const int e = rt_unpack_seed_rows(c, from[p].data(), (uint32_t)from[p].size(),
-                                                          m->halo_recv + ro, RT_OUT_DEVICE);
-                        if (e) return fail(m, e, std::string("rt_unpack_seed_rows: ") + rt_last_error(c));
-                        ro += from[p].size() * row_words;
-                    }
+            NCCLC(m, ncclGroupStart());
+            size_t so = 0, ro = 0;
+            for (uint32_t p = 0; p < n; ++p) {
+                if (to_cnt[p]) {
+                    NCCLC(m, ncclSend(m->halo_send + so * row_words, to_cnt[p] * row_words, ncclUint32, (int)p,
+                                      m->nccl, m->stream));
+                    so += to_cnt[p];
+                }
+                if (from_cnt[p]) {
+                    NCCLC(m, ncclRecv(m->halo_recv + ro * row_words, from_cnt[p] * row_words, ncclUint32, (int)p,
+                                      m->nccl, m->stream));
+                    ro += from_cnt[p];
+                }
             }
+            NCCLC(m, ncclGroupEnd());
+            HIPC(m, hipStreamSynchronize(m->stream));
+            for (uint32_t p = 0, ro2 = 0; p < n; ro2 += from_cnt[p], ++p)
+                if (from_cnt[p]) {
+                    const int e = rt_unpack_seed_rows(c, from_rows.data() + ro2, from_cnt[p],
+                                                      m->halo_recv + ro2 * row_words, RT_OUT_DEVICE);
+                    if (e) return fail(m, e, std::string("rt_unpack_seed_rows: ") + rt_last_error(c));
+                }
         }
     }
     const int e = rt_render(c, m->tile, W, H, prog, kernel, &tile, flags);
@@ -355,8 +380,7 @@ int rt_comm_render(rt_comm *m, rt_ctx *c, float *frame, uint32_t W, uint32_t H, 
         m->key_stripe = stripe;
     }
     /* record this frame's seed writes: raytrace writes row (y + prog) % Hpad, the other
-       kernels row y (raytracer.cl:20-30, :142-144, :207-209) */
-    const uint32_t shift = kernel == RT_KERNEL_SPHERES ? prog : 0u;
+       kernels row y */
     for (uint32_t y = 0; y < H; ++y) m->writer[((uint64_t)y + shift) % m->hpad] = (int32_t)row_rank(y, stripe, n);
     return rt_comm_gather_frame(m, m->tile, frame, W, H, stripe, root);
 }

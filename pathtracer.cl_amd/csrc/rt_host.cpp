@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -63,6 +64,18 @@ const char *hip_str(hipError_t e) { return hipGetErrorString(e); }
 
 constexpr double kPi = 3.14159265358979323846; /* M_PI */
 
+/* Scheduling constants of the triangle kernel, each swept on the dragon frame (DESIGN.md §5;
+   results are independent of all of them):
+     kProbeN    cost-probe rays per pixel, kProbeN x kProbeN;
+     kFetchK    completed queries that end a wave's stepping round (12 / 16 / 20 / 24 / 32 / 40:
+                166.8 / 163.9 / 163.0 / 162.3 / 163.9 / 168.2 ms); the same for waves holding
+                box pixels (8 / 16 / 24 within 0.5 %);
+     kFetchFrac the stepping round also ends at ceil(live lanes x kFetchFrac / 64) completed
+                queries (r02 A/B: full frame 162.8 -> 160.6 ms, slowest 8-way tile 219 -> 107 ms). */
+constexpr uint32_t kProbeN = 2;
+constexpr uint32_t kFetchK = 24;
+constexpr uint32_t kFetchFrac = 24;
+
 } // namespace
 
 struct rt_ctx {
@@ -83,14 +96,19 @@ struct rt_ctx {
     uint32_t *d_nodes4q = nullptr; /* 4-wide tree, compressed nodes */
     float *d_tris = nullptr;
     size_t tris_cap = 0;       /* triangle records d_tris holds (mesh + camera-ray candidate lists) */
-    uint8_t *d_lists = nullptr; /* candidate count per pixel (k_pixel_lists) */
+    uint8_t *d_lists = nullptr;       /* candidate count per pixel (k_pixel_lists) */
+    uint32_t *d_list_first = nullptr; /* first list slot per pixel (compacted list area) */
+    uint32_t *d_list_alloc = nullptr; /* the list area's allocator */
     size_t lists_bytes = 0;
     int pixel_lists = -1; /* RT_PIXEL_LISTS: 0 off, 1 on, unset: on for sampleRate >= 4 (the pre-pass
                              costs about a traversal per pixel: a 1-spp frame does not repay it) */
+    size_t list_mb = 4096; /* RT_LIST_MB: device memory of the list area (pixels beyond it take the tree) */
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
+    uint32_t order_cap = 0;
     uint32_t *d_flags = nullptr; /* cost probe per pixel (k_probe_cost) */
+    RtSchedScratch sched;        /* the device-side schedule (rt_sched.hip) */
     /* deferred shadow rays of box pixels (k_tris -> k_defer_shadow -> k_defer_finish) */
     int32_t *d_class = nullptr;  /* per pixel: -1 mesh, -2 box, >= 0 box with a defer slot */
     size_t class_bytes = 0;
@@ -101,7 +119,7 @@ struct rt_ctx {
     size_t defer_rec_cap = 0, defer_seg_cap = 0, defer_slot_cap = 0; /* allocated entries */
     uint32_t n_defer = 0;
     int defer = -1;          /* RT_DEFER: 1 on, 0 off, unset = auto (on when the launch has fewer than
-                                4 pixels per resident lane at sampleRate >= 4: tiles of a multi-GPU
+                                2 pixels per resident lane at sampleRate >= 4: tiles of a multi-GPU
                                 many-sample frame) */
     size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer buffers */
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
@@ -110,13 +128,9 @@ struct rt_ctx {
     size_t flags_bytes = 0;
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
-    uint32_t fetch_k = 24;     /* re-swept after RT_SHADOW_REDO: 12 / 16 / 20 / 24 / 32 / 40 -> 166.8 / 163.9 / 163.0 / 162.3 / 163.9 / 168.2 ms */
-    uint32_t fetch_k_box = 24; /* waves holding box pixels (probe); 8 / 16 / 24 within 0.5 % */
-    uint32_t probe_n = 2;      /* cost probe: probe_n x probe_n rays per pixel (RT_PROBE_N) */
-    uint32_t fetch_frac = 24;  /* stepping-round exit relative to the live lanes (RT_FETCH_FRAC, 1/64ths; 0 = off):
-                                  r02 A/B (profiles/r02b/fetch_ab.jsonl) full frame 162.8 -> 160.6 ms, one row
-                                  alone 157.8 -> 78.9 ms, slowest of 8 row-stripe tiles 219 -> 107 ms */
-    uint32_t box_exit = 0;     /* a box pixel's completed query ends the stepping round (RT_BOX_EXIT) */
+    bool schedule_rebuilt = false; /* the last triangle render recomputed the schedule */
+    rt_render_info info = {};      /* rt_last_render_info */
+    bool info_list_pending = false; /* info.list_records still to be read from the allocator */
     int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
@@ -361,121 +375,79 @@ int grid_blocks(rt_ctx *c, int trav, bool count, bool defer, int *out)
     return RT_OK;
 }
 
-/* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by
-   its paths: a camera ray that hits the mesh ends after one shadow query per
-   light (rtcommon.h:411-421), one that misses bounces off the box up to
-   maxDepth+1 times with shadow queries at each (rtcommon.h:425-461), and each
-   query costs its traversal steps.  A probe (k_probe_cost) traces a 2x2 grid of
-   camera rays per pixel and, on mesh hits, their shadow rays toward the light
-   centres with the real traversal, counting steps; a probe ray that misses stands
-   for a box path of (1 + lights) x (maxDepth + 1) queries of 1.4x the mean
-   probed query.  The queue hands out the
-   most expensive 8x8 tiles first, so the launch does not end on a tail of long
-   pixels (measured: without the step counts the last pixels to finish were mesh
-   pixels of 50 steps per query, handed out late as "cheap").  Scheduling only:
-   every pixel's result is independent of when it is rendered.  Cached until
-   camera, mesh, frame, tile or path depth change. */
-/* Pixel classes for the triangle kernel, from the probe words: a pixel some of whose probe
-   rays missed the mesh is a box pixel (its samples bounce off the box up to maxDepth + 1
-   times: the long serial chains).  Box pixels get a slot in the deferred-shadow buffers
-   (DESIGN.md §5): per slot, one 32-B record per (sample, segment, light), a segment-kind
-   byte per (sample, segment), a visibility byte and a queue entry per record.  Slots are
-   dealt in pixel order up to RT_DEFER_MB of device memory; further box pixels trace their
-   shadow rays inline (class -2). */
-int classify_pixels(rt_ctx *c, const std::vector<uint32_t> &f, uint32_t W, uint32_t hl, uint64_t lanes,
-                    hipStream_t st)
+/* Deferred-shadow buffers for n slots: per slot, one 32-B record per (sample, segment, light),
+   a segment-kind byte per (sample, segment), a visibility byte and a queue entry per record. */
+int ensure_defer(rt_ctx *c, uint64_t n, uint64_t recs, uint64_t segs)
 {
-    const size_t npx = (size_t)W * hl;
-    /* Deferral shortens the box chains but moves their shadow queries into a second launch
-       that cannot use the tail of the first: it pays where the chains set the frame time (a
-       tile with few pixels per lane) of a many-sample frame, not on a full frame (dragon
-       1920x1080: 161.7 -> 173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) nor on short
-       chains (bunny class 1024^2 at 1 spp: 0.95 -> 1.35 ms, r02u) */
-    /* (r02z, with the candidate lists: the 2-way dragon tile, 1.04M pixels, 65.5 ms deferred
-       against 60.7 inline; the 4-way 39 vs 46 ms, the 8-way 30 vs 44 ms: the line sits below
-       two pixels per resident lane) */
-    const bool use = c->defer == 1 || (c->defer < 0 && npx < 2 * lanes && c->sample_rate >= 4);
-    const uint32_t pn2 = c->probe_n * c->probe_n;
-    const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
-    const uint64_t nl = c->lights.size();
-    const uint64_t recs = spp * nd * nl; /* records per slot */
-    uint64_t max_slots = 0;
-    if (use && nl > 0 && spp > 0 && spp <= 1024 && recs > 0) {
-        const uint64_t bytes_per_slot = recs * (32 + 1 + 4) + spp * nd + 4;
-        max_slots = ((uint64_t)c->defer_mb << 20) / bytes_per_slot;
-        max_slots = std::min<uint64_t>(max_slots, 0xffffffffull / recs);
+    if (c->defer_slot_cap < n) {
+        free_dev(c->d_defer_pixel);
+        c->d_defer_pixel = nullptr;
+        c->defer_slot_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_defer_pixel, n * 4));
+        c->defer_slot_cap = n;
     }
-    std::vector<int32_t> cls(npx);
-    std::vector<uint32_t> px;
-    for (size_t p = 0; p < npx; ++p) {
-        const bool box = (f[p] >> RT_PROBE_HIT_SHIFT) < pn2;
-        if (!box) cls[p] = -1;
-        else if (px.size() < max_slots) {
-            cls[p] = (int32_t)px.size();
-            px.push_back((uint32_t)p);
-        } else cls[p] = -2;
+    if (c->defer_rec_cap < n * recs) {
+        free_dev(c->d_defer_rec);
+        free_dev(c->d_defer_vis);
+        free_dev(c->d_defer_queue);
+        c->d_defer_rec = nullptr;
+        c->d_defer_vis = nullptr;
+        c->d_defer_queue = nullptr;
+        c->defer_rec_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_defer_rec, n * recs * 32));
+        HIPCHK(c, hipMalloc(&c->d_defer_vis, n * recs));
+        HIPCHK(c, hipMalloc(&c->d_defer_queue, n * recs * 4));
+        c->defer_rec_cap = n * recs;
     }
-    if (c->class_bytes < npx * 4) {
-        free_dev(c->d_class);
-        c->d_class = nullptr;
-        c->class_bytes = 0;
-        HIPCHK(c, hipMalloc(&c->d_class, npx * 4));
-        c->class_bytes = npx * 4;
+    if (c->defer_seg_cap < n * segs) {
+        free_dev(c->d_defer_seg);
+        c->d_defer_seg = nullptr;
+        c->defer_seg_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_defer_seg, n * segs));
+        c->defer_seg_cap = n * segs;
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_class, cls.data(), npx * 4, hipMemcpyHostToDevice, st));
-    const uint64_t n = px.size();
-    if (n) {
-        if (c->defer_slot_cap < n) {
-            free_dev(c->d_defer_pixel);
-            c->d_defer_pixel = nullptr;
-            c->defer_slot_cap = 0;
-            HIPCHK(c, hipMalloc(&c->d_defer_pixel, n * 4));
-            c->defer_slot_cap = n;
-        }
-        if (c->defer_rec_cap < n * recs) {
-            free_dev(c->d_defer_rec);
-            free_dev(c->d_defer_vis);
-            free_dev(c->d_defer_queue);
-            c->d_defer_rec = nullptr;
-            c->d_defer_vis = nullptr;
-            c->d_defer_queue = nullptr;
-            c->defer_rec_cap = 0;
-            HIPCHK(c, hipMalloc(&c->d_defer_rec, n * recs * 32));
-            HIPCHK(c, hipMalloc(&c->d_defer_vis, n * recs));
-            HIPCHK(c, hipMalloc(&c->d_defer_queue, n * recs * 4));
-            c->defer_rec_cap = n * recs;
-        }
-        if (c->defer_seg_cap < n * spp * nd) {
-            free_dev(c->d_defer_seg);
-            c->d_defer_seg = nullptr;
-            c->defer_seg_cap = 0;
-            HIPCHK(c, hipMalloc(&c->d_defer_seg, n * spp * nd));
-            c->defer_seg_cap = n * spp * nd;
-        }
-        if (!c->d_defer_qcount) HIPCHK(c, hipMalloc(&c->d_defer_qcount, 2 * sizeof(uint32_t)));
-        HIPCHK(c, hipMemcpyAsync(c->d_defer_pixel, px.data(), n * 4, hipMemcpyHostToDevice, st));
-    }
-    HIPCHK(c, hipStreamSynchronize(st));
-    c->n_defer = (uint32_t)n;
+    if (!c->d_defer_qcount) HIPCHK(c, hipMalloc(&c->d_defer_qcount, 2 * sizeof(uint32_t)));
     return RT_OK;
 }
 
+/* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by its paths: a
+   camera ray that hits the mesh ends after one shadow query per light (rtcommon.h:411-421),
+   one that misses bounces off the box up to maxDepth+1 times with shadow queries at each
+   (rtcommon.h:425-461), and each query costs its traversal steps.  A probe (k_probe_cost)
+   traces a 2x2 grid of camera rays per pixel and, on mesh hits, their shadow rays toward the
+   light centres with the real traversal, counting steps.  From it the device computes the
+   tile costs, the LPT order (most expensive 8x8 tiles first, so the launch does not end on a
+   tail of long pixels) and the pixel classes (rt_sched.hip) — no host round trip, except one
+   4-byte read of the box-pixel count when the launch defers shadow rays (to size the
+   buffers).  Box pixels (some probe ray missed the mesh: the long serial chains) get a slot
+   in the deferred-shadow buffers in pixel order up to RT_DEFER_MB of device
+   memory; further box pixels trace their shadow rays inline (class -2).  Scheduling only:
+   every pixel's result is independent of when it is rendered.  Cached until camera, mesh,
+   traversal, frame, tile or path parameters change. */
 int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
 {
     const uint32_t W = a.W, hl = a.Hl;
+    /* everything the order, the pixel classes and the defer slots depend on — including the
+       traversal (only the compressed tree is probed and only its kernel form records deferred
+       shadow rays: a key without it would hand a BVH4F / linear launch the stale slots) */
+    const uintptr_t np = reinterpret_cast<uintptr_t>(a.nodes);
     std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
                                  (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks,
-                                 c->sample_rate, (uint32_t)(c->defer + 1)};
+                                 c->sample_rate, (uint32_t)(c->defer + 1), (uint32_t)trav_kind(c), (uint32_t)np,
+                                 (uint32_t)((uint64_t)np >> 32)};
     const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
-    const uint32_t tx = (W + 7) / 8, ty = (hl + 7) / 8, n_t = tx * ty;
+    const uint32_t n_t = ((W + 7) / 8) * ((hl + 7) / 8);
+    c->schedule_rebuilt = false;
     if (key == c->order_key) return RT_OK;
-    if (a.nodes != reinterpret_cast<const float *>(c->d_nodes4q) || !c->d_nodes4q) {
+    c->order_key.clear();
+    c->n_defer = 0;
+    if (trav_kind(c) != RT_TRAV_BVH4Q || a.nodes != reinterpret_cast<const float *>(c->d_nodes4q)) {
         /* the probe walks the compressed tree with its spill layout: other traversal kinds
-           (measurement variants) keep the row-major queue */
+           (measurement variants) keep the row-major queue and no classes */
         free_dev(c->d_order);
         c->d_order = nullptr;
-        c->n_defer = 0;
+        c->order_cap = 0;
         c->order_key = key;
         return RT_OK;
     }
@@ -487,57 +459,64 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         HIPCHK(c, hipMalloc(&c->d_flags, npx * 4));
         c->flags_bytes = npx * 4;
     }
+    if (c->class_bytes < npx * 4) {
+        free_dev(c->d_class);
+        c->d_class = nullptr;
+        c->class_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_class, npx * 4));
+        c->class_bytes = npx * 4;
+    }
+    if (c->order_cap < n_t) {
+        free_dev(c->d_order);
+        c->d_order = nullptr;
+        c->order_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_order, n_t * sizeof(uint32_t)));
+        c->order_cap = n_t;
+    }
     RtTriLaunch pa = a;
-    pa.probe_n = c->probe_n;
-    const int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
+    pa.probe_n = kProbeN;
+    const uint32_t pn2 = kProbeN * kProbeN;
+    int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
-    std::vector<uint32_t> f(npx);
-    HIPCHK(c, hipMemcpyAsync(f.data(), c->d_flags, npx * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    e = rt_sched_order(c->sched, c->d_flags, W, hl, pn2, (uint32_t)c->lights.size(), c->max_depth, c->d_order, st);
+    if (e) return hip_fail(c, (hipError_t)e, "tile order");
+    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, st);
+    if (e) return hip_fail(c, (hipError_t)e, "box-pixel scan");
+    /* Deferral shortens the box chains but moves their shadow queries into a second launch
+       that cannot use the tail of the first: it pays where the chains set the frame time (a
+       tile with few pixels per lane) of a many-sample frame, not on a full frame (dragon
+       1920x1080: 161.7 -> 173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) nor on short
+       chains (bunny class 1024^2 at 1 spp: 0.95 -> 1.35 ms, r02u).  (r02z, with the candidate
+       lists: the 2-way dragon tile, 1.04M pixels, 65.5 ms deferred against 60.7 inline; the
+       4-way 39 vs 46 ms, the 8-way 30 vs 44 ms: the line sits below two pixels per resident
+       lane.) */
+    const uint64_t lanes = (uint64_t)blocks * RT_BLOCK;
+    const bool use = c->defer == 1 || (c->defer < 0 && npx < 2 * lanes && c->sample_rate >= 4);
+    const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
     const uint64_t nl = c->lights.size();
-    uint64_t hit_steps = 0, n_hit = 0;
-    const uint64_t pn2 = (uint64_t)c->probe_n * c->probe_n;
-    for (uint32_t v : f) {
-        hit_steps += v & RT_PROBE_STEP_MASK;
-        n_hit += v >> RT_PROBE_HIT_SHIFT;
+    const uint64_t recs = spp * nd * nl; /* records per slot */
+    uint64_t max_slots = 0;
+    if (use && nl > 0 && spp > 0 && spp <= 1024 && recs > 0) {
+        const uint64_t bytes_per_slot = recs * (32 + 1 + 4) + spp * nd + 4;
+        max_slots = ((uint64_t)c->defer_mb << 20) / bytes_per_slot;
+        max_slots = std::min<uint64_t>(max_slots, 0xffffffffull / recs);
     }
-    /* mean steps of one probed query (a hit ray's closest-hit + shadow queries, or a missing
-       ray's closest-hit query, in the sums) */
-    double q_steps = n_hit ? (double)hit_steps / (double)(n_hit * (1 + nl) + (pn2 * npx - n_hit)) : 20.0;
-    if (q_steps < 1.0) q_steps = 1.0;
-    double box_factor = 1.4;
-    if (const char *v = getenv("RT_PROBE_BOX_FACTOR")) box_factor = atof(v); /* tuning knob */
-    /* one probe ray that misses stands for a box path: (1 + lights) x (maxDepth + 1) queries */
-    const double c_box = (double)((1 + nl) * (uint64_t)(c->max_depth + 1)) * q_steps * box_factor;
-    /* tile key: a blend of its most expensive pixel (a pixel is a serial chain: the tile's
-       last lane finishes with it) and its total (RT_LPT_MAX: weight of the maximum) */
-    double w_max = 0.75;
-    if (const char *v = getenv("RT_LPT_MAX")) w_max = atof(v); /* tuning knob */
-    std::vector<double> cost(n_t, 0.0), cmax(n_t, 0.0);
-    for (uint32_t y = 0; y < hl; ++y)
-        for (uint32_t x = 0; x < W; ++x) {
-            const uint32_t v = f[(size_t)y * W + x];
-            const double pc = ((double)(v & RT_PROBE_STEP_MASK) +
-                               (double)(pn2 - (v >> RT_PROBE_HIT_SHIFT)) * c_box) * (4.0 / (double)pn2) + 1.0;
-            const uint32_t t = (y / 8) * tx + x / 8;
-            cost[t] += pc;
-            cmax[t] = std::max(cmax[t], pc);
+    uint64_t n = 0;
+    if (max_slots) {
+        uint32_t n_box = 0; /* the one host read: the buffers are sized to the box pixels */
+        HIPCHK(c, hipMemcpyAsync(&n_box, c->sched.scan + npx, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        n = std::min<uint64_t>(n_box, max_slots);
+        if (n) {
+            const int r = ensure_defer(c, n, recs, spp * nd);
+            if (r != RT_OK) return r;
         }
-    if (w_max > 0.0) /* measured: 0 -> 0.5 / 1.0: 178.4 -> 173.7 / 174.0 ms per dragon frame */
-        for (uint32_t t = 0; t < n_t; ++t) cost[t] = (1.0 - w_max) * cost[t] / 64.0 + w_max * cmax[t];
-    std::vector<uint32_t> o(n_t);
-    for (uint32_t i = 0; i < n_t; ++i) o[i] = i;
-    std::stable_sort(o.begin(), o.end(), [&](uint32_t p, uint32_t q) { return cost[p] > cost[q]; });
-    {
-        const int r = classify_pixels(c, f, W, hl, (uint64_t)blocks * RT_BLOCK, st);
-        if (r != RT_OK) return r;
     }
-    free_dev(c->d_order);
-    c->d_order = nullptr;
-    HIPCHK(c, hipMalloc(&c->d_order, n_t * sizeof(uint32_t)));
-    HIPCHK(c, hipMemcpyAsync(c->d_order, o.data(), n_t * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    e = rt_sched_classify(c->sched, (uint32_t)npx, (uint32_t)n, c->d_class, c->d_defer_pixel, st);
+    if (e) return hip_fail(c, (hipError_t)e, "pixel classes");
+    c->n_defer = (uint32_t)n;
     c->order_key = key;
+    c->schedule_rebuilt = true;
     return RT_OK;
 }
 
@@ -574,15 +553,12 @@ int rt_create(int device, rt_ctx **out)
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) c->view[i][j] = (i == j) ? 1.0f : 0.0f;
     c->rng.seed(1);
-    if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0"; /* A/B knob */
-    if (const char *v = getenv("RT_FETCH_K")) c->fetch_k = (uint32_t)std::max(1, std::min(64, atoi(v))); /* tuning knob */
-    if (const char *v = getenv("RT_PROBE_N")) c->probe_n = (uint32_t)std::max(1, std::min(5, atoi(v)));
-    if (const char *v = getenv("RT_FETCH_K_BOX")) c->fetch_k_box = (uint32_t)std::max(1, std::min(64, atoi(v)));
-    if (const char *v = getenv("RT_FETCH_FRAC")) c->fetch_frac = (uint32_t)std::max(0, std::min(64, atoi(v)));
-    if (const char *v = getenv("RT_BOX_EXIT")) c->box_exit = atoi(v) != 0;
-    if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0; /* A/B knob */
-    if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0; /* A/B knob */
+    /* A/B and capacity knobs (none changes a result bit) */
+    if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0";
+    if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
+    if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
+    if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evm) != hipSuccess ||
@@ -617,6 +593,9 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
     free_dev(c->d_lists);
+    free_dev(c->d_list_first);
+    free_dev(c->d_list_alloc);
+    rt_sched_free(c->sched);
     free_dev(c->d_seeds);
     free_dev(c->d_work);
     free_dev(c->d_counters);
@@ -961,36 +940,46 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.work_counter = c->d_work;
         a.counters = c->d_counters;
         const int trav = trav_kind(c);
-        int blocks = 0;
-        const int r = grid_blocks(c, trav, c->counting, false, &blocks);
-        if (r != RT_OK) return r;
         const uint64_t items = (uint64_t)((W + 7) / 8) * ((hl + 7) / 8) * 64;
-        if (const char *v = getenv("RT_GRID_PCT")) /* A/B knob: persistent grid as a share of full occupancy */
-            blocks = std::max(1, blocks * std::max(1, std::min(100, atoi(v))) / 100);
-        blocks = (int)std::min<uint64_t>((uint64_t)blocks, (items + RT_BLOCK - 1) / RT_BLOCK);
-        if (blocks < 1) blocks = 1;
+        const uint64_t item_blocks = (items + RT_BLOCK - 1) / RT_BLOCK;
+        /* persistent grids: the plain form's and the deferred-shadow form's own occupancy
+           (RT_TRIS_WAVES_DEFER), each at most one block per RT_BLOCK queue items */
+        int blocks = 0, blocks_defer = 0;
+        int r = grid_blocks(c, trav, c->counting, false, &blocks);
+        if (r != RT_OK) return r;
+        blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks, item_blocks));
+        if (trav == RT_TRAV_BVH4Q) {
+            r = grid_blocks(c, trav, c->counting, true, &blocks_defer);
+            if (r != RT_OK) return r;
+            blocks_defer = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks_defer, item_blocks));
+        }
+        /* the spill area is indexed by blockIdx: sized for the larger of the grids any kernel of
+           this render (probe, k_tris in either form, k_defer_shadow) may run with */
         a.spill_cap = spill_cap(c);
         if (a.spill_cap) {
-            const int rs = ensure_spill(c, (size_t)blocks * RT_BLOCK * a.spill_cap);
+            const int rs = ensure_spill(c, (size_t)std::max(blocks, blocks_defer) * RT_BLOCK * a.spill_cap);
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
-        a.fetch_k = c->fetch_k;
-        a.fetch_k_box = c->fetch_k_box;
-        a.fetch_frac = c->fetch_frac;
-        a.box_exit = c->box_exit;
+        a.fetch_k = kFetchK;
+        a.fetch_k_box = kFetchK;
+        a.fetch_frac = kFetchFrac;
+        a.box_exit = 0;
+        a.probe_n = kProbeN;
         a.tile_order = nullptr;
         a.pixel_flags = nullptr;
         a.pixel_class = nullptr;
         a.n_defer = 0;
+        const auto h0 = std::chrono::steady_clock::now();
+        c->schedule_rebuilt = false;
         if (c->schedule) {
             const int ro = tile_order(c, a, blocks, st);
             if (ro != RT_OK) return ro;
             a.tile_order = c->d_order;
             a.pixel_flags = a.tile_order ? c->d_flags : nullptr;
             a.pixel_class = a.tile_order ? c->d_class : nullptr;
-            a.probe_n = c->probe_n;
-            if (a.pixel_class && c->n_defer) {
+            /* only the compressed tree's kernel form records deferred shadow rays */
+            if (a.pixel_class && c->n_defer && trav == RT_TRAV_BVH4Q) {
                 a.n_defer = c->n_defer;
                 a.defer_rec = c->d_defer_rec;
                 a.defer_seg = c->d_defer_seg;
@@ -999,17 +988,15 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 a.defer_qcount = c->d_defer_qcount;
                 a.defer_pixel = c->d_defer_pixel;
                 HIPCHK(c, hipMemsetAsync(c->d_defer_qcount, 0, 2 * sizeof(uint32_t), st));
-                /* the deferred form's own occupancy (RT_TRIS_WAVES_DEFER) */
-                int bd = 0;
-                const int rd = grid_blocks(c, trav, c->counting, true, &bd);
-                if (rd != RT_OK) return rd;
-                blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)bd, (items + RT_BLOCK - 1) / RT_BLOCK));
+                blocks = blocks_defer;
             }
         }
+        const double sched_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
-            fprintf(stderr, "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p\n", (void *)c,
-                    trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order);
+            fprintf(stderr, "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p, defer %u\n",
+                    (void *)c, trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order,
+                    a.n_defer);
         /* diagnostics: per-pixel start/finish clocks (+ queries, steps and the wall clocks
            by phase in a counting launch: 8 x u32 per pixel), dumped raw to $RT_PIXEL_STATS */
         const char *stats_path = getenv("RT_PIXEL_STATS");
@@ -1020,35 +1007,48 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             HIPCHK(c, hipMemsetAsync(d_stats, 0, (size_t)W * hl * 32, st));
             a.pixel_stats = d_stats;
         }
-        /* camera-ray candidate lists (k_pixel_lists, rebuilt every frame): list slots after the
-           mesh's triangle records, one count per pixel */
+        /* camera-ray candidate lists (k_pixel_lists, rebuilt every frame): a compacted list area
+           after the mesh's triangle records in the same buffer (a list block is a leaf code like
+           any other), a count and a first slot per pixel.  Leaf codes address slots below 2^28;
+           pixels whose list does not fit the area (RT_LIST_MB) take the tree, and a list area
+           that cannot be allocated turns the lists off for the render — same bits either way. */
         a.pixel_lists = nullptr;
         const bool bvh4 = c->d_nodes4 && (trav == RT_TRAV_BVH4Q || trav == RT_TRAV_BVH4);
         const uint64_t kept = c->n_tris;
-        a.list_base = (uint32_t)kept;
-        const uint64_t list_recs = (uint64_t)W * hl * RT_LIST_MAX;
-        const bool lists = (c->pixel_lists == 1 || (c->pixel_lists < 0 && c->sample_rate >= 4)) && bvh4 &&
-                           kept + list_recs < (1ull << 28);
+        const uint64_t npx = (uint64_t)W * hl;
+        uint64_t list_cap = std::min<uint64_t>(npx * RT_LIST_MAX, ((uint64_t)c->list_mb << 20) / 48);
+        list_cap = std::min<uint64_t>(list_cap, kept < (1ull << 28) ? (1ull << 28) - 1 - kept : 0);
+        bool lists = (c->pixel_lists == 1 || (c->pixel_lists < 0 && c->sample_rate >= 4)) && bvh4 && list_cap > 0;
+        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), kept, st) != RT_OK) {
+            (void)hipGetLastError(); /* out of device memory: no lists this render */
+            lists = false;
+        }
+        if (lists && c->lists_bytes < npx) {
+            free_dev(c->d_lists);
+            free_dev(c->d_list_first);
+            c->d_lists = nullptr;
+            c->d_list_first = nullptr;
+            c->lists_bytes = 0;
+            HIPCHK(c, hipMalloc(&c->d_lists, npx));
+            HIPCHK(c, hipMalloc(&c->d_list_first, npx * sizeof(uint32_t)));
+            c->lists_bytes = npx;
+        }
+        if (lists && !c->d_list_alloc) HIPCHK(c, hipMalloc(&c->d_list_alloc, sizeof(uint32_t)));
         if (lists) {
-            const int r = ensure_tris_capacity(c, (size_t)(kept + list_recs), kept, st);
-            if (r != RT_OK) return r;
-            if (c->lists_bytes < (size_t)W * hl) {
-                free_dev(c->d_lists);
-                c->d_lists = nullptr;
-                c->lists_bytes = 0;
-                HIPCHK(c, hipMalloc(&c->d_lists, (size_t)W * hl));
-                c->lists_bytes = (size_t)W * hl;
-            }
             a.pixel_lists = c->d_lists;
+            a.list_first = c->d_list_first;
+            a.list_base = (uint32_t)kept;
+            a.list_cap = (uint32_t)list_cap;
+            a.list_alloc = c->d_list_alloc;
         }
         a.tris = c->d_tris;
         HIPCHK(c, hipEventRecord(c->ev0, st));
         e = lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr, c->d_lists,
-                                          st)
+                                          c->d_list_first, st)
                   : 0;
         HIPCHK(c, hipEventRecord(c->evm, st));
         if (!e && lists && getenv("RT_LIST_STATS")) { /* diagnostics: candidate list lengths */
-            std::vector<uint8_t> h((size_t)W * hl);
+            std::vector<uint8_t> h((size_t)npx);
             HIPCHK(c, hipMemcpyAsync(h.data(), c->d_lists, h.size(), hipMemcpyDeviceToHost, st));
             HIPCHK(c, hipStreamSynchronize(st));
             uint64_t b[6] = {}, sum = 0, nl = 0;
@@ -1065,6 +1065,17 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         if (!e && a.n_defer) e = rt_launch_defer(a, c->counting, blocks, st);
         c->last_deferred = a.n_defer;
         HIPCHK(c, hipEventRecord(c->ev1, st));
+        c->info = rt_render_info{};
+        c->info.kernel = RT_KERNEL_TRIS;
+        c->info.traversal = (uint32_t)trav;
+        c->info.grid_blocks = (uint32_t)blocks;
+        c->info.lists = lists ? 1u : 0u;
+        c->info.list_capacity = lists ? list_cap : 0;
+        c->info.list_pixels_tree = lists ? (uint32_t)npx : 0u; /* pixel count until rt_last_render_info reads the counts */
+        c->info.pixels_deferred = a.n_defer;
+        c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
+        c->info.schedule_host_ms = sched_ms;
+        c->info_list_pending = lists;
         if (d_stats) {
             std::vector<uint32_t> h((size_t)W * hl * 8);
             HIPCHK(c, hipMemcpyAsync(h.data(), d_stats, h.size() * 4, hipMemcpyDeviceToHost, st));
@@ -1098,6 +1109,9 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         HIPCHK(c, hipEventRecord(c->evm, st));
         e = rt_launch_spheres(a, kernel == RT_KERNEL_SPHERES_SS, st);
         HIPCHK(c, hipEventRecord(c->ev1, st));
+        c->info = rt_render_info{};
+        c->info.kernel = (uint32_t)kernel;
+        c->info_list_pending = false;
     }
     if (e) return hip_fail(c, (hipError_t)e, "kernel launch");
     c->have_timing = true;
@@ -1195,6 +1209,27 @@ int rt_read(rt_ctx *c, float *host, size_t n_floats)
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(host, c->last_out, c->last_bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_last_render_info(rt_ctx *c, rt_render_info *out)
+{
+    if (!c || !out) return RT_ERR_ARG;
+    if (c->info_list_pending) { /* how much of the list area the render's lists took */
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        uint32_t used = 0;
+        HIPCHK(c, hipMemcpy(&used, c->d_list_alloc, sizeof(used), hipMemcpyDeviceToHost));
+        c->info.list_records = std::min<uint64_t>(used, c->info.list_capacity);
+        const size_t npx = c->info.list_pixels_tree; /* pixels of the launch, set below */
+        std::vector<uint8_t> h(npx);
+        if (npx) HIPCHK(c, hipMemcpy(h.data(), c->d_lists, npx, hipMemcpyDeviceToHost));
+        uint32_t tree = 0;
+        for (uint8_t v : h) tree += v == RT_LIST_NONE ? 1u : 0u;
+        c->info.list_pixels_tree = tree;
+        c->info_list_pending = false;
+    }
+    *out = c->info;
     return RT_OK;
 }
 

@@ -155,10 +155,15 @@ struct RtTriLaunch {
     const uint32_t *defer_pixel; /* per slot: yl * W + x */
     uint32_t n_defer;           /* slots in use */
     /* Camera-ray candidate lists (k_pixel_lists): per pixel the triangles any of its sample
-       rays could accept, RT_LIST_MAX at most, their records copied to triangle slots
-       list_base + pixel * RT_LIST_MAX + i; pixel_lists[pixel] = count, RT_LIST_NONE = no list */
+       rays could accept, RT_LIST_MAX at most, their records copied, compacted, into the triangle
+       buffer's slots [list_base, list_base + list_cap) (a wave-aggregated allocator, list_alloc);
+       pixel_lists[pixel] = count (RT_LIST_NONE: no list, the pixel's camera rays take the tree),
+       list_first[pixel] = its first slot */
     const uint8_t *pixel_lists;
+    const uint32_t *list_first;
     uint32_t list_base;
+    uint32_t list_cap;
+    uint32_t *list_alloc;
 };
 #ifndef RT_LIST_MAX
 #define RT_LIST_MAX 32
@@ -195,9 +200,27 @@ int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *str
    records in the triangle buffer at a.list_base); nodes4 = full-precision 4-wide tree,
    q4 = compressed nodes (their normal boxes; may be NULL). */
 int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint8_t *counts,
-                          void *stream);
-/* Scheduling probe: per-pixel "primary ray hits the mesh" flags (rt_kernels.hip). */
+                          uint32_t *first, void *stream);
+/* Scheduling probe: per pixel the mesh hits of a grid of probe rays and the traversal steps of
+   their queries (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
+/* The pixel-queue schedule from the probe, on the device (rt_sched.hip): LPT tile order, box
+   flags and their exclusive scan, pixel classes with deferred-shadow slots. */
+struct RtSchedScratch {
+    void *tmp = nullptr; /* hipCUB temporary storage */
+    size_t tmp_bytes = 0;
+    float *keys = nullptr, *keys_sorted = nullptr;
+    uint32_t *idx = nullptr;
+    uint32_t *box = nullptr, *scan = nullptr; /* npx + 1 entries: scan[npx] = box pixels */
+    unsigned long long *sums = nullptr;       /* probe steps, probe hits */
+    uint32_t cap_tiles = 0, cap_px = 0;
+};
+void rt_sched_free(RtSchedScratch &s);
+int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_t hl, uint32_t pn2, uint32_t n_lights,
+                   uint32_t max_depth, uint32_t *order, void *stream);
+int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, void *stream);
+int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *defer_pixel,
+                      void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed
    buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,

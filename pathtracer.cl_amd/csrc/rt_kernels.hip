@@ -991,7 +991,7 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                     if (!shadow && depth == 0 && a.pixel_lists) { /* a camera ray: the pixel's candidate list */
                         const uint32_t pix = yl * a.W + x;
                         const uint32_t pc = a.pixel_lists[pix];
-                        const uint32_t first = a.list_base + pix * RT_LIST_MAX;
+                        const uint32_t first = a.list_first[pix];
                         if (pc == 0) { /* no triangle can be accepted by any of the pixel's camera rays */
                             running = false;
                             ts.best = -1;
@@ -1614,43 +1614,95 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                              const float4 *__restrict__ tris, const Frustum &f, int *slots, float *keys, uint32_t cap,
                              uint32_t &n, lds_int *stack);
 
+/* The component-wise box of the unit directions normalize(view + right a + up b) over a pixel's
+   square a in [ax, ax + 1], b in [by, by + 1] (strat_rand offsets, raytracer.cl:216-224).  The
+   four corner rays (camera_dir, the kernel's own float arithmetic) span it only up to the
+   curvature of the normalisation: an interior direction leaves the corners' box by about
+   1 / (8 L^2), L = (W / 2) / tan(fov / 2) (2e-5 at W = 64).  Bound: d = v / |v| has
+   |D^2 d[w, w]| <= 6 |w|^2 / |v|^2, and a C^2 function on the unit square differs from the
+   bilinear interpolation of its corners (whose range is the corners' box) by at most
+   (1/8)(max |d_aa| + max |d_bb|) = 0.75 (|right|^2 + |up|^2) / min|v|^2, with min|v| over the
+   square at least the smallest corner |v| less |right| + |up|.  The pad on top covers the
+   float evaluation of camera_dir (a few ulp of a unit vector). */
+__device__ __forceinline__ void pixel_dir_box(const rt_camera &cam, float ax, float by, double dlo[3], double dhi[3])
+{
+    double nmin = 1e300;
+    for (int k = 0; k < 3; ++k) {
+        dlo[k] = 1e300;
+        dhi[k] = -1e300;
+    }
+    for (int c = 0; c < 4; ++c) {
+        const float a = ax + (float)(c & 1), b = by + (float)(c >> 1);
+        const V3 d = camera_dir(cam, a, b);
+        const double dv[3] = {d.x, d.y, d.z};
+        for (int k = 0; k < 3; ++k) {
+            dlo[k] = fmin(dlo[k], dv[k]);
+            dhi[k] = fmax(dhi[k], dv[k]);
+        }
+        const double vx = (double)cam.view.x + (double)cam.right.x * a + (double)cam.up.x * b;
+        const double vy = (double)cam.view.y + (double)cam.right.y * a + (double)cam.up.y * b;
+        const double vz = (double)cam.view.z + (double)cam.right.z * a + (double)cam.up.z * b;
+        nmin = fmin(nmin, sqrt(vx * vx + vy * vy + vz * vz));
+    }
+    const double r2 = (double)cam.right.x * cam.right.x + (double)cam.right.y * cam.right.y +
+                      (double)cam.right.z * cam.right.z;
+    const double u2 = (double)cam.up.x * cam.up.x + (double)cam.up.y * cam.up.y + (double)cam.up.z * cam.up.z;
+    nmin -= sqrt(r2) + sqrt(u2);
+    const double bulge = nmin > 1e-3 ? 0.75 * (r2 + u2) / (nmin * nmin) : 2.0; /* 2: the whole direction range */
+    const double pad = 1e-5 + bulge;
+    for (int k = 0; k < 3; ++k) {
+        dlo[k] -= pad;
+        dhi[k] += pad;
+    }
+}
+
 __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const float *__restrict__ nodes4,
-                                                          const uint32_t *__restrict__ q4, uint8_t *__restrict__ counts)
+                                                          const uint32_t *__restrict__ q4, uint8_t *__restrict__ counts,
+                                                          uint32_t *__restrict__ firsts)
 {
     /* one wave per 8 x 8 pixel tile: neighbouring frusta walk the same nodes */
     __shared__ int s_fstack[kFrustumStack * RT_BLOCK];
     const uint32_t item = blockIdx.x * RT_BLOCK + threadIdx.x, tiles_x = (a.W + 7u) / 8u;
     const uint32_t tile = item >> 6, in = item & 63u;
     const uint32_t x = (tile % tiles_x) * 8u + (in & 7u), yl = (tile / tiles_x) * 8u + (in >> 3);
-    if (x >= a.W || yl >= a.Hl) return;
+    const bool valid = x < a.W && yl < a.Hl;
     const uint32_t p = yl * a.W + x;
-    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
-    const float hw = ((float)a.W) / 2.0f, hh = ((float)a.H) / 2.0f;
-    double dlo[3] = {1e300, 1e300, 1e300}, dhi[3] = {-1e300, -1e300, -1e300};
-    for (int c = 0; c < 4; ++c) {
-        const V3 d = camera_dir(a.cam, (float)(x + (c & 1)) - hw, (float)(y + (c >> 1)) - hh);
-        const double dv[3] = {d.x, d.y, d.z};
-        for (int k = 0; k < 3; ++k) {
-            dlo[k] = fmin(dlo[k], dv[k]);
-            dhi[k] = fmax(dhi[k], dv[k]);
-        }
-    }
-    Frustum f;
-    for (int k = 0; k < 3; ++k) {
-        f.dlo[k] = dlo[k] - 1e-5;
-        f.dhi[k] = dhi[k] + 1e-5;
-        f.o[k] = k == 0 ? a.cam.position.x : k == 1 ? a.cam.position.y : a.cam.position.z;
-    }
-    frustum_init(f);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
-    float4 *__restrict__ lst = const_cast<float4 *>(tris) + 3ull * (a.list_base + (size_t)p * RT_LIST_MAX);
     int slot[RT_LIST_MAX];
     float key[RT_LIST_MAX];
     uint32_t n = 0;
-    const bool ok = frustum_list(nodes4, q4, tris, f, slot, key, RT_LIST_MAX, n,
-                                 (lds_int *)(s_fstack + threadIdx.x));
+    bool ok = false;
+    if (valid) {
+        const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+        /* a = fa - W/2 with fa in [x, x + 1] (the kernel's float subtraction, exact at these
+           magnitudes), likewise b */
+        const float ax = (float)x - ((float)a.W) / 2.0f, by = (float)y - ((float)a.H) / 2.0f;
+        Frustum f;
+        pixel_dir_box(a.cam, ax, by, f.dlo, f.dhi);
+        for (int k = 0; k < 3; ++k) f.o[k] = k == 0 ? a.cam.position.x : k == 1 ? a.cam.position.y : a.cam.position.z;
+        frustum_init(f);
+        ok = frustum_list(nodes4, q4, tris, f, slot, key, RT_LIST_MAX, n, (lds_int *)(s_fstack + threadIdx.x));
+    }
+    /* compacted list storage: the wave's lists are allocated together (one atomic), in lane order */
+    const uint32_t want = ok ? n : 0u;
+    const int lane = (int)(threadIdx.x & 63u);
+    uint32_t incl = want;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    uint32_t base = 0;
+    if (lane == 0 && total) base = atomicAdd(a.list_alloc, total);
+    base = __shfl(base, 0);
+    const uint32_t off = base + incl - want;
+    /* no room left in the list area: the pixel's camera rays take the tree */
+    if (ok && (uint64_t)off + n > a.list_cap) ok = false;
+    if (!valid) return;
     counts[p] = ok ? (uint8_t)n : (uint8_t)RT_LIST_NONE;
+    firsts[p] = a.list_base + off;
     if (!ok) return;
+    float4 *__restrict__ lst = const_cast<float4 *>(tris) + 3ull * (a.list_base + (size_t)off);
     /* The records in order of their earliest accept t, each one's r1.w carrying the NEXT
        record's bound (+inf on the last): a closest-hit query whose best t is already below
        it has its answer (trav_step_q ends the list there — the accept rule needs t < best_t,
@@ -1881,12 +1933,15 @@ int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *str
     return (int)hipGetLastError();
 }
 
-int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint8_t *counts, void *stream)
+int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint8_t *counts,
+                          uint32_t *first, void *stream)
 {
     const uint32_t items = ((a.W + 7u) / 8u) * ((a.Hl + 7u) / 8u) * 64u;
     if (!a.W || !a.Hl) return 0;
+    hipError_t e = hipMemsetAsync(a.list_alloc, 0, sizeof(uint32_t), (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_pixel_lists, dim3((items + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0, (hipStream_t)stream,
-                       a, nodes4, q4, counts);
+                       a, nodes4, q4, counts, first);
     return (int)hipGetLastError();
 }
 

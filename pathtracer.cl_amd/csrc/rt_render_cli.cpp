@@ -9,7 +9,10 @@
  *             [--sample-rate S] [--depth D] [--mesh N_TRIS | --ply FILE] [--linear]
  *             [--raw out.f32] [--pfm out.pfm] [--device K]
  *             [--events d,d,l,d,m:5:-3,s:64:32,d,...]   (interactive replay: ProgressiveViewHIP
- *              display / arrow keys l r u n / drag motion / reshape, GlutCLWindow.cpp:136-301)
+ *              display / arrow keys l r u n / drag motion / reshape, GlutCLWindow.cpp:136-301;
+ *              one JSON line per event on stdout: the view state and whether a redisplay was
+ *              posted) [--max-progression N] [--frames-out FILE]   (every displayed frame,
+ *              appended as raw RGBA32F)
  *             [--tile STRIPE,N,R]   (this process renders rank R's row stripes of N: the raw output
  *              is the compact tile — the sharding path rehearsed as separate processes)
  *             [--comm-ranks N --comm-rank R --comm-id FILE]   (native multi-GPU: one process per
@@ -122,8 +125,8 @@ bool share_comm_id(const std::string &path, int rank, uint8_t id[RT_COMM_ID_BYTE
 
 int main(int argc, char **argv)
 {
-    std::string scene = "main", raw, pfm, ply_path, events, comm_id;
-    unsigned W = 512, H = 512, frames = 1, sr = 1, depth = 6, n_tris = 0;
+    std::string scene = "main", raw, pfm, ply_path, events, comm_id, frames_out;
+    unsigned W = 512, H = 512, frames = 1, sr = 1, depth = 6, n_tris = 0, max_prog = 10000;
     int device = 0, comm_ranks = 0, comm_rank = 0;
     rt_tile tile{8, 1, 0};
     bool linear = false;
@@ -145,6 +148,8 @@ int main(int argc, char **argv)
         else if (a == "--mesh") n_tris = (unsigned)std::atoi(v);
         else if (a == "--ply") ply_path = v;
         else if (a == "--events") events = v;
+        else if (a == "--max-progression") max_prog = (unsigned)std::atoi(v);
+        else if (a == "--frames-out") frames_out = v;
         else if (a == "--raw") raw = v;
         else if (a == "--pfm") pfm = v;
         else if (a == "--device") device = std::atoi(v);
@@ -179,24 +184,39 @@ int main(int argc, char **argv)
         }
         if (!events.empty()) { /* interactive replay through the display state machine */
             ProgressiveViewHIP view(rt, W, H, kernel);
+            view.setProgressive(max_prog);
+            FILE *fo = frames_out.empty() ? nullptr : std::fopen(frames_out.c_str(), "wb");
+            if (!frames_out.empty() && !fo) return 1;
             size_t pos = 0;
             while (pos <= events.size()) {
                 const size_t end = std::min(events.find(',', pos), events.size());
                 const std::string ev = events.substr(pos, end - pos);
                 pos = end + 1;
                 if (ev.empty()) continue;
-                if (ev == "d") view.display();
-                else if (ev == "l") view.specialKey(ProgressiveViewHIP::KEY_LEFT);
-                else if (ev == "r") view.specialKey(ProgressiveViewHIP::KEY_RIGHT);
-                else if (ev == "u") view.specialKey(ProgressiveViewHIP::KEY_UP);
-                else if (ev == "n") view.specialKey(ProgressiveViewHIP::KEY_DOWN);
+                bool post = false, traced = false;
+                if (ev == "d") {
+                    post = view.display();
+                    traced = view.rendered();
+                    if (traced && fo) {
+                        const std::vector<float> &px = view.pixels();
+                        if (std::fwrite(px.data(), 4, px.size(), fo) != px.size()) return 1;
+                    }
+                } else if (ev == "l") post = view.specialKey(ProgressiveViewHIP::KEY_LEFT);
+                else if (ev == "r") post = view.specialKey(ProgressiveViewHIP::KEY_RIGHT);
+                else if (ev == "u") post = view.specialKey(ProgressiveViewHIP::KEY_UP);
+                else if (ev == "n") post = view.specialKey(ProgressiveViewHIP::KEY_DOWN);
                 else if (ev[0] == 'm' || ev[0] == 's') {
                     int a1 = 0, a2 = 0;
                     if (std::sscanf(ev.c_str() + 1, ":%d:%d", &a1, &a2) != 2) return usage();
-                    if (ev[0] == 'm') view.motion(a1, a2);
+                    if (ev[0] == 'm') post = view.motion(a1, a2);
                     else view.reshape((unsigned)a1, (unsigned)a2);
                 } else return usage();
+                std::printf("{\"event\": \"%s\", \"rendered\": %s, \"redisplay\": %s, \"progression\": %u, "
+                            "\"azimuth\": %.9g, \"elevation\": %.9g, \"width\": %u, \"height\": %u}\n",
+                            ev.c_str(), traced ? "true" : "false", post ? "true" : "false", view.progression(),
+                            view.azimuth(), view.elevation(), view.width(), view.height());
             }
+            if (fo) std::fclose(fo);
             std::printf("{\"progression\": %u, \"azimuth\": %.9g, \"elevation\": %.9g, \"width\": %u, "
                         "\"height\": %u}\n",
                         view.progression(), view.azimuth(), view.elevation(), view.width(), view.height());

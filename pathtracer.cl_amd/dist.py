@@ -178,6 +178,34 @@ def seed_halo_plan_native(writer: np.ndarray, height: int, hpad: int, stripe: in
     return src[:n], dst[:n], rows[:n]
 
 
+def seed_halo_peer_blocks(src, dst, rows, n_ranks: int, me: int):
+    """rt_seed_halo_peer_blocks (librtmi, host only): rank `me`'s side of a halo plan — the rows
+    it sends to and receives from each peer, one block per peer in peer order.  Returns
+    (send: list of per-peer row arrays, recv: list of per-peer row arrays)."""
+    from . import _abi
+
+    lib = _abi.load()
+    k = len(src)
+    s_ = np.ascontiguousarray(src, np.uint32)
+    d_ = np.ascontiguousarray(dst, np.uint32)
+    r_ = np.ascontiguousarray(rows, np.uint32)
+    send_rows = np.empty(max(k, 1), np.uint32)
+    recv_rows = np.empty(max(k, 1), np.uint32)
+    send_cnt = np.empty(n_ranks, np.uint32)
+    recv_cnt = np.empty(n_ranks, np.uint32)
+    st = lib.rt_seed_halo_peer_blocks(_abi.ptr(s_), _abi.ptr(d_), _abi.ptr(r_), k, n_ranks, me, _abi.ptr(send_rows),
+                                      _abi.ptr(send_cnt), _abi.ptr(recv_rows), _abi.ptr(recv_cnt))
+    if st != _abi.RT_OK:
+        raise _abi.RtError(st, "rt_seed_halo_peer_blocks")
+    send, recv, so, ro = [], [], 0, 0
+    for p in range(n_ranks):
+        send.append(send_rows[so:so + send_cnt[p]].copy())
+        recv.append(recv_rows[ro:ro + recv_cnt[p]].copy())
+        so += int(send_cnt[p])
+        ro += int(recv_cnt[p])
+    return send, recv
+
+
 class NativeComm:
     """librtmi's RCCL communicator (rt_comm_*; one per rank and GPU).
 
@@ -237,6 +265,12 @@ class NativeComm:
 
     def reset_halo(self) -> None:
         self._check(self._lib.rt_comm_reset_halo(self._h), "rt_comm_reset_halo")
+
+    def count(self) -> int:
+        """ncclCommCount: the ranks RCCL sees in this communicator."""
+        n = self._abi.ctypes.c_int(0)
+        self._check(self._lib.rt_comm_count(self._h, self._abi.ctypes.byref(n)), "rt_comm_count")
+        return n.value
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -255,6 +255,13 @@ class RayTracer:
                     "rt_last_kernel_split_ms")
         return pre.value, main.value
 
+    def renderInfo(self) -> dict:
+        """rt_last_render_info: the last render's lists, deferral and schedule (no result depends
+        on any of it)."""
+        i = _abi.RtRenderInfo()
+        self._check(self._lib.rt_last_render_info(self._h, ctypes.byref(i)), "rt_last_render_info")
+        return {f: getattr(i, f) for f, _ in _abi.RtRenderInfo._fields_ if f != "reserved"}
+
     def traceRays(self, rays: np.ndarray, any_hit: bool = False) -> tuple[np.ndarray, np.ndarray]:
         r = np.ascontiguousarray(rays, _abi.RAY_DTYPE)
         idx = np.empty(r.size, np.int32)

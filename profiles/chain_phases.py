@@ -3,7 +3,7 @@ pixel, the clocks of the loop phases while the pixel was live (D path advance, A
 ray, C stepping rounds), its loop iterations, queries and traversal steps.  Prints the costliest
 pixels of (a) row 81 rendered alone and (b) the full dragon frame.
 
-    RT_FETCH_FRAC=24 python profiles/chain_phases.py
+    python profiles/chain_phases.py
 """
 import json
 import os

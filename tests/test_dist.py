@@ -202,3 +202,66 @@ def test_native_halo_plan_equals_python(pt, H, hpad, stripe, n):
         halo.commit(s)
         np.testing.assert_array_equal(writer, halo.writer)
     assert total > 0
+
+
+# (kernel, progression) sequences of rt_comm_render calls: progressive sphere frames with
+# restarts, interleaved with raytrace_ss / raytrace_tris frames (unshifted seed rows)
+_COMM_SEQUENCE = [(0, 0), (0, 1), (0, 2), (0, 3), (2, 0), (0, 4), (0, 5), (1, 0), (0, 0), (0, 1), (2, 0),
+                  (2, 0), (0, 1), (0, 9), (1, 0), (0, 2)]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("H,hpad,stripe", [(61, 64, 8), (45, 48, 4)])
+def test_native_comm_render_block_plan_replay(pt, n, H, hpad, stripe):
+    """rt_comm_render's halo step, replayed on the host for N ranks (csrc/rt_comm.hip): every rank
+    plans with rt_seed_halo_plan, splits the plan into per-peer blocks with
+    rt_seed_halo_peer_blocks and packs its send block to each peer; peer p unpacks what it
+    receives from rank q in the order of its own receive block.  The blocks must pair up (q's
+    block to p lists exactly p's rows from q, in the same order, so the packed buffers match
+    word for word), every row a rank reads must then hold the latest write of any rank
+    (dist.SeedHalo's contract), and the plan must equal SeedHalo.plan — for raytrace frames
+    (rows shifted by the progression) and for the unshifted kernels after them."""
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    halo = dist.SeedHalo(H, hpad, stripe, n)
+    writer = np.full(hpad, -1, np.int32)
+    truth = np.arange(hpad, dtype=np.int64) * 3 + 11
+    local = [truth.copy() for _ in range(n)]
+    moved = 0
+    for f, (kernel, prog) in enumerate(_COMM_SEQUENCE):
+        shift = prog if kernel == 0 else 0
+        if f > 0:  # the first frame on a communicator is "fresh": identical seeds everywhere
+            plan = halo.plan(shift)
+            src, dst, rows = dist.seed_halo_plan_native(writer, H, hpad, stripe, n, shift)
+            exp = [(a, b, int(r)) for (a, b), rr in plan.items() for r in rr]
+            assert list(zip(src.tolist(), dst.tolist(), rows.tolist())) == exp, (f, kernel, prog)
+            blocks = [dist.seed_halo_peer_blocks(src, dst, rows, n, me) for me in range(n)]
+            inbox = {}
+            for q in range(n):
+                send, _ = blocks[q]
+                for p_ in range(n):
+                    if len(send[p_]):
+                        inbox[(q, p_)] = (send[p_].copy(), local[q][send[p_].astype(np.int64)].copy())
+            for p_ in range(n):
+                _, recv = blocks[p_]
+                for q in range(n):
+                    if len(recv[q]) == 0:
+                        assert (q, p_) not in inbox
+                        continue
+                    rows_sent, packed = inbox.pop((q, p_))
+                    np.testing.assert_array_equal(rows_sent, recv[q])
+                    local[p_][recv[q].astype(np.int64)] = packed
+                    moved += len(recv[q])
+            assert not inbox
+        else:
+            # the native planner still records the first frame's writes (rt_comm_render commits)
+            dist.seed_halo_plan_native(writer, H, hpad, stripe, n, shift)
+        for y in range(H):
+            r = (y + shift) % hpad
+            k = halo.row_rank[y]
+            assert local[k][r] == truth[r], (f, kernel, prog, y, r)
+            truth[r] = local[k][r] = _write_value(r, f)
+        halo.commit(shift)
+        np.testing.assert_array_equal(writer, halo.writer)
+    assert moved > 0

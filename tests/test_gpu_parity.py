@@ -101,6 +101,70 @@ def test_spheres_vs_oracle_progressive(tracer, pt, oracle):
     rt.close()
 
 
+def test_sphere_config_full_size_progressive_vs_oracle(tracer, pt, oracle):
+    """BASELINE configs[1] at its own size: the built-in sphere scene at 1024x1024, 8
+    progressive frames (row-shifted seeds, mix 1/p) from the context's own glibc rand() seeds,
+    every frame and the final seed planes equal to the oracle's, bit for bit; ray counts too."""
+    sc = pt.scenes
+    W = H = 1024
+    Wp, Hp = sc.padded_dims(W, H)
+    S = sc.main_scene()
+    cam = sc.camera_spherical(W, **sc.MAIN_CAMERA)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(S)
+    c = sc.MAIN_CAMERA
+    rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+    rt.setSampleRate(1)
+    rt.setMaxPathDepth(6)
+    sd = sc.default_seeds(Wp, Hp)  # the stream a fresh context draws for its first size
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    for p in range(8):
+        rt.rayTrace(got, W, H, p, kernel=0)
+        c_or = oracle.render_spheres(exp, cam, S, W, H, Wp, Hp, 1, 6, p, sd)
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
+        cnt = rt.counters()
+        assert (cnt["rays_closest"], cnt["rays_shadow"]) == c_or
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
+    rt.close()
+
+
+def test_bunny_config_full_size_vs_oracle(tracer, pt, oracle):
+    """BASELINE configs[2] at its own size: the bunny-class mesh (69,451 triangles) at
+    1024x1024, 1 spp, BVH traversal, from the context's own seeds; a strided subset of 2,048
+    pixels (the oracle's linear loop) equals the GPU frame on those pixels and their seed slots,
+    and the GPU frame's other pixels are filled."""
+    sc = pt.scenes
+    W = H = 1024
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["bunny"])
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(S)
+    c = sc.PLY_CAMERA
+    rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+    rt.setSampleRate(1)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    got = np.zeros(W * H * 4, np.float32)
+    rt.rayTrace(got, W, H, 0, kernel=2)
+    s_got = rt.getSeeds()
+    rt.close()
+    sd = sc.default_seeds(Wp, Hp)
+    pix = (np.arange(2048, dtype=np.int64) * (W * H // 2048) + 211).astype(np.uint32)
+    exp = np.zeros(W * H * 4, np.float32)
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, 1, 6, 0, sd, verts, idx, pixels=pix)
+    g = got.reshape(-1, 4)[pix.astype(np.int64)]
+    e = exp.reshape(-1, 4)[pix.astype(np.int64)]
+    np.testing.assert_array_equal(bits(g), bits(e))
+    sl = pix.astype(np.int64) // W * Wp + pix % W
+    plane = Wp * Hp
+    np.testing.assert_array_equal(s_got[sl], sd[sl])
+    np.testing.assert_array_equal(s_got[plane + sl], sd[plane + sl])
+    assert (e[:, :3] > 0).any() and np.isfinite(got).all()
+
+
 @pytest.mark.parametrize("n_tris", [69_451])
 def test_tris_vs_oracle_mesh(n_tris, tracer, pt, oracle):
     """Bunny-class mesh, BVH traversal, against the oracle's linear loop."""
@@ -839,6 +903,83 @@ def test_pixel_candidate_lists_vs_oracle(pt, oracle, monkeypatch, n_tris, sr):
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"RT_PIXEL_LISTS={mode} {builder}")
 
 
+def test_pixel_candidate_lists_small_wide_frames(pt, oracle, monkeypatch):
+    """The list frustum on frames whose pixels subtend a wide angle: a 24x20 frame
+    at fov 100 (L = (W/2)/tan(fov/2) ~ 10, where normalising the corner rays misses interior
+    directions by ~1/(8 L^2) ~ 1e-3) with the mesh filling the view, sampleRate 4, lists forced
+    on — equal to the oracle.  Then a list area too small for every pixel (RT_LIST_MB: the
+    pixels that do not fit take the tree) on the 64x48 frame: equal to the oracle, and the
+    render reports the lists on with pixels on the tree."""
+    sc = pt.scenes
+    verts, idx = sc.make_mesh(2000)
+    for (W, H, fov, dist, env) in ((24, 20, 100.0, 3.2, {}), (64, 48, 53.0, 5.0, {"RT_LIST_MB": "1"})):
+        Wp, Hp = sc.padded_dims(W, H)
+        seeds = sc.default_seeds(Wp, Hp, skip=11)
+        c = dict(sc.PLY_CAMERA)
+        c["distance"] = dist
+        cam = sc.camera_spherical(W, fov=fov, **c)
+        exp = np.zeros(W * H * 4, np.float32)
+        oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, 4, 6, 0, seeds.copy(), verts, idx)
+        monkeypatch.setenv("RT_PIXEL_LISTS", "1")
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        rt.setCamera(cam)
+        rt.setSampleRate(4)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        got = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(got, W, H, 0, kernel=2)
+        info = rt.renderInfo()
+        rt.close()
+        for k in env:
+            monkeypatch.delenv(k)
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"{W}x{H} fov {fov} {env}")
+        assert info["lists"] == 1
+        if env:
+            assert 0 < info["list_pixels_tree"] and info["list_records"] <= info["list_capacity"], info
+
+
+def test_traversal_switch_on_a_context_keeps_results(pt, oracle):
+    """the cached schedule (LPT order, pixel classes, deferred-shadow slots)
+    belongs to one traversal.  One context renders the same tile at sampleRate 4 (deferral on:
+    few pixels per lane) with the compressed tree, then the full-precision tree, then the linear
+    loop, then the compressed tree again; every render equals the oracle on the tile's rows."""
+    sc = pt.scenes
+    W, H, sr, tile = 96, 64, 4, (8, 4, 1)
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(2000)
+    seeds = sc.default_seeds(Wp, Hp, skip=5)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    rows = np.arange(H)[(np.arange(H) // tile[0]) % tile[1] == tile[2]]
+    pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+    exp = np.zeros(W * H * 4, np.float32)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix)
+    exp_tile = exp.reshape(H, W, 4)[rows].reshape(-1)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(sc.ply_scene())
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    deferred = []
+    for trav in ("bvh", "bvh4f", "linear", "bvh"):
+        rt.setTraversal(trav)
+        rt.setSeeds(Wp, Hp, seeds)
+        got = np.zeros(len(rows) * W * 4, np.float32)
+        rt.rayTrace(got, W, H, 0, kernel=2, tile=tile)
+        deferred.append(rt.counters()["pixels_deferred"])
+        np.testing.assert_array_equal(bits(got), bits(exp_tile), err_msg=trav)
+        s_got = rt.getSeeds()
+        sl = pix.astype(np.int64) // W * Wp + pix % W
+        np.testing.assert_array_equal(s_got[sl], sd[sl], err_msg=trav)
+    rt.close()
+    assert deferred[0] > 0 and deferred[1] == 0 and deferred[2] == 0 and deferred[3] > 0, deferred
+
+
 def test_kernel_time_split(pt, monkeypatch):
     """rt_last_kernel_split_ms: a many-sample frame's device time splits into the candidate-list
     pre-pass and the main kernel, the two adding up to rt_last_kernel_ms; without lists
@@ -942,71 +1083,90 @@ def test_gpu_builder_equals_linear(case, pt):
                 np.testing.assert_array_equal(bits(got[k][1]), bits(ref[k][1]), err_msg=f"{case} {key} t {k}")
 
 
-def test_interactive_view_replay(tracer, pt, tmp_path):
-    """ProgressiveViewHIP (GlutCLWindow.cpp:136-301 without GL) driven through the C++ CLI by
-    display / arrow-key / drag / reshape events equals the same event sequence replayed on the
-    Python RayTracer with the window's state machine written out: progression resets on every
-    camera change and on reshape, orbit about (0,-4,0) from azimuth 105 / elevation 40."""
+def test_interactive_view_replay(tracer, pt, oracle, tmp_path):
+    """f3: ProgressiveViewHIP (GlutCLWindow.cpp:136-301 without GL) driven through the C++ CLI by
+    display / arrow-key / drag / reshape events.  Every displayed frame equals the oracle's render
+    of the reference kernel for the state the window is in — camera from setCameraSpherical(
+    (0,-4,0), elevation, azimuth, 5) at fov 53 once the orbit has moved it (main.cpp's camera
+    before), progression 0 after a (re)allocation and +1 per refining display, the seed planes
+    of the context's glibc rand() stream regenerated on every size change — bit for bit, frames
+    and their progressive mix.  Every key / drag posts a redisplay exactly when refinement had
+    finished (GlutCLWindow.cpp:294-301), and a display at maxProgression renders nothing."""
+    import json
     import subprocess
 
     from conftest import ROOT
 
-    events = "d,d,d,l,d,d,m:7:-4,d,u,u,d,s:48:40,d,d,n,d,r,d,m:-400:90,d"
-    raw = tmp_path / "view.f32"
+    max_prog = 4
+    events = ("d,d,d,d,d,d,l,d,d,m:7:-4,d,u,u,d,d,d,d,d,d,m:3:2,d,s:48:40,d,d,n,d,r,d,m:-400:90,d,d,"
+              "d,d,d,d,u,d")
+    frames_path = tmp_path / "frames.f32"
     res = subprocess.run([str(ROOT / "pathtracer.cl_amd" / "rt_render"), "--scene", "main", "--width", "64",
-                          "--height", "48", "--events", events, "--raw", str(raw)], check=True, timeout=120,
-                         capture_output=True, text=True)
-    import json
-
-    state = json.loads(res.stdout.strip().splitlines()[-1])
-    got = np.fromfile(raw, np.float32)
+                          "--height", "48", "--events", events, "--max-progression", str(max_prog),
+                          "--frames-out", str(frames_path)], check=True, timeout=120, capture_output=True, text=True)
+    lines = [json.loads(x) for x in res.stdout.strip().splitlines()]
+    states, final = lines[:-1], lines[-1]
+    shown = np.fromfile(frames_path, np.float32)
 
     sc = pt.scenes
     f32 = np.float32
-    rt = pt.RayTracer(0)
-    rt.setSpheres(sc.main_scene())
-    rt.setSampleRate(1)
-    rt.setMaxPathDepth(6)
-    rt.setCameraSpherical((0.0, -4.0, 0.0), 14.0, 118.0, 5.0)  # main.cpp:127-128
-    az, el, dist = f32(105.0), f32(40.0), f32(5.0)
-    W, H, prog, realloc, buf = 64, 48, 0, True, None
-
-    def orbit():
-        rt.setCameraSpherical((0.0, -4.0, 0.0), float(el), float(az), float(dist))
-
-    for ev in events.split(","):
+    S = sc.main_scene()
+    az, el = f32(105.0), f32(40.0)  # GlutCLWindow's constructor (:24-28)
+    orbited = False
+    W, H, prog, realloc = 64, 48, 0, True
+    exp = sd = None
+    consumed = 0  # values of the context's rand() stream used by earlier seed layouts
+    off = 0
+    n_rendered = n_post = 0
+    evs = events.split(",")
+    assert len(states) == len(evs)
+    for ev, st in zip(evs, states):
+        assert st["event"] == ev
+        post = False
+        rendered = False
         if ev == "d":
             if realloc:
-                buf = np.zeros(W * H * 4, np.float32)
-                prog, realloc = 0, False
-                rt.rayTrace(buf, W, H, prog, kernel=0)
-            elif prog < 10000:
-                prog += 1
-                rt.rayTrace(buf, W, H, prog, kernel=0)
-        elif ev in "lrun":
+                Wp, Hp = sc.padded_dims(W, H)
+                sd = sc.default_seeds(Wp, Hp, skip=consumed)
+                consumed += 2 * Wp * Hp
+                exp = np.zeros(W * H * 4, np.float32)
+                prog, realloc, rendered, post = 0, False, True, max_prog > 0
+            elif prog < max_prog:
+                prog, rendered, post = prog + 1, True, True
+            if rendered:
+                cam = (sc.camera_spherical(W, (0.0, -4.0, 0.0), float(el), float(az), 5.0) if orbited
+                       else sc.camera_spherical(W, **sc.MAIN_CAMERA))
+                oracle.render_spheres(exp, cam, S, W, H, Wp, Hp, 1, 6, prog, sd)
+                got = shown[off:off + W * H * 4]
+                off += W * H * 4
+                np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"displayed frame {n_rendered} ({ev})")
+                n_rendered += 1
+        elif ev in ("l", "r", "u", "n") or ev[0] == "m":
             if ev == "l":
                 az = np.fmod(f32(az + f32(3.0)), f32(360.0))
             elif ev == "r":
                 az = np.fmod(f32(az - f32(3.0)), f32(360.0))
             elif ev == "u":
                 el = min(f32(el + f32(3.0)), f32(90.0))
-            else:
+            elif ev == "n":
                 el = max(f32(el - f32(3.0)), f32(10.0))
-            orbit()
-            prog = 0
-        elif ev[0] == "m":
-            dx, dy = map(int, ev[2:].split(":"))
-            az = np.fmod(f32(az + f32(dx)), f32(360.0))
-            el = max(min(f32(el + f32(dy)), f32(90.0)), f32(10.0))
-            orbit()
+            else:
+                dx, dy = map(int, ev[2:].split(":"))
+                az = np.fmod(f32(az + f32(dx)), f32(360.0))
+                el = max(min(f32(el + f32(dy)), f32(90.0)), f32(10.0))
+            orbited = True
+            post = prog >= max_prog  # restart(), GlutCLWindow.cpp:294-301
             prog = 0
         else:
             W, H = map(int, ev[2:].split(":"))
             realloc = True
-    rt.close()
-    assert (state["progression"], state["width"], state["height"]) == (prog, W, H)
-    assert np.float32(state["azimuth"]) == az and np.float32(state["elevation"]) == el
-    np.testing.assert_array_equal(bits(got), bits(buf))
+        n_post += post and ev != "d"
+        assert (st["rendered"], st["redisplay"], st["progression"]) == (rendered, post, prog), (ev, st)
+        assert (st["width"], st["height"]) == (W, H)
+        assert f32(st["azimuth"]) == az and f32(st["elevation"]) == el
+    assert off == shown.size and n_rendered >= 20
+    assert n_post >= 2  # drags / keys after refinement finished did post a redisplay
+    assert (final["progression"], final["width"], final["height"]) == (prog, W, H)
 
 
 def test_huge_coordinates_fall_back_to_full_precision_nodes(tracer, pt):
@@ -1042,21 +1202,21 @@ def test_huge_coordinates_fall_back_to_full_precision_nodes(tracer, pt):
 
 
 def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
-    """The pixel queue's order (step-counting probe, LPT key), the box-wave priority and the
-    probe density are scheduling only: a frame with box and mesh pixels, 16 spp, renders to
-    the same bits and seeds with the queue row-major (RT_SCHEDULE=0), with the default
-    schedule, with other probe / key settings, and with the box pixels' shadow rays traced
-    inline (RT_DEFER=0) or deferred for only the few box pixels 1 MB of slots holds, and with
-    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0)."""
+    """The pixel queue's order (step-counting probe, LPT key) and the box-wave priority are
+    scheduling only: a frame with box and mesh pixels, 16 spp, renders to the same bits and
+    seeds with the queue row-major (RT_SCHEDULE=0), with the default schedule, with the box
+    pixels' shadow rays traced inline (RT_DEFER=0) or deferred for only the few box pixels 1 MB
+    of slots holds, with camera rays traversing the tree instead of their candidate lists
+    (RT_PIXEL_LISTS=0), and with a list area too small for every pixel (RT_LIST_MB=2)."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
     verts, idx = sc.make_mesh(20_000)
     seeds = sc.default_seeds(Wp, Hp, skip=7)
     frames = []
-    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_PROBE_N": "1", "RT_LPT_MAX": "0"}, {"RT_PROBE_N": "3"},
-                {"RT_DEFER": "0"}, {"RT_DEFER": "1", "RT_DEFER_MB": "1"}, {"RT_PIXEL_LISTS": "0"}):
-        for k in ("RT_SCHEDULE", "RT_PROBE_N", "RT_LPT_MAX", "RT_DEFER", "RT_DEFER_MB", "RT_PIXEL_LISTS"):
+    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_DEFER": "0"}, {"RT_DEFER": "1", "RT_DEFER_MB": "1"},
+                {"RT_PIXEL_LISTS": "0"}, {"RT_LIST_MB": "2"}):
+        for k in ("RT_SCHEDULE", "RT_DEFER", "RT_DEFER_MB", "RT_PIXEL_LISTS", "RT_LIST_MB"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)

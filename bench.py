@@ -383,9 +383,11 @@ def interactive_cost(rt, step, cam_setup, azimuth, device, dist):
     for k, az in (("cold", azimuth + 3.0), ("restore", azimuth)):
         rt.setCameraSpherical(cam_setup["target"], cam_setup["elevation"], az, cam_setup["distance"])
         c_ms = timed()
+        info = rt.renderInfo()
         w_ms = timed()
         if k == "cold":
-            res = {"cold_frame_ms": c_ms, "warm_frame_ms": w_ms, "schedule_host_ms": rt.renderInfo()["schedule_host_ms"]}
+            res = {"cold_frame_ms": c_ms, "warm_frame_ms": w_ms,
+                   "cold_schedule_host_ms": info["schedule_host_ms"]}
     if dist:
         t = torch.tensor([res["cold_frame_ms"], res["warm_frame_ms"]], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

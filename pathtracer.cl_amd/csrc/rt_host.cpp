@@ -966,6 +966,16 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.fetch_frac = kFetchFrac;
         a.box_exit = 0;
         a.probe_n = kProbeN;
+        a.diag_pixel = 0xffffffffu;
+#if RT_DIAG_ONE_PIXEL
+        a.diag_k = 1;
+        if (const char *v = getenv("RT_DIAG_PIXEL")) { /* diagnostics build only: "x,y[,k]" */
+            unsigned dx = 0, dy = 0, dk = 1;
+            const int n = sscanf(v, "%u,%u,%u", &dx, &dy, &dk);
+            if (n >= 2) a.diag_pixel = dy * W + dx;
+            if (n == 3) a.diag_k = dk;
+        }
+#endif
         a.tile_order = nullptr;
         a.pixel_flags = nullptr;
         a.pixel_class = nullptr;

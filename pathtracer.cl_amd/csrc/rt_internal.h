@@ -29,6 +29,10 @@
 #ifndef RT_STEP_UNROLL
 #define RT_STEP_UNROLL 6 /* traversal steps per exit check in k_tris (3 / 4 / 6: 176.3 / 174.0 / 173.4 ms) */
 #endif
+#ifndef RT_DIAG_ONE_PIXEL
+#define RT_DIAG_ONE_PIXEL 0 /* diagnostics build: k_tris renders only the pixel RT_DIAG_PIXEL=x,y names (the
+                               others are skipped), so its serial chain runs alone in its wave */
+#endif
 #ifndef RT_PLAIN_PIXEL_STATS
 #define RT_PLAIN_PIXEL_STATS 0 /* RT_PIXEL_STATS clocks in plain (not only counting) launches: a
                                   diagnostics build (costs registers: 0.5 %) */
@@ -139,6 +143,8 @@ struct RtTriLaunch {
     uint32_t fetch_frac;        /* stepping-round exit at ceil(live lanes x fetch_frac / 64) completed
                                    queries when that is below fetch_k (0: fetch_k only) */
     uint32_t box_exit;          /* a box pixel's completed query ends the stepping round */
+    uint32_t diag_pixel;        /* RT_DIAG_ONE_PIXEL builds: yl * W + x of the target pixel, and how many */
+    uint32_t diag_k;            /* pixels of its 8 x 8 tile are rendered (from it on, in-tile order) */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =
                                    start / finish (s_memrealtime, 100 MHz, low 32 bits), queries, steps */
     /* Deferred shadow rays of box pixels (DESIGN.md §5 "Deferred shadow rays"): a box pixel's

@@ -907,7 +907,14 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                     if (a.tile_order) tile = a.tile_order[tile];
                     x = (tile % tiles_x) * 8u + (in & 7u);
                     yl = (tile / tiles_x) * 8u + (in >> 3);
-                    if (x < a.W && yl < a.Hl) {
+                    bool take = x < a.W && yl < a.Hl;
+                    if (RT_DIAG_ONE_PIXEL) { /* diagnostics build: the target pixel and the diag_k - 1 pixels
+                                                after it in its 8 x 8 tile (in-tile order, wrapping) */
+                        const uint32_t dx = a.diag_pixel % a.W, dy = a.diag_pixel / a.W;
+                        const uint32_t in0 = (dy & 7u) * 8u + (dx & 7u);
+                        take = take && (x >> 3) == (dx >> 3) && (yl >> 3) == (dy >> 3) && ((in - in0) & 63u) < a.diag_k;
+                    }
+                    if (take) {
                         const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];

@@ -14,8 +14,9 @@ DEV="--offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-
 /opt/rocm/bin/hipcc $FL -c -o $B/p.o rt_ply.cpp &
 /opt/rocm/bin/hipcc $FL $DEV -c -o $B/g.o rt_build_gpu.hip &
 /opt/rocm/bin/hipcc $FL $DEV -c -o $B/c.o rt_comm.hip &
+/opt/rocm/bin/hipcc $FL $DEV -c -o $B/s.o rt_sched.hip &
 wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT $B/k.o $B/h.o $B/b.o $B/p.o $B/g.o $B/c.o -lpthread \
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT $B/k.o $B/h.o $B/b.o $B/p.o $B/g.o $B/c.o $B/s.o -lpthread \
     -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf $B
 echo built $OUT

@@ -347,7 +347,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
     }
-    if kernel == pt.RayTracer.KERNEL_TRIS:
+    if kernel == pt.RayTracer.KERNEL_TRIS and info:
         line["config"]["candidate_lists"] = {"on": bool(info["lists"]), "capacity_records": int(info["list_capacity"]),
                                              "records": int(info["list_records"]),
                                              "pixels_on_tree": int(info["list_pixels_tree"])}
@@ -387,7 +387,7 @@ def interactive_cost(rt, step, cam_setup, azimuth, device, dist):
         w_ms = timed()
         if k == "cold":
             res = {"cold_frame_ms": c_ms, "warm_frame_ms": w_ms,
-                   "cold_schedule_host_ms": info["schedule_host_ms"]}
+                   "cold_schedule_host_ms": info.get("schedule_host_ms", 0.0)}
     if dist:
         t = torch.tensor([res["cold_frame_ms"], res["warm_frame_ms"]], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

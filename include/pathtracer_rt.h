@@ -209,7 +209,8 @@ typedef struct rt_render_info {
     uint32_t pixels_deferred;  /* box pixels whose shadow rays were deferred */
     uint32_t schedule_rebuilt; /* 1: the cost probe, LPT order and pixel classes were recomputed
                                   (camera, mesh, frame, tile or parameters changed) */
-    uint32_t reserved;
+    uint32_t lists_rebuilt;    /* 1: the lists were built for this render (0: the previous render's,
+                                  same camera, mesh, frame and tile, were reused) */
     double schedule_host_ms;   /* host time spent enqueueing / sizing the schedule this render */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);

@@ -120,7 +120,7 @@ class RtRenderInfo(ctypes.Structure):
         ("list_pixels_tree", ctypes.c_uint32),
         ("pixels_deferred", ctypes.c_uint32),
         ("schedule_rebuilt", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("lists_rebuilt", ctypes.c_uint32),
         ("schedule_host_ms", ctypes.c_double),
     ]
 
@@ -202,7 +202,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         )
     lib = ctypes.CDLL(str(p))
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if p == LIB_PATH:
+                raise RuntimeError(f"{p} lacks {name}: rebuild it (`make -C pathtracer.cl_amd/csrc`)")
+            continue  # an older build loaded for an A/B run: only its own entry points
         fn.restype = res
         fn.argtypes = args
     if path is None:

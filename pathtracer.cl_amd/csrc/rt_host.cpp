@@ -73,6 +73,9 @@ constexpr double kPi = 3.14159265358979323846; /* M_PI */
      kFetchFrac the stepping round also ends at ceil(live lanes x kFetchFrac / 64) completed
                 queries (r02 A/B: full frame 162.8 -> 160.6 ms, slowest 8-way tile 219 -> 107 ms). */
 constexpr uint32_t kProbeN = 2;
+/* a 1-spp frame traces fewer rays than a 2x2 probe would: one probe ray per pixel there (bunny
+   class 1024^2 at 1 spp: a camera move cost 2.2 ms against a 1.0 ms frame with the 2x2 probe) */
+uint32_t probe_n(uint32_t sample_rate) { return sample_rate >= 2 ? kProbeN : 1u; }
 constexpr uint32_t kFetchK = 24;
 constexpr uint32_t kFetchFrac = 24;
 
@@ -96,13 +99,14 @@ struct rt_ctx {
     uint32_t *d_nodes4q = nullptr; /* 4-wide tree, compressed nodes */
     float *d_tris = nullptr;
     size_t tris_cap = 0;       /* triangle records d_tris holds (mesh + camera-ray candidate lists) */
-    uint8_t *d_lists = nullptr;       /* candidate count per pixel (k_pixel_lists) */
-    uint32_t *d_list_first = nullptr; /* first list slot per pixel (compacted list area) */
+    uint16_t *d_list_code = nullptr;  /* per pixel: offset in its tile's block << 5 | count - 1 (k_pixel_lists) */
+    uint32_t *d_list_tile = nullptr;  /* per 8x8 tile: first slot of its block of lists */
     uint32_t *d_list_alloc = nullptr; /* the list area's allocator */
-    size_t lists_bytes = 0;
+    size_t list_px_cap = 0, list_tile_cap = 0;
     int pixel_lists = -1; /* RT_PIXEL_LISTS: 0 off, 1 on, unset: on for sampleRate >= 4 (the pre-pass
                              costs about a traversal per pixel: a 1-spp frame does not repay it) */
     size_t list_mb = 4096; /* RT_LIST_MB: device memory of the list area (pixels beyond it take the tree) */
+    std::vector<uint32_t> list_key; /* what the lists in the list area were built for (empty: none) */
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
     uint32_t *d_order = nullptr; /* pixel-queue tile order (expensive tiles first) */
@@ -346,6 +350,7 @@ int ensure_tris_capacity(rt_ctx *c, size_t records, size_t keep, hipStream_t st)
     free_dev(c->d_tris);
     c->d_tris = nt;
     c->tris_cap = records;
+    c->list_key.clear(); /* only the mesh's records were carried over */
     return RT_OK;
 }
 
@@ -474,8 +479,8 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         c->order_cap = n_t;
     }
     RtTriLaunch pa = a;
-    pa.probe_n = kProbeN;
-    const uint32_t pn2 = kProbeN * kProbeN;
+    pa.probe_n = probe_n(c->sample_rate);
+    const uint32_t pn2 = pa.probe_n * pa.probe_n;
     int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
     e = rt_sched_order(c->sched, c->d_flags, W, hl, pn2, (uint32_t)c->lights.size(), c->max_depth, c->d_order, st);
@@ -592,8 +597,8 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_halo_rows);
     free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
-    free_dev(c->d_lists);
-    free_dev(c->d_list_first);
+    free_dev(c->d_list_code);
+    free_dev(c->d_list_tile);
     free_dev(c->d_list_alloc);
     rt_sched_free(c->sched);
     free_dev(c->d_seeds);
@@ -965,7 +970,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.fetch_k_box = kFetchK;
         a.fetch_frac = kFetchFrac;
         a.box_exit = 0;
-        a.probe_n = kProbeN;
+        a.probe_n = probe_n(c->sample_rate);
         a.diag_pixel = 0xffffffffu;
 #if RT_DIAG_ONE_PIXEL
         a.diag_k = 1;
@@ -1022,47 +1027,68 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
            any other), a count and a first slot per pixel.  Leaf codes address slots below 2^28;
            pixels whose list does not fit the area (RT_LIST_MB) take the tree, and a list area
            that cannot be allocated turns the lists off for the render — same bits either way. */
-        a.pixel_lists = nullptr;
+        a.list_code = nullptr;
+        a.list_tile = nullptr;
         const bool bvh4 = c->d_nodes4 && (trav == RT_TRAV_BVH4Q || trav == RT_TRAV_BVH4);
-        const uint64_t kept = c->n_tris;
+        const uint64_t kept = (c->n_tris + 7ull) & ~7ull; /* the list area starts on a 128-B line */
         const uint64_t npx = (uint64_t)W * hl;
         uint64_t list_cap = std::min<uint64_t>(npx * RT_LIST_MAX, ((uint64_t)c->list_mb << 20) / 48);
-        list_cap = std::min<uint64_t>(list_cap, kept < (1ull << 28) ? (1ull << 28) - 1 - kept : 0);
+        list_cap = std::min<uint64_t>(list_cap, kept < (1ull << 28) ? (1ull << 28) - 8 - kept : 0);
         bool lists = (c->pixel_lists == 1 || (c->pixel_lists < 0 && c->sample_rate >= 4)) && bvh4 && list_cap > 0;
-        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), kept, st) != RT_OK) {
+        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), c->n_tris, st) != RT_OK) {
             (void)hipGetLastError(); /* out of device memory: no lists this render */
             lists = false;
         }
-        if (lists && c->lists_bytes < npx) {
-            free_dev(c->d_lists);
-            free_dev(c->d_list_first);
-            c->d_lists = nullptr;
-            c->d_list_first = nullptr;
-            c->lists_bytes = 0;
-            HIPCHK(c, hipMalloc(&c->d_lists, npx));
-            HIPCHK(c, hipMalloc(&c->d_list_first, npx * sizeof(uint32_t)));
-            c->lists_bytes = npx;
+        const uint64_t n_tiles = (uint64_t)((W + 7) / 8) * ((hl + 7) / 8);
+        if (lists && (c->list_px_cap < npx || c->list_tile_cap < n_tiles)) {
+            free_dev(c->d_list_code);
+            free_dev(c->d_list_tile);
+            c->d_list_code = nullptr;
+            c->d_list_tile = nullptr;
+            c->list_px_cap = c->list_tile_cap = 0;
+            c->list_key.clear();
+            HIPCHK(c, hipMalloc(&c->d_list_code, npx * sizeof(uint16_t)));
+            HIPCHK(c, hipMalloc(&c->d_list_tile, n_tiles * sizeof(uint32_t)));
+            c->list_px_cap = npx;
+            c->list_tile_cap = n_tiles;
         }
         if (lists && !c->d_list_alloc) HIPCHK(c, hipMalloc(&c->d_list_alloc, sizeof(uint32_t)));
         if (lists) {
-            a.pixel_lists = c->d_lists;
-            a.list_first = c->d_list_first;
+            a.list_code = c->d_list_code;
+            a.list_tile = c->d_list_tile;
             a.list_base = (uint32_t)kept;
             a.list_cap = (uint32_t)list_cap;
             a.list_alloc = c->d_list_alloc;
         }
         a.tris = c->d_tris;
+        /* The lists depend only on the camera, the mesh and tree, the frame shape and the tile —
+           like the BVH and the schedule, they are rebuilt when one of those changes and reused
+           by the frames in between (GlutCLWindow refines one view over many frames,
+           GlutCLWindow.cpp:151-158; a camera move rebuilds them: bench.py cold_frame_ms). */
+        bool build_lists = false;
+        if (lists) {
+            const uintptr_t tp = reinterpret_cast<uintptr_t>(c->d_tris), np4 = reinterpret_cast<uintptr_t>(c->d_nodes4);
+            std::vector<uint32_t> key = {W, H, hl, stripe, nr, rk, (uint32_t)trav, (uint32_t)c->mesh_serial,
+                                         (uint32_t)(c->mesh_serial >> 32), (uint32_t)list_cap, (uint32_t)tp,
+                                         (uint32_t)((uint64_t)tp >> 32), (uint32_t)np4, (uint32_t)((uint64_t)np4 >> 32)};
+            const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
+            key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
+            build_lists = key != c->list_key;
+            c->list_key = key;
+        }
         HIPCHK(c, hipEventRecord(c->ev0, st));
-        e = lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr, c->d_lists,
-                                          c->d_list_first, st)
-                  : 0;
+        e = build_lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr,
+                                                c->d_list_code, c->d_list_tile, st)
+                        : 0;
+        if (e) c->list_key.clear();
         HIPCHK(c, hipEventRecord(c->evm, st));
         if (!e && lists && getenv("RT_LIST_STATS")) { /* diagnostics: candidate list lengths */
-            std::vector<uint8_t> h((size_t)npx);
-            HIPCHK(c, hipMemcpyAsync(h.data(), c->d_lists, h.size(), hipMemcpyDeviceToHost, st));
+            std::vector<uint16_t> h((size_t)npx);
+            HIPCHK(c, hipMemcpyAsync(h.data(), c->d_list_code, h.size() * 2, hipMemcpyDeviceToHost, st));
             HIPCHK(c, hipStreamSynchronize(st));
             uint64_t b[6] = {}, sum = 0, nl = 0;
-            for (uint8_t v : h) {
+            for (uint16_t code : h) {
+                const uint32_t v = code == RT_LIST_NONE ? 255u : code == RT_LIST_EMPTY ? 0u : (code & 31u) + 1u;
                 b[v == 0 ? 0 : v <= 8 ? 1 : v <= 16 ? 2 : v <= 24 ? 3 : v <= 32 ? 4 : 5]++;
                 if (v <= RT_LIST_MAX) sum += v, nl++;
             }
@@ -1080,6 +1106,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info.traversal = (uint32_t)trav;
         c->info.grid_blocks = (uint32_t)blocks;
         c->info.lists = lists ? 1u : 0u;
+        c->info.lists_rebuilt = build_lists ? 1u : 0u;
         c->info.list_capacity = lists ? list_cap : 0;
         c->info.list_pixels_tree = lists ? (uint32_t)npx : 0u; /* pixel count until rt_last_render_info reads the counts */
         c->info.pixels_deferred = a.n_defer;
@@ -1232,10 +1259,10 @@ int rt_last_render_info(rt_ctx *c, rt_render_info *out)
         HIPCHK(c, hipMemcpy(&used, c->d_list_alloc, sizeof(used), hipMemcpyDeviceToHost));
         c->info.list_records = std::min<uint64_t>(used, c->info.list_capacity);
         const size_t npx = c->info.list_pixels_tree; /* pixels of the launch, set below */
-        std::vector<uint8_t> h(npx);
-        if (npx) HIPCHK(c, hipMemcpy(h.data(), c->d_lists, npx, hipMemcpyDeviceToHost));
+        std::vector<uint16_t> h(npx);
+        if (npx) HIPCHK(c, hipMemcpy(h.data(), c->d_list_code, npx * 2, hipMemcpyDeviceToHost));
         uint32_t tree = 0;
-        for (uint8_t v : h) tree += v == RT_LIST_NONE ? 1u : 0u;
+        for (uint16_t v : h) tree += v == RT_LIST_NONE ? 1u : 0u;
         c->info.list_pixels_tree = tree;
         c->info_list_pending = false;
     }

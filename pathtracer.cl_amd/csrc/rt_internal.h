@@ -161,12 +161,15 @@ struct RtTriLaunch {
     const uint32_t *defer_pixel; /* per slot: yl * W + x */
     uint32_t n_defer;           /* slots in use */
     /* Camera-ray candidate lists (k_pixel_lists): per pixel the triangles any of its sample
-       rays could accept, RT_LIST_MAX at most, their records copied, compacted, into the triangle
-       buffer's slots [list_base, list_base + list_cap) (a wave-aggregated allocator, list_alloc);
-       pixel_lists[pixel] = count (RT_LIST_NONE: no list, the pixel's camera rays take the tree),
-       list_first[pixel] = its first slot */
-    const uint8_t *pixel_lists;
-    const uint32_t *list_first;
+       rays could accept, RT_LIST_MAX at most, their records copied into the triangle buffer's
+       slots [list_base, list_base + list_cap).  Each 8x8 tile's lists are one block (one
+       allocation per pre-pass wave, list_alloc): list_tile[tile] = the block's first slot,
+       list_code[pixel] = its list's offset in the block / 8 << 5 | (count - 1) (lists start on
+       128-B lines: 8-record multiples from an 8-aligned list_base), or RT_LIST_EMPTY (no
+       candidate: no mesh hit possible) or RT_LIST_NONE (no list: the pixel's camera rays take
+       the tree).  2 B per pixel + 4 B per tile: small enough to stay in L2 beside the tree. */
+    const uint16_t *list_code;
+    const uint32_t *list_tile;
     uint32_t list_base;
     uint32_t list_cap;
     uint32_t *list_alloc;
@@ -174,7 +177,9 @@ struct RtTriLaunch {
 #ifndef RT_LIST_MAX
 #define RT_LIST_MAX 32
 #endif
-#define RT_LIST_NONE 255
+#define RT_LIST_NONE 0xffffu
+#define RT_LIST_EMPTY 0xfffeu
+static_assert(RT_LIST_MAX == 32, "list codes hold count - 1 in 5 bits and a block offset / 8 (< 64 * 32 / 8) in 11");
 /* segment kinds of a deferred pixel's path (trace_path_tri, rtcommon.h:378-468) */
 enum { RT_SEG_BOX = 0, RT_SEG_TRI = 1, RT_SEG_NONE = 2 };
 
@@ -205,8 +210,8 @@ int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *str
 /* Camera-ray candidate lists for the launch's pixels (writes a.pixel_lists and the list
    records in the triangle buffer at a.list_base); nodes4 = full-precision 4-wide tree,
    q4 = compressed nodes (their normal boxes; may be NULL). */
-int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint8_t *counts,
-                          uint32_t *first, void *stream);
+int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint16_t *codes,
+                          uint32_t *tile_base, void *stream);
 /* Scheduling probe: per pixel the mesh hits of a grid of probe rays and the traversal steps of
    their queries (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);

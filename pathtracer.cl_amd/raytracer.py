@@ -258,9 +258,12 @@ class RayTracer:
     def renderInfo(self) -> dict:
         """rt_last_render_info: the last render's lists, deferral and schedule (no result depends
         on any of it)."""
+        fn = getattr(self._lib, "rt_last_render_info", None)
+        if fn is None:  # an older library loaded for an A/B run
+            return {}
         i = _abi.RtRenderInfo()
-        self._check(self._lib.rt_last_render_info(self._h, ctypes.byref(i)), "rt_last_render_info")
-        return {f: getattr(i, f) for f, _ in _abi.RtRenderInfo._fields_ if f != "reserved"}
+        self._check(fn(self._h, ctypes.byref(i)), "rt_last_render_info")
+        return {f: getattr(i, f) for f, _ in _abi.RtRenderInfo._fields_}
 
     def traceRays(self, rays: np.ndarray, any_hit: bool = False) -> tuple[np.ndarray, np.ndarray]:
         r = np.ascontiguousarray(rays, _abi.RAY_DTYPE)

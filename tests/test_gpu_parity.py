@@ -942,6 +942,41 @@ def test_pixel_candidate_lists_small_wide_frames(pt, oracle, monkeypatch):
             assert 0 < info["list_pixels_tree"] and info["list_records"] <= info["list_capacity"], info
 
 
+def test_candidate_lists_reused_across_frames(pt, oracle, monkeypatch):
+    """The candidate lists depend only on camera, mesh / tree, frame and tile: frames of one
+    view reuse them (rt_render_info.lists_rebuilt 0) and a camera move rebuilds them.  Every
+    frame of a progressive sequence, before and after a move, equals the oracle."""
+    sc = pt.scenes
+    W, H, sr = 64, 48, 2
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    monkeypatch.setenv("RT_PIXEL_LISTS", "1")
+    rt = pt.RayTracer(0)
+    rt.setSpheres(sc.ply_scene())
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    seeds = sc.default_seeds(Wp, Hp, skip=17)
+    rt.setSeeds(Wp, Hp, seeds)
+    sd = seeds.copy()
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    rebuilt = []
+    for f, az in enumerate((105.0, 105.0, 105.0, 108.0, 108.0)):
+        c = dict(sc.PLY_CAMERA)
+        c["azimuth"] = az
+        rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+        cam = sc.camera_spherical(W, **c)
+        p = 0 if f in (0, 3) else f - (0 if f < 3 else 3)
+        rt.rayTrace(got, W, H, p, kernel=2)
+        rebuilt.append(rt.renderInfo()["lists_rebuilt"])
+        oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, sr, 6, p, sd, verts, idx)
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {f}")
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
+    rt.close()
+    assert rebuilt == [1, 0, 0, 1, 0], rebuilt
+
+
 def test_traversal_switch_on_a_context_keeps_results(pt, oracle):
     """the cached schedule (LPT order, pixel classes, deferred-shadow slots)
     belongs to one traversal.  One context renders the same tile at sampleRate 4 (deferral on:

@@ -134,7 +134,8 @@ struct rt_ctx {
     bool schedule = true;
     bool schedule_rebuilt = false; /* the last triangle render recomputed the schedule */
     rt_render_info info = {};      /* rt_last_render_info */
-    bool info_list_pending = false; /* info.list_records still to be read from the allocator */
+    bool info_list_pending = false; /* info.list_records / list_pixels_tree still to be read */
+    size_t info_list_px = 0;        /* pixels of the render the pending list counts belong to */
     int builder = RT_BUILD_HOST;      /* builder for the next rt_set_mesh */
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
@@ -1108,7 +1109,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info.lists = lists ? 1u : 0u;
         c->info.lists_rebuilt = build_lists ? 1u : 0u;
         c->info.list_capacity = lists ? list_cap : 0;
-        c->info.list_pixels_tree = lists ? (uint32_t)npx : 0u; /* pixel count until rt_last_render_info reads the counts */
+        c->info_list_px = lists ? (size_t)npx : 0u;
         c->info.pixels_deferred = a.n_defer;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
@@ -1258,7 +1259,7 @@ int rt_last_render_info(rt_ctx *c, rt_render_info *out)
         uint32_t used = 0;
         HIPCHK(c, hipMemcpy(&used, c->d_list_alloc, sizeof(used), hipMemcpyDeviceToHost));
         c->info.list_records = std::min<uint64_t>(used, c->info.list_capacity);
-        const size_t npx = c->info.list_pixels_tree; /* pixels of the launch, set below */
+        const size_t npx = c->info_list_px;
         std::vector<uint16_t> h(npx);
         if (npx) HIPCHK(c, hipMemcpy(h.data(), c->d_list_code, npx * 2, hipMemcpyDeviceToHost));
         uint32_t tree = 0;

@@ -368,8 +368,9 @@ def main():
 
 
 def interactive_cost(rt, step, cam_setup, azimuth, device, dist):
-    """Wall time of a step right after a 3-degree camera move (one arrow key) and of the next
-    step, same camera; max over ranks.  Restores the camera afterwards."""
+    """Wall time of a step right after a 3-degree camera move (one arrow key: the schedule and,
+    from sampleRate 4, the candidate lists are rebuilt), of the next step and of the one after
+    (the view's steady state); max over ranks.  Restores the camera afterwards."""
     import torch
 
     def timed():
@@ -384,14 +385,17 @@ def interactive_cost(rt, step, cam_setup, azimuth, device, dist):
         rt.setCameraSpherical(cam_setup["target"], cam_setup["elevation"], az, cam_setup["distance"])
         c_ms = timed()
         info = rt.renderInfo()
+        s_ms = timed()  # below sampleRate 4 the second frame of a view builds the candidate lists
         w_ms = timed()
         if k == "cold":
-            res = {"cold_frame_ms": c_ms, "warm_frame_ms": w_ms,
+            res = {"cold_frame_ms": c_ms, "second_frame_ms": s_ms, "warm_frame_ms": w_ms,
                    "cold_schedule_host_ms": info.get("schedule_host_ms", 0.0)}
     if dist:
-        t = torch.tensor([res["cold_frame_ms"], res["warm_frame_ms"]], dtype=torch.float64, device=f"cuda:{device}")
+        keys = ("cold_frame_ms", "second_frame_ms", "warm_frame_ms")
+        t = torch.tensor([res[k] for k in keys], dtype=torch.float64, device=f"cuda:{device}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        res["cold_frame_ms"], res["warm_frame_ms"] = float(t[0]), float(t[1])
+        for i, k in enumerate(keys):
+            res[k] = float(t[i])
     return {k: round(v, 3) for k, v in res.items()}
 
 

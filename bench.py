@@ -183,9 +183,24 @@ def main():
     # native sharding (csrc/rt_comm.hip): librtmi's RCCL communicator renders the rank's
     # stripes, moves the seed-row halo and assembles the frame on rank 0's GPU
     comm = None
+    comm_note = None
     if n_ranks > 1 and args.comm == "native" and dist.get_backend() == "nccl":
-        comm = ptdist.NativeComm.from_torch(device)
-        frame_full = torch.zeros((W * H * 4) if rank == 0 else 4, dtype=torch.float32, device=f"cuda:{device}")
+        # every rank must take the same path: the communicator is created collectively and the
+        # outcome agreed on, so a failure anywhere sends all ranks to the torch.distributed gather
+        err = None
+        try:
+            comm = ptdist.NativeComm.from_torch(device)
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if err else 1], dtype=torch.int64, device=f"cuda:{device}")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()):
+            if comm is not None:
+                comm.close()
+            comm = None
+            comm_note = f"native communicator unavailable ({err or 'on another rank'}): torch.distributed gather"
+        else:
+            frame_full = torch.zeros((W * H * 4) if rank == 0 else 4, dtype=torch.float32, device=f"cuda:{device}")
 
     def step():
         p = frame_no[0] if progressive else 0
@@ -353,6 +368,8 @@ def main():
                                              "pixels_on_tree": int(info["list_pixels_tree"])}
         line["config"]["pixels_deferred"] = int(info["pixels_deferred"])
     line.update(cold)
+    if comm_note:
+        line["comm_note"] = comm_note
     if sharded is not None:
         line.update(sharded)
     if cpu is not None and "gpu_vs_reference_bit_exact" in cpu:

@@ -212,6 +212,8 @@ typedef struct rt_render_info {
     uint32_t lists_rebuilt;    /* 1: the lists were built for this render (0: the previous render's,
                                   same camera, mesh, frame and tile, were reused) */
     double schedule_host_ms;   /* host time spent enqueueing / sizing the schedule this render */
+    uint32_t split_chunks;     /* sample-split render (a tile with few pixels per lane): chunks per
+                                  pixel, each an independent task seeded by the seed pass; 0: whole pixels */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
 

@@ -122,6 +122,7 @@ class RtRenderInfo(ctypes.Structure):
         ("schedule_rebuilt", ctypes.c_uint32),
         ("lists_rebuilt", ctypes.c_uint32),
         ("schedule_host_ms", ctypes.c_double),
+        ("split_chunks", ctypes.c_uint32),
     ]
 
 

@@ -126,7 +126,13 @@ struct rt_ctx {
     int defer = -1;          /* RT_DEFER: 1 on, 0 off, unset = auto (on when the launch has fewer than
                                 2 pixels per resident lane at sampleRate >= 4: tiles of a multi-GPU
                                 many-sample frame) */
-    size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer buffers */
+    size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer (or sample-split) buffers */
+    /* sample-split tiles (k_split_seeds -> k_tris chunks -> k_split_finish) */
+    int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (see split_plan) */
+    uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
+    float *d_split_col = nullptr;     /* per sample and pixel: its radiance */
+    uint32_t *d_split_counter = nullptr;
+    size_t split_seed_bytes = 0, split_col_bytes = 0;
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
     size_t halo_rows_cap = 0, halo_buf_cap = 0;
@@ -173,8 +179,8 @@ struct rt_ctx {
     bool have_timing = false;
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
-    /* persistent-grid size per (traversal kind, counting): index trav * 2 + count */
-    int grid_cache[4 * (RT_TRAV_BVH4Q + 1)] = {};
+    /* persistent-grid size per (traversal kind, counting, kernel form): index (trav * 2 + count) * 3 + form */
+    int grid_cache[6 * (RT_TRAV_BVH4Q + 1)] = {};
 };
 
 namespace {
@@ -367,14 +373,14 @@ int ensure_spill(rt_ctx *c, size_t entries)
     return RT_OK;
 }
 
-int grid_blocks(rt_ctx *c, int trav, bool count, bool defer, int *out)
+int grid_blocks(rt_ctx *c, int trav, bool count, int form, int *out)
 {
-    const int key = trav * 4 + (count ? 2 : 0) + (defer ? 1 : 0);
+    const int key = (trav * 2 + (count ? 1 : 0)) * 3 + form;
     if (key < 0 || key >= (int)(sizeof(c->grid_cache) / sizeof(c->grid_cache[0])))
         return fail(c, RT_ERR_ARG, "unknown traversal kind");
     if (!c->grid_cache[key]) {
         int b = 0;
-        const int e = rt_tris_grid_blocks(c->device, trav, count, defer, &b);
+        const int e = rt_tris_grid_blocks(c->device, trav, count, form, &b);
         if (e) return hip_fail(c, (hipError_t)e, "occupancy query");
         c->grid_cache[key] = b;
     }
@@ -417,6 +423,39 @@ int ensure_defer(rt_ctx *c, uint64_t n, uint64_t recs, uint64_t segs)
     return RT_OK;
 }
 
+/* Sample-split tiles (RT_SPLIT): when a launch has fewer pixels than about two
+   per resident lane — a multi-GPU tile of a many-sample frame — every lane holds one pixel
+   from the start and the launch lasts as long as its slowest pixel's serial sample chain.
+   Splitting each pixel's samples into chunks (seeded by a closest-hit-only pass) turns it back
+   into a queue of many short tasks. */
+bool split_wanted(const rt_ctx *c, uint64_t npx, uint64_t lanes)
+{
+    (void)npx;
+    (void)lanes;
+    return c->split == 1 && c->sample_rate >= 2;
+}
+
+/* Sample-split buffers: per pixel (nch + 1) seed pairs, per sample and pixel an RGB radiance. */
+int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
+{
+    if (c->split_seed_bytes < seed_bytes) {
+        free_dev(c->d_split_seed);
+        c->d_split_seed = nullptr;
+        c->split_seed_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_split_seed, seed_bytes));
+        c->split_seed_bytes = seed_bytes;
+    }
+    if (c->split_col_bytes < col_bytes) {
+        free_dev(c->d_split_col);
+        c->d_split_col = nullptr;
+        c->split_col_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_split_col, col_bytes));
+        c->split_col_bytes = col_bytes;
+    }
+    if (!c->d_split_counter) HIPCHK(c, hipMalloc(&c->d_split_counter, sizeof(uint32_t)));
+    return RT_OK;
+}
+
 /* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by its paths: a
    camera ray that hits the mesh ends after one shadow query per light (rtcommon.h:411-421),
    one that misses bounces off the box up to maxDepth+1 times with shadow queries at each
@@ -440,7 +479,8 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     const uintptr_t np = reinterpret_cast<uintptr_t>(a.nodes);
     std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
                                  (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks,
-                                 c->sample_rate, (uint32_t)(c->defer + 1), (uint32_t)trav_kind(c), (uint32_t)np,
+                                 c->sample_rate, (uint32_t)(c->defer + 1), (uint32_t)(c->split + 1),
+                                 (uint32_t)trav_kind(c), (uint32_t)np,
                                  (uint32_t)((uint64_t)np >> 32)};
     const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
@@ -498,7 +538,8 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
        4-way 39 vs 46 ms, the 8-way 30 vs 44 ms: the line sits below two pixels per resident
        lane.) */
     const uint64_t lanes = (uint64_t)blocks * RT_BLOCK;
-    const bool use = c->defer == 1 || (c->defer < 0 && npx < 2 * lanes && c->sample_rate >= 4);
+    const bool use = !split_wanted(c, npx, lanes) &&
+                     (c->defer == 1 || (c->defer < 0 && npx < 2 * lanes && c->sample_rate >= 4));
     const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
     const uint64_t nl = c->lights.size();
     const uint64_t recs = spp * nd * nl; /* records per slot */
@@ -564,6 +605,7 @@ int rt_create(int device, rt_ctx **out)
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0";
     if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
+    if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -596,6 +638,9 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_defer_vis);
     free_dev(c->d_defer_queue);
     free_dev(c->d_defer_qcount);
+    free_dev(c->d_split_seed);
+    free_dev(c->d_split_col);
+    free_dev(c->d_split_counter);
     free_dev(c->d_halo_rows);
     free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
@@ -951,20 +996,23 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         const uint64_t item_blocks = (items + RT_BLOCK - 1) / RT_BLOCK;
         /* persistent grids: the plain form's and the deferred-shadow form's own occupancy
            (RT_TRIS_WAVES_DEFER), each at most one block per RT_BLOCK queue items */
-        int blocks = 0, blocks_defer = 0;
-        int r = grid_blocks(c, trav, c->counting, false, &blocks);
+        int blocks = 0, blocks_defer = 0, blocks_split = 0;
+        int r = grid_blocks(c, trav, c->counting, RT_FORM_PLAIN, &blocks);
         if (r != RT_OK) return r;
         blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks, item_blocks));
         if (trav == RT_TRAV_BVH4Q) {
-            r = grid_blocks(c, trav, c->counting, true, &blocks_defer);
+            r = grid_blocks(c, trav, c->counting, RT_FORM_DEFER, &blocks_defer);
             if (r != RT_OK) return r;
             blocks_defer = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks_defer, item_blocks));
+            r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
+            if (r != RT_OK) return r;
         }
         /* the spill area is indexed by blockIdx: sized for the larger of the grids any kernel of
            this render (probe, k_tris in either form, k_defer_shadow) may run with */
         a.spill_cap = spill_cap(c);
         if (a.spill_cap) {
-            const int rs = ensure_spill(c, (size_t)std::max(blocks, blocks_defer) * RT_BLOCK * a.spill_cap);
+            const int rs =
+                ensure_spill(c, (size_t)std::max(blocks, std::max(blocks_defer, blocks_split)) * RT_BLOCK * a.spill_cap);
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
@@ -1008,12 +1056,33 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 blocks = blocks_defer;
             }
         }
+        /* sample-split tiles: chunks of about spp / 16 samples; the buffers within RT_DEFER_MB */
+        a.split_chunks = 0;
+        if (a.tile_order && !a.n_defer && trav == RT_TRAV_BVH4Q &&
+            split_wanted(c, (uint64_t)W * hl, (uint64_t)blocks * RT_BLOCK)) {
+            const uint32_t spp = c->sample_rate * c->sample_rate;
+            const uint32_t csz = (spp + 15u) / 16u, nch = (spp + csz - 1u) / csz;
+            const size_t npx_s = (size_t)W * hl;
+            const size_t seed_bytes = npx_s * (nch + 1u) * 8u, col_bytes = npx_s * spp * 12u;
+            if (seed_bytes + col_bytes <= (c->defer_mb << 20)) {
+                const int rs = ensure_split(c, seed_bytes, col_bytes);
+                if (rs != RT_OK) return rs;
+                a.split_chunks = nch;
+                a.split_chunk = csz;
+                a.split_seed = c->d_split_seed;
+                a.split_col = c->d_split_col;
+                a.split_counter = c->d_split_counter;
+                a.split_seed_blocks = (uint32_t)blocks;
+                blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks_split, item_blocks * nch));
+            }
+        }
         const double sched_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
-            fprintf(stderr, "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p, defer %u\n",
+            fprintf(stderr,
+                    "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p, defer %u, split %u x %u\n",
                     (void *)c, trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order,
-                    a.n_defer);
+                    a.n_defer, a.split_chunks, a.split_chunk);
         /* diagnostics: per-pixel start/finish clocks (+ queries, steps and the wall clocks
            by phase in a counting launch: 8 x u32 per pixel), dumped raw to $RT_PIXEL_STATS */
         const char *stats_path = getenv("RT_PIXEL_STATS");
@@ -1123,6 +1192,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info.list_capacity = lists ? list_cap : 0;
         c->info_list_px = lists ? (size_t)npx : 0u;
         c->info.pixels_deferred = a.n_defer;
+        c->info.split_chunks = a.split_chunks;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
         c->info_list_pending = lists;

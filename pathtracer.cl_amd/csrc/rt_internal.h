@@ -173,6 +173,17 @@ struct RtTriLaunch {
     uint32_t list_base;
     uint32_t list_cap;
     uint32_t *list_alloc;
+    /* Sample-split tiles: a pixel's random numbers depend only on its closest
+       hits, so a seed pass (k_split_seeds) walks every pixel's samples with the closest-hit
+       queries alone and stores the seed at the first sample of each chunk; k_tris then renders
+       the chunks as independent tasks, each sample's radiance stored, and k_split_finish sums
+       them in sample order and writes the pixel and its final seed. */
+    uint32_t split_chunks;    /* chunks per pixel (0: pixels are whole tasks) */
+    uint32_t split_chunk;     /* samples per chunk */
+    uint32_t *split_seed;     /* per pixel (yl * W + x) and chunk 0..split_chunks: 2 words; the last = the final seed */
+    float *split_col;         /* per sample s and pixel p: radiance at ((s * W * Hl) + p) * 3 */
+    uint32_t *split_counter;  /* the seed pass's queue cursor */
+    uint32_t split_seed_blocks; /* grid of the seed pass */
 };
 #ifndef RT_LIST_MAX
 #define RT_LIST_MAX 32
@@ -236,7 +247,8 @@ int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int
    buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,
                         uint32_t *buf, bool unpack, void *stream);
-/* Persistent-grid size for the triangle kernel on this device. */
-int rt_tris_grid_blocks(int device, int trav, bool count, bool defer, int *blocks);
+/* Persistent-grid size for the triangle kernel on this device; form: RT_FORM_*. */
+enum { RT_FORM_PLAIN = 0, RT_FORM_DEFER = 1, RT_FORM_SPLIT = 2 };
+int rt_tris_grid_blocks(int device, int trav, bool count, int form, int *blocks);
 
 #endif /* RT_INTERNAL_H */

@@ -71,6 +71,16 @@ def main():
            "idle_lane_fraction": round(float(1.0 - occ.mean()), 4),
            "end_quantiles_ms": {q: round(float(np.quantile(end, q / 100)), 2) for q in (50, 90, 99, 100)},
            "live_hist": [round(float(x), 3) for x in occ[::100]]}
+    # pixels by their query count (a mesh pixel: ~2 per sample; a box pixel: ~2 x (maxDepth + 1) per sample)
+    q = st[:, 2]
+    spp = sr * sr
+    classes = {}
+    for name, lo, hi in (("q<=3spp", 0, 3 * spp), ("3spp<q<=6spp", 3 * spp, 6 * spp), ("q>6spp", 6 * spp, 1 << 62)):
+        m = (q > lo) & (q <= hi) if lo else q <= hi
+        if m.any():
+            classes[name] = {"pixels": int(m.sum()), "start_max_ms": round(float(start[m].max()), 2),
+                             "end_ms": {k: round(float(np.quantile(end[m], k / 100)), 2) for k in (50, 90, 99, 100)}}
+    res["by_queries"] = classes
     print(json.dumps(res))
 
 

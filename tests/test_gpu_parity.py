@@ -1015,6 +1015,54 @@ def test_traversal_switch_on_a_context_keeps_results(pt, oracle):
     assert deferred[0] > 0 and deferred[1] == 0 and deferred[2] == 0 and deferred[3] > 0, deferred
 
 
+@pytest.mark.parametrize("sr", [2, 3, 5])
+def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
+    """Sample-split rendering forced on (RT_SPLIT=1): the seed pass stores each chunk's first
+    seed from the pixel's closest-hit queries alone, k_tris renders the chunks as independent
+    tasks and k_split_finish sums the samples in order.  Whole frames over two progressive
+    frames and a row-stripe tile equal the oracle bit for bit, frames and seeds, with chunkings
+    that do not divide the sample count evenly (sr 3: 9 chunks of 1 sample; sr 5: 13 chunks of
+    2, the last of 1)."""
+    monkeypatch.setenv("RT_SPLIT", "1")
+    sc = pt.scenes
+    W, H = 72, 40
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    seeds = sc.default_seeds(Wp, Hp, skip=3)
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    spp = sr * sr
+    csz = (spp + 15) // 16
+    rt = pt.RayTracer(0)  # RT_SPLIT is read when the context is created
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    for p in range(2):
+        rt.rayTrace(got, W, H, p, kernel=2)
+        assert rt.renderInfo()["split_chunks"] == (spp + csz - 1) // csz
+        oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, p, sd, verts, idx)
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
+        np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg=f"seeds after frame {p}")
+    tile = (8, 2, 1)
+    rows = np.arange(H)[(np.arange(H) // tile[0]) % tile[1] == tile[2]]
+    pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(len(rows) * W * 4, np.float32)
+    rt.rayTrace(got, W, H, 0, kernel=2, tile=tile)
+    assert rt.renderInfo()["split_chunks"] > 0
+    np.testing.assert_array_equal(bits(got), bits(exp.reshape(H, W, 4)[rows].reshape(-1)), err_msg="tile")
+    np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg="tile seeds")
+    rt.close()
+
+
 def test_kernel_time_split(pt, monkeypatch):
     """rt_last_kernel_split_ms: a many-sample frame's device time splits into the candidate-list
     pre-pass and the main kernel, the two adding up to rt_last_kernel_ms; without lists
@@ -1303,3 +1351,33 @@ def test_deferred_shadow_rays_at_full_size(tracer, pt, monkeypatch):
     for tile in (None, (8, 8, 3)):
         np.testing.assert_array_equal(res[("1", tile)][0], res[("0", tile)][0])
         np.testing.assert_array_equal(res[("1", tile)][1], res[("0", tile)][1])
+
+
+def test_sample_split_at_full_size(tracer, pt, monkeypatch):
+    """Sample-split rendering on the dragon-class frame at full size, sampleRate 16 (16 chunks
+    of 16 samples), as a row-stripe tile of 8 (259k pixels: fewer than the resident lanes):
+    the same bits and seeds as whole-pixel tasks (RT_SPLIT=0), which the oracle pins."""
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 16
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    seeds = sc.default_seeds(Wp, Hp, skip=4)
+    tile = (8, 8, 5)
+    rows = len(np.arange(H)[(np.arange(H) // 8) % 8 == 5])
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RT_SPLIT", mode)
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        rt.setCamera(sc.camera_spherical(W, **sc.PLY_CAMERA))
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        out = np.zeros(W * rows * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
+        assert (rt.renderInfo()["split_chunks"] == 16) == (mode == "1")
+        res[mode] = (bits(out).copy(), rt.getSeeds().copy())
+        rt.close()
+    np.testing.assert_array_equal(res["1"][0], res["0"][0])
+    np.testing.assert_array_equal(res["1"][1], res["0"][1])

@@ -128,11 +128,20 @@ struct rt_ctx {
                                 many-sample frame) */
     size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer (or sample-split) buffers */
     /* sample-split tiles (k_split_seeds -> k_tris chunks -> k_split_finish) */
-    int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (see split_plan) */
+    int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (see split_wanted) */
+    bool seed_coop = true;            /* RT_SEED_COOP=0: the seed pass with one lane per query (A/B) */
+    uint32_t split_probe = 4;         /* RT_SPLIT_PROBE: probe rays per pixel side in a split render (A/B) */
+    uint32_t split_gpw = 0;           /* RT_SPLIT_GPW: box-pixel chains per seed-pass wave (A/B) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
     float *d_split_col = nullptr;     /* per sample and pixel: its radiance */
-    uint32_t *d_split_counter = nullptr;
+    uint32_t *d_split_counter = nullptr; /* [0]: the seed pass's cursor, [32]: the box pixels' (own line) */
     size_t split_seed_bytes = 0, split_col_bytes = 0;
+    uint32_t *d_split_box = nullptr;  /* the box pixels (yl * W + x): their chains run on stream2 */
+    size_t split_box_cap = 0;
+    uint32_t n_split_box = 0;
+    int split_box_grid = 0;           /* the box pixels' seed-pass grid of the render being launched */
+    hipStream_t stream2 = nullptr;    /* the box pixels' seed pass and chunks, beside the mesh pixels' */
+    hipEvent_t ev_split0 = nullptr, ev_box = nullptr;
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
     size_t halo_rows_cap = 0, halo_buf_cap = 0;
@@ -452,8 +461,55 @@ int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
         HIPCHK(c, hipMalloc(&c->d_split_col, col_bytes));
         c->split_col_bytes = col_bytes;
     }
-    if (!c->d_split_counter) HIPCHK(c, hipMalloc(&c->d_split_counter, sizeof(uint32_t)));
+    if (!c->d_split_counter) HIPCHK(c, hipMalloc(&c->d_split_counter, 64 * sizeof(uint32_t)));
+    if (!c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    if (!c->ev_split0) HIPCHK(c, hipEventCreateWithFlags(&c->ev_split0, hipEventDisableTiming));
+    if (!c->ev_box) HIPCHK(c, hipEventCreateWithFlags(&c->ev_box, hipEventDisableTiming));
     return RT_OK;
+}
+
+/* The box pixels' seed-pass grid: one chain per lane (COOP: per 4-lane group; RT_SPLIT_GPW per
+   wave), at most a quarter of the full grid (further chains queue behind the first); full_grid
+   0: unbounded. */
+int split_box_blocks(const rt_ctx *c, bool coop, int full_grid)
+{
+    const uint32_t per_wave = c->split_gpw ? c->split_gpw : (coop ? 16u : 64u);
+    int n = (int)((c->n_split_box + per_wave * 4u - 1u) / (per_wave * 4u));
+    if (full_grid > 0) n = std::min(n, std::max(1, full_grid / 4));
+    return n;
+}
+
+/* A sample-split render: the box pixels' seed pass and then their chunks on stream2, beside
+   the mesh pixels' seed pass and chunks on the render stream (the box pixels' chains are the
+   long ones: they overlap the rest of the frame instead of preceding it); then the in-order
+   sums.  Each stream has its own queue cursors and its own part of the spill area. */
+int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
+{
+    const uint32_t n_box = a.split_which == RT_SPLIT_MESH ? a.split_n_box : 0u;
+    if (n_box) {
+        RtTriLaunch b = a;
+        b.split_which = RT_SPLIT_BOX;
+        b.split_counter = a.split_counter + 32;
+        b.work_counter = a.work_counter + 32;
+        b.spill = a.spill + (size_t)std::max<int>(blocks, (int)a.split_seed_blocks) * RT_BLOCK * a.spill_cap;
+        b.split_gpw = c->split_gpw;
+        b.split_seed_blocks = (uint32_t)std::max(1, c->split_box_grid);
+        HIPCHK(c, hipEventRecord(c->ev_split0, st));
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split0, 0));
+        const int chunk_grid = (int)std::min<uint64_t>((uint64_t)blocks, ((uint64_t)n_box * a.split_chunks + RT_BLOCK - 1) / RT_BLOCK);
+        int e = rt_launch_split_seeds(b, c->stream2);
+        if (!e) e = rt_launch_tris(b, RT_TRAV_BVH4Q, c->counting, std::max(1, chunk_grid), c->stream2);
+        if (e) return hip_fail(c, (hipError_t)e, "box-pixel split launches");
+        HIPCHK(c, hipEventRecord(c->ev_box, c->stream2));
+    }
+    if (n_box && getenv("RT_SPLIT_SERIAL")) HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0)); /* diagnostics */
+    RtTriLaunch m = a; /* the mesh pixels' seed pass: short chains, one lane each */
+    m.split_coop = 0;
+    int e = rt_launch_split_seeds(m, st);
+    if (!e) e = rt_launch_tris(m, RT_TRAV_BVH4Q, c->counting, blocks, st);
+    if (e) return e;
+    if (n_box) HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0));
+    return rt_launch_split_finish(a, st);
 }
 
 /* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by its paths: a
@@ -521,13 +577,20 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         c->order_cap = n_t;
     }
     RtTriLaunch pa = a;
-    pa.probe_n = probe_n(c->sample_rate);
+    /* a sample-split render also takes its box pixels (whose long chains run apart) from the
+       probe: a denser grid finds more of the silhouette pixels whose samples partly miss */
+    pa.probe_n = split_wanted(c, (uint64_t)W * hl, (uint64_t)blocks * RT_BLOCK) && c->sample_rate >= 4
+                     ? c->split_probe
+                     : probe_n(c->sample_rate);
     const uint32_t pn2 = pa.probe_n * pa.probe_n;
     int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
     e = rt_sched_order(c->sched, c->d_flags, W, hl, pn2, (uint32_t)c->lights.size(), c->max_depth, c->d_order, st);
     if (e) return hip_fail(c, (hipError_t)e, "tile order");
-    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, st);
+    /* a sample-split render also runs the probe's long mesh chains (more than 96 steps per probe
+       ray: grazing camera rays without a candidate list) beside the box pixels' */
+    const bool split = split_wanted(c, npx, (uint64_t)blocks * RT_BLOCK);
+    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? 96u * pn2 : 0u, st);
     if (e) return hip_fail(c, (hipError_t)e, "box-pixel scan");
     /* Deferral shortens the box chains but moves their shadow queries into a second launch
        that cannot use the tail of the first: it pays where the chains set the frame time (a
@@ -550,6 +613,28 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         max_slots = std::min<uint64_t>(max_slots, 0xffffffffull / recs);
     }
     uint64_t n = 0;
+    c->n_split_box = 0;
+    if (split) {
+        /* sample-split tiles: every box pixel (some probe ray missed the mesh: the long chains)
+           gets a slot; their seed pass and chunks run on a stream of their own */
+        uint32_t n_box = 0;
+        HIPCHK(c, hipMemcpyAsync(&n_box, c->sched.scan + npx, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (c->split_box_cap < n_box) {
+            free_dev(c->d_split_box);
+            c->d_split_box = nullptr;
+            c->split_box_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_split_box, (size_t)n_box * 4));
+            c->split_box_cap = n_box;
+        }
+        e = rt_sched_classify(c->sched, (uint32_t)npx, n_box, c->d_class, c->d_split_box, st);
+        if (e) return hip_fail(c, (hipError_t)e, "pixel classes");
+        c->n_split_box = n_box;
+        c->n_defer = 0;
+        c->order_key = key;
+        c->schedule_rebuilt = true;
+        return RT_OK;
+    }
     if (max_slots) {
         uint32_t n_box = 0; /* the one host read: the buffers are sized to the box pixels */
         HIPCHK(c, hipMemcpyAsync(&n_box, c->sched.scan + npx, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -606,12 +691,15 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
+    if (const char *v = getenv("RT_SEED_COOP")) c->seed_coop = atoi(v) != 0;
+    if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v));
+    if (const char *v = getenv("RT_SPLIT_PROBE")) c->split_probe = (uint32_t)std::min(5, std::max(1, atoi(v)));
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evm) != hipSuccess ||
-        hipMalloc(&c->d_work, 64) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_work, 64 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_HIP;
     }
@@ -641,6 +729,10 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_split_seed);
     free_dev(c->d_split_col);
     free_dev(c->d_split_counter);
+    free_dev(c->d_split_box);
+    if (c->ev_split0) (void)hipEventDestroy(c->ev_split0);
+    if (c->ev_box) (void)hipEventDestroy(c->ev_box);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     free_dev(c->d_halo_rows);
     free_dev(c->d_halo_buf);
     free_dev(c->d_tris);
@@ -1011,8 +1103,10 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
            this render (probe, k_tris in either form, k_defer_shadow) may run with */
         a.spill_cap = spill_cap(c);
         if (a.spill_cap) {
-            const int rs =
-                ensure_spill(c, (size_t)std::max(blocks, std::max(blocks_defer, blocks_split)) * RT_BLOCK * a.spill_cap);
+            /* twice the largest grid: a sample-split render runs two streams side by side, each
+               on its own part of the area */
+            const int rs = ensure_spill(
+                c, (size_t)std::max(blocks, std::max(blocks_defer, blocks_split)) * 2 * RT_BLOCK * a.spill_cap);
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
@@ -1072,8 +1166,19 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 a.split_seed = c->d_split_seed;
                 a.split_col = c->d_split_col;
                 a.split_counter = c->d_split_counter;
-                a.split_seed_blocks = (uint32_t)blocks;
-                blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks_split, item_blocks * nch));
+                a.split_which = c->n_split_box ? RT_SPLIT_MESH : RT_SPLIT_ALL;
+                a.split_box = c->d_split_box;
+                a.split_n_box = c->n_split_box;
+                /* 4 lanes per seed-pass query where the tree's worst stack (plus a candidate
+                   list's blocks) fits a group's LDS stack */
+                a.split_coop = c->seed_coop && c->bvh.stack4 + 4 <= RT_COOP_STACK ? 1u : 0u;
+                /* the box pixels' seed pass (one lane per pixel) keeps its blocks resident beside
+                   the mesh pixels' kernels, whose grids leave room for it */
+                const int box_blocks = c->n_split_box ? split_box_blocks(c, a.split_coop != 0, blocks) : 0;
+                c->split_box_grid = box_blocks;
+                a.split_seed_blocks = (uint32_t)std::max(1, blocks - box_blocks);
+                blocks = std::max(1, std::min((int)std::min<uint64_t>((uint64_t)blocks_split, item_blocks * nch),
+                                              blocks_split - box_blocks));
             }
         }
         const double sched_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
@@ -1168,18 +1273,19 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             std::vector<uint16_t> h((size_t)npx);
             HIPCHK(c, hipMemcpyAsync(h.data(), c->d_list_code, h.size() * 2, hipMemcpyDeviceToHost, st));
             HIPCHK(c, hipStreamSynchronize(st));
-            uint64_t b[6] = {}, sum = 0, nl = 0;
+            uint64_t b[7] = {}, sum = 0, nl = 0;
             for (uint16_t code : h) {
-                const uint32_t v = code == RT_LIST_NONE ? 255u : code == RT_LIST_EMPTY ? 0u : (code & 31u) + 1u;
-                b[v == 0 ? 0 : v <= 8 ? 1 : v <= 16 ? 2 : v <= 24 ? 3 : v <= 32 ? 4 : 5]++;
+                const uint32_t v = code == RT_LIST_NONE ? 255u : code == RT_LIST_EMPTY ? 0u : (code & (RT_LIST_MAX - 1u)) + 1u;
+                b[v == 0 ? 0 : v <= 8 ? 1 : v <= 16 ? 2 : v <= 24 ? 3 : v <= 32 ? 4 : v <= 64 ? 5 : 6]++;
                 if (v <= RT_LIST_MAX) sum += v, nl++;
             }
-            fprintf(stderr, "lists: 0:%llu 1-8:%llu 9-16:%llu 17-24:%llu 25-32:%llu none:%llu mean %.2f\n",
+            fprintf(stderr, "lists: 0:%llu 1-8:%llu 9-16:%llu 17-24:%llu 25-32:%llu 33-64:%llu none:%llu mean %.2f\n",
                     (unsigned long long)b[0], (unsigned long long)b[1], (unsigned long long)b[2],
                     (unsigned long long)b[3], (unsigned long long)b[4], (unsigned long long)b[5],
-                    nl ? (double)sum / (double)nl : 0.0);
+                    (unsigned long long)b[6], nl ? (double)sum / (double)nl : 0.0);
         }
-        if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
+        if (!e && a.split_chunks) e = split_render(c, a, blocks, st);
+        else if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
         if (!e && a.n_defer) e = rt_launch_defer(a, c->counting, blocks, st);
         c->last_deferred = a.n_defer;
         HIPCHK(c, hipEventRecord(c->ev1, st));

@@ -184,13 +184,29 @@ struct RtTriLaunch {
     float *split_col;         /* per sample s and pixel p: radiance at ((s * W * Hl) + p) * 3 */
     uint32_t *split_counter;  /* the seed pass's queue cursor */
     uint32_t split_seed_blocks; /* grid of the seed pass */
+    uint32_t split_which;     /* RT_SPLIT_ALL, or the mesh pixels / the box pixels of a two-stream split */
+    const uint32_t *split_box; /* RT_SPLIT_BOX: the box pixels (yl * W + x), split_n_box of them */
+    uint32_t split_n_box;
+    uint32_t split_coop;      /* seed pass: 4 lanes per query (the tree's stack fits the group's LDS stack) */
+    uint32_t split_gpw;       /* seed pass: queries (chains) per wave, 0 = all lanes / groups */
 };
+enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
+#define RT_COOP_STACK (RT_STACK_DEPTH * 4) /* LDS stack entries of a 4-lane query group (k_split_seeds) */
 #ifndef RT_LIST_MAX
-#define RT_LIST_MAX 32
+#define RT_LIST_MAX 64
 #endif
 #define RT_LIST_NONE 0xffffu
 #define RT_LIST_EMPTY 0xfffeu
-static_assert(RT_LIST_MAX == 32, "list codes hold count - 1 in 5 bits and a block offset / 8 (< 64 * 32 / 8) in 11");
+#if RT_LIST_MAX == 32
+#define RT_LIST_BITS 5
+#elif RT_LIST_MAX == 64
+#define RT_LIST_BITS 6
+#else
+#error "RT_LIST_MAX: 32 or 64"
+#endif
+/* list code = (offset in the tile's block / 8) << RT_LIST_BITS | (count - 1): the offset is below
+   64 * RT_LIST_MAX, so a code stays below RT_LIST_EMPTY */
+static_assert(((64u * RT_LIST_MAX / 8u - 1u) << RT_LIST_BITS | (RT_LIST_MAX - 1u)) < 0xfffeu, "list code range");
 /* segment kinds of a deferred pixel's path (trace_path_tri, rtcommon.h:378-468) */
 enum { RT_SEG_BOX = 0, RT_SEG_TRI = 1, RT_SEG_NONE = 2 };
 
@@ -211,6 +227,10 @@ struct RtSphLaunch {
 enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH4 = 2, RT_TRAV_BVH4Q = 4 };
 
 int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream);
+/* Sample-split renders: the seed pass (grid a.split_seed_blocks, cursor a.split_counter reset
+   first) and the in-order sums; rt_launch_tris runs the chunk tasks (a.split_chunks > 0). */
+int rt_launch_split_seeds(const RtTriLaunch &a, void *stream);
+int rt_launch_split_finish(const RtTriLaunch &a, void *stream);
 int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
@@ -240,7 +260,8 @@ struct RtSchedScratch {
 void rt_sched_free(RtSchedScratch &s);
 int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_t hl, uint32_t pn2, uint32_t n_lights,
                    uint32_t max_depth, uint32_t *order, void *stream);
-int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, void *stream);
+int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, uint32_t step_max,
+                      void *stream);
 int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *defer_pixel,
                       void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed

@@ -531,11 +531,12 @@ __device__ __forceinline__ float uniform_f(float v)
    wave-private batch of kBatch consecutive items: one atomicAdd per batch instead of one per
    refill.  A single head word saturates at about 88 dequeues per microsecond
    (MI355X_MICROARCH.md, dequeue), which the many short tasks of a sample-split launch exceed.
-   Wave-uniform: call with every lane active; bnext / bend start equal. */
+   Wave-uniform: call with every lane active; bnext / bend start equal; batch >= the takers
+   per wave (k <= batch). */
 constexpr uint32_t kBatch = 64;
 
 __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long long idle, uint32_t &bnext,
-                                               uint32_t &bend)
+                                               uint32_t &bend, uint32_t batch = kBatch)
 {
     const uint32_t k = (uint32_t)__popcll(idle);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
@@ -544,13 +545,13 @@ __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long 
     uint32_t nb = 0;
     if (k > from_b) {
         const int leader = __ffsll((long long)idle) - 1;
-        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(counter, kBatch);
+        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(counter, batch);
         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader));
     }
     const uint32_t item = rank < from_b ? bnext + rank : nb + (rank - from_b);
     if (k > from_b) {
         bnext = nb + (k - from_b);
-        bend = nb + kBatch;
+        bend = nb + batch;
     } else {
         bnext += k;
     }
@@ -599,6 +600,394 @@ __device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uin
 {
     if (n_ranks <= 1) return yl;
     return ((yl / stripe) * n_ranks + rank) * stripe + (yl % stripe);
+}
+
+#ifndef RT_SEED_UNROLL
+#define RT_SEED_UNROLL 2 /* seed-pass traversal steps per loop iteration */
+#endif
+
+/* Cooperative closest-hit query: the 4 lanes of a group (lanes 4g..4g+3 of a wave) advance ONE
+   query together — at a node each lane tests one child box, at a leaf (or a candidate-list
+   block) each lane tests one triangle — so a step's work is a quarter of the per-lane step's
+   and a leaf of up to 4 triangles takes one memory round trip instead of one per triangle.  The
+   group's stack lives in LDS (kCoopStack entries per group).  The result is the reference's
+   closest hit (minimum t, ties to the highest original index: an order-free rule). */
+constexpr int kCoopStack = RT_COOP_STACK; /* entries per group: the per-lane LDS stack's words */
+/* quad (4-lane group) exchanges through DPP quad_perm: a VALU modifier, not an LDS round trip
+   like ds_bpermute (__shfl), whose latency a lone chain's wave cannot hide */
+template <int CTRL>
+__device__ __forceinline__ int quad_dpp(int v)
+{
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+template <int M> /* the value of lane sub ^ M */
+__device__ __forceinline__ int quad_xor(int v)
+{
+    return M == 1 ? quad_dpp<0xB1>(v) : M == 2 ? quad_dpp<0x4E>(v) : quad_dpp<0x1B>(v);
+}
+__device__ __forceinline__ float quad_xorf1(float v) { return __int_as_float(quad_xor<1>(__float_as_int(v))); }
+__device__ __forceinline__ float quad_xorf2(float v) { return __int_as_float(quad_xor<2>(__float_as_int(v))); }
+__device__ __forceinline__ float quad_xorf3(float v) { return __int_as_float(quad_xor<3>(__float_as_int(v))); }
+/* the value of quad lane k (k uniform within the quad) */
+__device__ __forceinline__ int quad_bcast(int v, int k)
+{
+    const int b0 = quad_dpp<0x00>(v), b1 = quad_dpp<0x55>(v), b2 = quad_dpp<0xAA>(v), b3 = quad_dpp<0xFF>(v);
+    return k == 0 ? b0 : k == 1 ? b1 : k == 2 ? b2 : b3;
+}
+
+/* The 4-lane group's stack in the block's LDS stack area, inside the words its wave's lanes own
+   in the per-lane layout ([depth][lane], RT_BLOCK words per depth): entry e of group g of wave w
+   is word RT_BLOCK * (e / 4) + 64 w + 4 g + e % 4 (2-way bank conflicts between the groups). */
+struct CoopStack {
+    lds_int *base; /* word 64 w + 4 g */
+    __device__ __forceinline__ lds_int &operator[](int e) const { return base[RT_BLOCK * (e >> 2) + (e & 3)]; }
+};
+
+struct CoopQuery {
+    int node, best, best_orig, sp;
+    float best_t;
+    V3 inv, oi;
+};
+
+__device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
+{
+    q.inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
+    q.oi = v3(o.x * q.inv.x, o.y * q.inv.y, o.z * q.inv.z);
+    q.node = 0;
+    q.best = -1;
+    q.best_orig = -1;
+    q.best_t = tmax;
+    q.sp = 0;
+}
+
+/* one step; true when the query is complete */
+__device__ __forceinline__ bool coop_step(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                          CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin)
+{
+    const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
+    const int node = q.node;
+    const bool leaf = node < 0;
+    const uint32_t enc = (uint32_t)(~node);
+    const uint32_t first = enc >> 3, cnt = (enc & 7u) + 1u;
+    const bool tri_ok = leaf && (uint32_t)sub < cnt;
+    const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (first + (tri_ok ? (uint32_t)sub : 0u))
+                            : reinterpret_cast<const uint4 *>(nodes) + 4 * node;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u *vrec = reinterpret_cast<const v4u *>(rec);
+    v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2];
+    v4u w3 = {0u, 0u, 0u, 0u};
+    if (!leaf) w3 = vrec[3];
+    asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+    if (leaf) {
+        const float4 ta = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z),
+                                      __uint_as_float(w0.w));
+        const float4 tb = make_float4(__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z), 0.0f);
+        const float4 tc = make_float4(__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z), 0.0f);
+        float t = 0.0f;
+        const bool h = mt_test(o, d, ta, tb, tc, t);
+        const int orig = __float_as_int(ta.w);
+        bool ok = tri_ok && h && !(t < tmin) && (t < q.best_t || (t == q.best_t && orig > q.best_orig));
+        float ct = ok ? t : kInf;
+        int co = ok ? orig : -1, cs = ok ? (int)(first + (uint32_t)sub) : -1;
+        /* the group's best candidate: minimum t, ties to the highest original index */
+        {
+            const float ot = quad_xorf1(ct);
+            const int oo = quad_xor<1>(co), os = quad_xor<1>(cs);
+            const bool take = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
+            ct = take ? ot : ct;
+            co = take ? oo : co;
+            cs = take ? os : cs;
+        }
+        {
+            const float ot = quad_xorf2(ct);
+            const int oo = quad_xor<2>(co), os = quad_xor<2>(cs);
+            const bool take = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
+            ct = take ? ot : ct;
+            co = take ? oo : co;
+            cs = take ? os : cs;
+        }
+        if (cs >= 0) {
+            q.best = cs;
+            q.best_t = ct;
+            q.best_orig = co;
+        }
+        /* a sorted candidate list's early end: the last tested record's next-candidate bound */
+        const uint32_t last = (cnt < 4u ? cnt : 4u) - 1u;
+        const float bound = __int_as_float(quad_bcast((int)w1.w, (int)last));
+        if (q.best_t < bound) return true;
+        if (cnt > 4u) {
+            q.node = ~(int)(((first + 4u) << 3) | (cnt - 5u));
+            return false;
+        }
+    } else {
+        const float tmin_c = -1e-3f, tmax_c = t_slack(q.best_t);
+        const V3 inv = q.inv, oi = q.oi;
+        const uint32_t w = w0.w;
+        const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
+        const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
+        const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
+        const float bx = __builtin_fmaf(__uint_as_float(w0.x), inv.x, -oi.x);
+        const float by = __builtin_fmaf(__uint_as_float(w0.y), inv.y, -oi.y);
+        const float bz = __builtin_fmaf(__uint_as_float(w0.z), inv.z, -oi.z);
+        const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+        const uint32_t sh = 8u * (uint32_t)sub;
+        const float nx = (float)(((px ? w1.x : w1.y) >> sh) & 0xffu), fx = (float)(((px ? w1.y : w1.x) >> sh) & 0xffu);
+        const float ny = (float)(((py ? w1.z : w1.w) >> sh) & 0xffu), fy = (float)(((py ? w1.w : w1.z) >> sh) & 0xffu);
+        const float nz = (float)(((pz ? w2.x : w2.y) >> sh) & 0xffu), fz = (float)(((pz ? w2.y : w2.x) >> sh) & 0xffu);
+        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nx, sx, bx), __builtin_fmaf(ny, sy, by)),
+                                         __builtin_fmaxf(__builtin_fmaf(nz, sz, bz), tmin_c));
+        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaf(fx, sx, bx), __builtin_fmaf(fy, sy, by)),
+                                         __builtin_fminf(__builtin_fmaf(fz, sz, bz), tmax_c));
+        bool hit = tn <= tf; /* an unused slot's inverted box never passes */
+        { /* determinant cull (rt_quant.h), as trav_step_q */
+            const uint32_t nlo = w2.z, nhi = w2.w;
+            const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
+            const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
+            const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
+            const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
+            const float bias = 128.0f * (d.x + d.y + d.z);
+            const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
+                                             __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu),
+                                                            __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
+            const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
+                                             __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu),
+                                                            __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
+            const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
+            const float bnd = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
+            if (bnd < 1e-4f) hit = false;
+        }
+        const int link = (int)(sub == 0 ? w3.x : sub == 1 ? w3.y : sub == 2 ? w3.z : w3.w);
+        const uint32_t gm = (uint32_t)(__ballot(hit) >> gbase) & 15u;
+        if (gm) {
+            /* rank among the group's hit children: nearest first, ties to the lower slot */
+            const float t1 = quad_xorf1(tn), t2 = quad_xorf2(tn), t3 = quad_xorf3(tn);
+            const int j1 = sub ^ 1, j2 = sub ^ 2, j3 = sub ^ 3;
+            const int rank = (((gm >> j1) & 1u) && (t1 < tn || (t1 == tn && j1 < sub)) ? 1 : 0) +
+                             (((gm >> j2) & 1u) && (t2 < tn || (t2 == tn && j2 < sub)) ? 1 : 0) +
+                             (((gm >> j3) & 1u) && (t3 < tn || (t3 == tn && j3 < sub)) ? 1 : 0);
+            const int nhit = __popc(gm);
+            const uint32_t r0 = (uint32_t)(__ballot(hit && rank == 0) >> gbase) & 15u;
+            const int next = quad_bcast(link, __ffs((int)r0) - 1);
+            if (hit && rank > 0) gst[q.sp + nhit - 1 - rank] = link; /* the nearest of them on top */
+            q.sp += nhit - 1;
+            q.node = next;
+            return false;
+        }
+    }
+    if (q.sp == 0) return true;
+    q.node = gst[--q.sp];
+    return false;
+}
+
+/* Sample-split tiles, step 1: the seed pass.  A pixel's random numbers depend only on its
+   closest hits (trace_path_tri, rtcommon.h:371-468): per surface hit two draws per light
+   whatever its shadow ray finds (:88-92), two more for the Lambert bounce off the box (:459);
+   a mesh hit (:421) or a box miss (:463-466) ends the sample; each sample starts with the two
+   strat_rand draws of its camera ray (raytracer.cl:216-224).  So one lane (COOP: one 4-lane
+   group) per pixel walks the pixel's samples with the closest-hit queries alone (camera rays
+   through the pixel's candidate list, box bounces through the tree, directions in k_tris's
+   arithmetic), draws and drops the light samples' numbers, and stores the seed at the first
+   sample of every chunk and after the last one.  The queries are resumable: the wave steps
+   every running query and a lane whose query completed advances at once, so no chain waits for
+   its neighbours'. */
+template <bool COOP>
+__device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
+{
+    Stack stk;
+    stk.init(s_stack, a.spill, a.spill_cap);
+    const int lane = (int)(threadIdx.x & 63), gbase = COOP ? (lane & ~3) : lane;
+    CoopStack gst;
+    gst.base = (lds_int *)(s_stack + (threadIdx.x & ~63u) + (uint32_t)gbase);
+    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
+    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
+    const uint32_t spp = a.sample_rate * a.sample_rate, nch = a.split_chunks, csz = a.split_chunk;
+    const uint32_t plane = a.Wpad * a.Hpad;
+    const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
+    const uint32_t n_items = a.split_which == RT_SPLIT_BOX ? a.split_n_box : tiles_x * tiles_y * 64u;
+    const uint32_t nl = a.n_lights;
+    const float hw = uniform_f(((float)a.W) / 2.0f);
+    const float hh = uniform_f(((float)a.H) / 2.0f);
+    const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
+    bool have = false, next = false, running = false, fin = false, drained = false;
+    uint32_t x = 0, yl = 0, sample = 0, depth = 0;
+    uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
+    Seed seed = {0u, 0u};
+    V3 qo = v3(0.0f, 0.0f, 0.0f), qd = v3(0.0f, 0.0f, 1.0f);
+    TravState ts;
+    ts.node = 0;
+    ts.best = -1;
+    ts.best_orig = -1;
+    ts.best_t = kInf;
+    ts.inv = qo;
+    ts.oi = qo;
+    CoopQuery cq;
+    coop_begin(cq, qo, qd, kInf);
+    uint32_t st_steps = 0, st_box = 0, st_t0 = 0; /* diagnostics (RT_PIXEL_STATS): per pixel */
+    for (;;) {
+        /* lanes (COOP: groups) without a pixel take the next ones of the queue */
+        /* takers: the first split_gpw lanes (COOP: 4-lane groups) of the wave */
+        const uint32_t gpw = a.split_gpw ? a.split_gpw : (COOP ? 16u : 64u);
+        const unsigned long long idle = __ballot(!have && lane == gbase && (uint32_t)(COOP ? lane >> 2 : lane) < gpw);
+        if (idle && !drained) {
+            /* a batch per wave of as many items as it has takers */
+            uint32_t item = batch_take(a.split_counter, idle, bnext, bend, gpw);
+            if (COOP) item = __shfl(item, gbase);
+            drained = bnext >= n_items;
+            if (!have) {
+                if (item < n_items) {
+                    bool take;
+                    if (a.split_which == RT_SPLIT_BOX) { /* the box pixels (long chains), by slot */
+                        const uint32_t p = a.split_box[item];
+                        x = p % a.W;
+                        yl = p / a.W;
+                        take = true;
+                    } else {
+                        uint32_t tile = item >> 6;
+                        const uint32_t in = item & 63u;
+                        if (a.tile_order) tile = a.tile_order[tile];
+                        x = (tile % tiles_x) * 8u + (in & 7u);
+                        yl = (tile / tiles_x) * 8u + (in >> 3);
+                        take = x < a.W && yl < a.Hl;
+                        if (take && a.split_which == RT_SPLIT_MESH) take = a.pixel_class[(size_t)yl * a.W + x] == -1;
+                    }
+                    if (take) {
+                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                        seed.x = a.seeds[slot];
+                        seed.y = a.seeds[plane + slot];
+                        sample = 0;
+                        have = true;
+                        next = true;
+                        if (a.pixel_stats) {
+                            st_steps = st_box = 0;
+                            st_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        }
+                    }
+                }
+            }
+        }
+        if (!__any(have)) {
+            if (drained) break;
+            continue;
+        }
+        /* a new sample: the chunk's first seed, then the camera ray and its query */
+        if (next) {
+            next = false;
+            if ((sample == spp || sample % csz == 0u) && lane == gbase) {
+                const uint32_t c = sample == spp ? nch : sample / csz;
+                reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * (nch + 1u) + c] =
+                    make_uint2(seed.x, seed.y);
+            }
+            if (sample == spp) {
+                have = false;
+                if (a.pixel_stats && lane == gbase) {
+                    uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
+                    ps[0] = st_t0;
+                    ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                    ps[2] = st_steps;
+                    ps[3] = st_box;
+                    ps[4] = 1u + (uint32_t)a.split_which;
+                }
+            } else {
+                const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
+                const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
+                const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
+                qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+                qd = camera_dir(a.cam, fa - hw, fb - hh);
+                depth = 0;
+                if (COOP) coop_begin(cq, qo, qd, kInf);
+                else trav_begin(ts, stk, qo, qd, kInf);
+                running = true;
+                if (a.list_code) { /* the pixel's candidate list, as k_tris takes it */
+                    const uint32_t code = a.list_code[yl * a.W + x];
+                    const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
+                    const uint32_t pc = (code & (RT_LIST_MAX - 1u)) + 1u, first = block + ((code >> RT_LIST_BITS) << 3);
+                    if (code == RT_LIST_EMPTY) {
+                        running = false;
+                        ts.best = -1;
+                        cq.best = -1;
+                        fin = true;
+                    } else if (code != RT_LIST_NONE) {
+                        for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
+                            const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
+                            const int v = ~(int)(((first + 8u * b) << 3) | (k - 1u));
+                            if (COOP) {
+                                if (lane == gbase) gst[cq.sp] = v;
+                                ++cq.sp;
+                            } else {
+                                stk.push(v);
+                            }
+                        }
+                        const int n0 = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
+                        if (COOP) cq.node = n0;
+                        else ts.node = n0;
+                    }
+                }
+            }
+        }
+        /* step the running queries (the box pixels' chains at top priority: they run beside the
+           chunk tasks and set when the box pixels' chunks can start) */
+        if (a.split_which == RT_SPLIT_BOX) __builtin_amdgcn_s_setprio(3);
+#pragma unroll
+        for (int u = 0; u < RT_SEED_UNROLL; ++u) {
+            if (running) {
+                ++st_steps;
+                bool done;
+                if (COOP) {
+                    done = coop_step(nodes, tris, cq, gst, qo, qd, RT_SMALL_F);
+                } else {
+                    TravCounts tc = {0u, 0u, 0u};
+                    done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
+                }
+                if (done) {
+                    running = false;
+                    fin = true;
+                }
+            }
+        }
+        /* lanes whose query completed: the segment's draws, then the bounce or the next sample */
+        if (fin) {
+            fin = false;
+            bool sample_done = true;
+            if ((COOP ? cq.best : ts.best) >= 0) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
+                for (uint32_t l = 0; l < nl; ++l) {
+                    (void)frand(seed);
+                    (void)frand(seed);
+                }
+            } else { /* the enclosing box (rtcommon.h:425-466) */
+                const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
+                if (depth == 0) ++st_box;
+                if (hd > RT_SMALL_F && hd < kInf) {
+                    const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
+                    const V3 hn = box_normal(hp, bw, bh, bw);
+                    for (uint32_t l = 0; l < nl; ++l) {
+                        (void)frand(seed);
+                        (void)frand(seed);
+                    }
+                    const float r1 = frand(seed);
+                    const float r2 = frand(seed);
+                    const float ct = rt_sqrtf(1.0f - r1);
+                    const float st = rt_sqrtf(1.0f - ct * ct);
+                    const float phi = RT_M_2PI_F * r2;
+                    float sphi, cphi;
+                    rt_sincosf(phi, &sphi, &cphi);
+                    qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
+                    qo = hp;
+                    ++depth;
+                    if (depth <= a.max_depth) {
+                        sample_done = false;
+                        if (COOP) coop_begin(cq, qo, qd, kInf);
+                        else trav_begin(ts, stk, qo, qd, kInf);
+                        running = true;
+                    }
+                }
+            }
+            if (sample_done) {
+                ++sample;
+                next = true;
+            }
+        }
+    }
 }
 
 /* ======================================================================== */
@@ -663,7 +1052,8 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
     const uint32_t tiles_x = (a.W + 7u) >> 3;
     const uint32_t tiles_y = (a.Hl + 7u) >> 3;
     const uint32_t n_items = tiles_x * tiles_y * 64u;
-    const uint32_t n_tasks = SPLIT ? n_items * a.split_chunks : n_items;
+    const uint32_t n_tasks =
+        SPLIT ? (a.split_which == RT_SPLIT_BOX ? a.split_n_box : n_items) * a.split_chunks : n_items;
     /* launch-uniform values pinned to SGPRs (readfirstlane), so they neither occupy nor
        spill vector registers */
     const float hw = uniform_f(((float)a.W) / 2.0f);
@@ -937,18 +1327,33 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                 if (item >= n_tasks) {
                     mode = M_DONE;
                 } else {
-                    /* 8 x 8 pixel tiles, row-major over the (local) frame; SPLIT: a tile's chunk
-                       0 of its 64 pixels, then chunk 1, ... */
+                    /* 8 x 8 pixel tiles, row-major over the (local) frame; SPLIT over tiles: a
+                       tile's chunk 0 of its 64 pixels, then chunk 1, ... (the mesh pixels only when
+                       the box pixels run apart: the 16 chunk layers of a tile run side by side,
+                       10 % faster than layer after layer over the frame); SPLIT over the box
+                       pixels: a pixel's chunks in turn */
                     uint32_t tile = item >> 6, chunk = 0;
                     const uint32_t in = item & 63u;
-                    if (SPLIT) {
-                        chunk = tile % a.split_chunks;
-                        tile = tile / a.split_chunks;
+                    bool take;
+                    if (SPLIT && a.split_which == RT_SPLIT_BOX) {
+                        const uint32_t slot = item / a.split_chunks;
+                        chunk = item - slot * a.split_chunks;
+                        const uint32_t p = a.split_box[slot];
+                        x = p % a.W;
+                        yl = p / a.W;
+                        take = true;
+                    } else {
+                        if (SPLIT) {
+                            chunk = tile % a.split_chunks;
+                            tile = tile / a.split_chunks;
+                        }
+                        if (a.tile_order) tile = a.tile_order[tile];
+                        x = (tile % tiles_x) * 8u + (in & 7u);
+                        yl = (tile / tiles_x) * 8u + (in >> 3);
+                        take = x < a.W && yl < a.Hl;
+                        if (SPLIT && take && a.split_which == RT_SPLIT_MESH)
+                            take = a.pixel_class[(size_t)yl * a.W + x] == -1;
                     }
-                    if (a.tile_order) tile = a.tile_order[tile];
-                    x = (tile % tiles_x) * 8u + (in & 7u);
-                    yl = (tile / tiles_x) * 8u + (in >> 3);
-                    bool take = x < a.W && yl < a.Hl;
                     if (RT_DIAG_ONE_PIXEL) { /* diagnostics build: the target pixel and the diag_k - 1 pixels
                                                 after it in its 8 x 8 tile (in-tile order, wrapping) */
                         const uint32_t dx = a.diag_pixel % a.W, dy = a.diag_pixel / a.W;
@@ -1047,7 +1452,7 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                     if (!shadow && depth == 0 && a.list_code) { /* a camera ray: the pixel's candidate list */
                         const uint32_t code = a.list_code[yl * a.W + x];
                         const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
-                        const uint32_t pc = (code & 31u) + 1u, first = block + ((code >> 5) << 3);
+                        const uint32_t pc = (code & (RT_LIST_MAX - 1u)) + 1u, first = block + ((code >> RT_LIST_BITS) << 3);
                         if (code == RT_LIST_EMPTY) { /* no triangle can be accepted by any of the pixel's camera rays */
                             running = false;
                             ts.best = -1;
@@ -1566,164 +1971,11 @@ __global__ __launch_bounds__(64) void k_defer_finish(RtTriLaunch a)
     }
 }
 
-/* Sample-split tiles, step 1: the seed pass.  A pixel's random numbers depend only on its
-   closest hits (trace_path_tri, rtcommon.h:371-468): per surface hit two draws per light
-   whatever its shadow ray finds (:88-92), two more for the Lambert bounce off the box (:459);
-   a mesh hit (:421) or a box miss (:463-466) ends the sample; each sample starts with the two
-   strat_rand draws of its camera ray (raytracer.cl:216-224).  So one lane per pixel walks the
-   pixel's samples with the closest-hit queries alone (camera rays through the pixel's
-   candidate list, box bounces through the tree, directions in k_tris's arithmetic), draws and
-   drops the light samples' numbers, and stores the seed at the first sample of every chunk
-   and after the last one.  The queries are resumable: the wave steps every running query and
-   a lane whose query completed advances at once, so no chain waits for its neighbours'. */
-#ifndef RT_SEED_UNROLL
-#define RT_SEED_UNROLL 2
-#endif
+template <bool COOP>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLaunch a)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
-    Stack stk;
-    stk.init(s_stack, a.spill, a.spill_cap);
-    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
-    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
-    const uint32_t spp = a.sample_rate * a.sample_rate, nch = a.split_chunks, csz = a.split_chunk;
-    const uint32_t plane = a.Wpad * a.Hpad;
-    const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
-    const uint32_t n_items = tiles_x * tiles_y * 64u;
-    const uint32_t nl = a.n_lights;
-    const float hw = uniform_f(((float)a.W) / 2.0f);
-    const float hh = uniform_f(((float)a.H) / 2.0f);
-    const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
-    bool have = false, next = false, running = false, fin = false, drained = false;
-    uint32_t x = 0, yl = 0, sample = 0, depth = 0;
-    uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
-    Seed seed = {0u, 0u};
-    V3 qo = v3(0.0f, 0.0f, 0.0f), qd = v3(0.0f, 0.0f, 1.0f);
-    TravState ts;
-    ts.node = 0;
-    ts.best = -1;
-    ts.best_orig = -1;
-    ts.best_t = kInf;
-    ts.inv = qo;
-    ts.oi = qo;
-    for (;;) {
-        /* lanes without a pixel take the next ones of the (LPT-ordered) queue */
-        const unsigned long long idle = __ballot(!have);
-        if (idle && !drained) {
-            const uint32_t item = batch_take(a.split_counter, idle, bnext, bend);
-            drained = bnext >= n_items;
-            if (!have) {
-                if (item < n_items) {
-                    uint32_t tile = item >> 6;
-                    const uint32_t in = item & 63u;
-                    if (a.tile_order) tile = a.tile_order[tile];
-                    x = (tile % tiles_x) * 8u + (in & 7u);
-                    yl = (tile / tiles_x) * 8u + (in >> 3);
-                    if (x < a.W && yl < a.Hl) {
-                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
-                        seed.x = a.seeds[slot];
-                        seed.y = a.seeds[plane + slot];
-                        sample = 0;
-                        have = true;
-                        next = true;
-                    }
-                }
-            }
-        }
-        if (!__any(have)) {
-            if (drained) break;
-            continue;
-        }
-        /* a new sample: the chunk's first seed, then the camera ray and its query */
-        if (next) {
-            next = false;
-            if (sample == spp || sample % csz == 0u) {
-                const uint32_t c = sample == spp ? nch : sample / csz;
-                reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * (nch + 1u) + c] =
-                    make_uint2(seed.x, seed.y);
-            }
-            if (sample == spp) {
-                have = false;
-            } else {
-                const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
-                const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
-                const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
-                const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
-                qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
-                qd = camera_dir(a.cam, fa - hw, fb - hh);
-                depth = 0;
-                trav_begin(ts, stk, qo, qd, kInf);
-                running = true;
-                if (a.list_code) { /* the pixel's candidate list, as k_tris takes it */
-                    const uint32_t code = a.list_code[yl * a.W + x];
-                    const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
-                    const uint32_t pc = (code & 31u) + 1u, first = block + ((code >> 5) << 3);
-                    if (code == RT_LIST_EMPTY) {
-                        running = false;
-                        ts.best = -1;
-                        fin = true;
-                    } else if (code != RT_LIST_NONE) {
-                        for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
-                            const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
-                            stk.push(~(int)(((first + 8u * b) << 3) | (k - 1u)));
-                        }
-                        ts.node = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
-                    }
-                }
-            }
-        }
-        /* step the running queries */
-#pragma unroll
-        for (int u = 0; u < RT_SEED_UNROLL; ++u) {
-            if (running) {
-                TravCounts tc = {0u, 0u, 0u};
-                if (trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc)) {
-                    running = false;
-                    fin = true;
-                }
-            }
-        }
-        /* lanes whose query completed: the segment's draws, then the bounce or the next sample */
-        if (fin) {
-            fin = false;
-            bool sample_done = true;
-            if (ts.best >= 0) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
-                for (uint32_t l = 0; l < nl; ++l) {
-                    (void)frand(seed);
-                    (void)frand(seed);
-                }
-            } else { /* the enclosing box (rtcommon.h:425-466) */
-                const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
-                if (hd > RT_SMALL_F && hd < kInf) {
-                    const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
-                    const V3 hn = box_normal(hp, bw, bh, bw);
-                    for (uint32_t l = 0; l < nl; ++l) {
-                        (void)frand(seed);
-                        (void)frand(seed);
-                    }
-                    const float r1 = frand(seed);
-                    const float r2 = frand(seed);
-                    const float ct = rt_sqrtf(1.0f - r1);
-                    const float st = rt_sqrtf(1.0f - ct * ct);
-                    const float phi = RT_M_2PI_F * r2;
-                    float sphi, cphi;
-                    rt_sincosf(phi, &sphi, &cphi);
-                    qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
-                    qo = hp;
-                    ++depth;
-                    if (depth <= a.max_depth) {
-                        sample_done = false;
-                        trav_begin(ts, stk, qo, qd, kInf);
-                        running = true;
-                    }
-                }
-            }
-            if (sample_done) {
-                ++sample;
-                next = true;
-            }
-        }
-    }
+    seed_pass<COOP>(a, s_stack);
 }
 
 /* Sample-split tiles, step 3: per pixel, the samples' radiance summed in sample order
@@ -1956,7 +2208,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
     if (lane == 0 && tile < n_tiles) tile_base[tile] = a.list_base + base;
     if (!valid) return;
     const uint32_t rel = incl - want; /* < 64 * RT_LIST_MAX, a multiple of 8 */
-    codes[p] = (uint16_t)(!ok ? RT_LIST_NONE : n == 0 ? RT_LIST_EMPTY : (rel << 2) | (n - 1u));
+    codes[p] = (uint16_t)(!ok ? RT_LIST_NONE : n == 0 ? RT_LIST_EMPTY : ((rel >> 3) << RT_LIST_BITS) | (n - 1u));
     if (!ok || n == 0) return;
     float4 *__restrict__ lst = const_cast<float4 *>(tris) + 3ull * (a.list_base + (size_t)base + rel);
     /* The records in order of their earliest accept t, each one's r1.w carrying the NEXT
@@ -2106,19 +2358,32 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
     /* the deferred-shadow and sample-split forms only where they are used (their code costs a
        full frame 1 %) */
     if (trav == RT_TRAV_BVH4Q && a.split_chunks) {
-        /* seed pass, chunk tasks, in-order sums: three launches on one stream */
-        hipError_t e = hipMemsetAsync(a.split_counter, 0, sizeof(uint32_t), st);
+        /* the chunk tasks (queue cursor a.work_counter, reset here) */
+        const hipError_t e = hipMemsetAsync(a.work_counter, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(k_split_seeds, dim3(a.split_seed_blocks), block, 0, st, a);
-        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
         RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, false, true);
-        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(k_split_finish, dim3((a.W * a.Hl + RT_BLOCK - 1) / RT_BLOCK), block, 0, st, a);
     } else if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR, false, false);
     else if (trav == RT_TRAV_BVH4Q && a.n_defer) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, true, false);
     else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, false, false);
     else RT_LAUNCH_TRIS(RT_TRAV_BVH4, false, false);
 #undef RT_LAUNCH_TRIS
+    return (int)hipGetLastError();
+}
+
+int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const hipError_t e = hipMemsetAsync(a.split_counter, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return (int)e;
+    if (a.split_coop) hipLaunchKernelGGL(k_split_seeds<true>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
+    else hipLaunchKernelGGL(k_split_seeds<false>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+int rt_launch_split_finish(const RtTriLaunch &a, void *stream)
+{
+    hipLaunchKernelGGL(k_split_finish, dim3((a.W * a.Hl + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0,
+                       (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 

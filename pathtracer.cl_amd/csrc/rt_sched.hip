@@ -88,13 +88,19 @@ __global__ __launch_bounds__(256) void k_tile_cost(const uint32_t *__restrict__ 
     idx[t] = t;
 }
 
-/* box[p] = 1 if some probe ray of pixel p missed the mesh; box[npx] = 0 (the scan's total) */
+/* box[p] = 1 if some probe ray missed the mesh, or (step_max > 0) its probe queries took more
+   than step_max steps in all (a long chain on the mesh: grazing camera rays without a candidate
+   list); box[npx] = 0 (the scan's total) */
 __global__ __launch_bounds__(256) void k_box_flags(const uint32_t *__restrict__ flags, uint32_t npx, uint32_t pn2,
-                                                   uint32_t *__restrict__ box)
+                                                   uint32_t step_max, uint32_t *__restrict__ box)
 {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p < npx) box[p] = (flags[p] >> RT_PROBE_HIT_SHIFT) < pn2 ? 1u : 0u;
-    else if (p == npx) box[p] = 0u;
+    if (p < npx) {
+        const uint32_t v = flags[p];
+        box[p] = (v >> RT_PROBE_HIT_SHIFT) < pn2 || (step_max && (v & RT_PROBE_STEP_MASK) > step_max) ? 1u : 0u;
+    } else if (p == npx) {
+        box[p] = 0u;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_classify(const uint32_t *__restrict__ box, const uint32_t *__restrict__ scan,
@@ -189,10 +195,11 @@ int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_
     return (int)e;
 }
 
-int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, void *stream)
+int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, uint32_t step_max,
+                      void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_box_flags, dim3((npx + 1u + 255u) / 256u), dim3(256), 0, st, flags, npx, pn2, s.box);
+    hipLaunchKernelGGL(k_box_flags, dim3((npx + 1u + 255u) / 256u), dim3(256), 0, st, flags, npx, pn2, step_max, s.box);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     size_t bytes = s.tmp_bytes;

@@ -1,7 +1,7 @@
 """Render one row-stripe tile (or the whole frame) of a bench configuration a few times, for
 kernel traces (rocprofv3 --kernel-trace --stats) of one launch form; RT_* knobs from the env.
 
-    python profiles/render_tile.py [--config dragon] [--tile 8,8,0] [--reps 3]
+    python profiles/render_tile.py [--config dragon] [--tile 8,8,0] [--reps 3] [--lib build.so]
 """
 import argparse
 import sys
@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--config", default="dragon")
     ap.add_argument("--tile", default=None)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="another build of librtmi.so (A/B)")
     args = ap.parse_args()
     import torch
     import ptload
@@ -23,7 +24,7 @@ def main():
     pt = ptload.load()
     sc = pt.scenes
     W, H, sr = {"dragon": (1920, 1080, 16), "lucy": (4096, 4096, 4), "bunny": (1024, 1024, 1)}[args.config]
-    rt = pt.RayTracer(0)
+    rt = pt.RayTracer(0, lib_path=args.lib)
     rt.setSpheres(sc.ply_scene())
     c = sc.PLY_CAMERA
     rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])

@@ -1,0 +1,69 @@
+"""Seed-pass chains of a sample-split tile, per pixel (diagnostics; RT_SPLIT=1 + RT_PIXEL_STATS):
+duration, traversal steps and camera rays that missed the mesh, for the mesh-class and the
+box-class pixels (the probe's classes).
+
+    python profiles/seed_stats.py [--tile 8,8,0]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tile", default="8,8,0")
+    args = ap.parse_args()
+    os.environ["RT_SPLIT"] = "1"
+    import numpy as np
+    import ptload
+
+    pt = ptload.load()
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 16
+    Wp, Hp = sc.padded_dims(W, H)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(sc.ply_scene())
+    c = sc.PLY_CAMERA
+    rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS["dragon"]))
+    tile = tuple(int(v) for v in args.tile.split(","))
+    rows = len(np.arange(H)[(np.arange(H) // tile[0]) % tile[1] == tile[2]])
+    out = np.zeros(W * rows * 4, np.float32)
+    rt.setSeeds(Wp, Hp, sc.default_seeds(Wp, Hp))
+    rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
+    path = os.path.join(tempfile.gettempdir(), f"seed_{os.getpid()}.bin")
+    os.environ["RT_PIXEL_STATS"] = path
+    rt.setSeeds(Wp, Hp, sc.default_seeds(Wp, Hp))
+    rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
+    os.environ.pop("RT_PIXEL_STATS")
+    st = np.fromfile(path, np.uint32).reshape(-1, 8).astype(np.int64)
+    os.remove(path)
+    t0 = st[st[:, 4] > 0, 0].min()
+    res = {"tile": tile, "pixels": int(len(st))}
+    for name, k in (("mesh", 2), ("box", 3)):
+        m = st[:, 4] == k
+        if not m.any():
+            continue
+        dur = (st[m, 1] - st[m, 0]) / 1e5
+        end = (st[m, 1] - t0) / 1e5
+        steps, box = st[m, 2], st[m, 3]
+        order = np.argsort(-dur)[:12]
+        res[name] = {"pixels": int(m.sum()), "end_ms_max": round(float(end.max()), 2),
+                     "dur_ms": {q: round(float(np.quantile(dur, q / 100)), 2) for q in (50, 90, 99, 100)},
+                     "steps": {q: int(np.quantile(steps, q / 100)) for q in (50, 90, 99, 100)},
+                     "missed_camera_rays": {q: int(np.quantile(box, q / 100)) for q in (50, 90, 99, 100)},
+                     "pixels_with_misses": int((box > 0).sum()),
+                     "longest": [[round(float(dur[i]), 2), int(steps[i]), int(box[i])] for i in order]}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

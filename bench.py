@@ -366,7 +366,8 @@ def main():
         line["config"]["candidate_lists"] = {"on": bool(info["lists"]), "capacity_records": int(info["list_capacity"]),
                                              "records": int(info["list_records"]),
                                              "pixels_on_tree": int(info["list_pixels_tree"])}
-        line["config"]["pixels_deferred"] = int(info["pixels_deferred"])
+        line["config"]["sample_split"] = {"chunks_per_pixel": int(info.get("split_chunks", 0)),
+                                          "long_chains": int(info.get("pixels_long", 0))}
     line.update(cold)
     if comm_note:
         line["comm_note"] = comm_note

@@ -92,7 +92,7 @@ typedef struct rt_counters {
                                   traversal because the answer cannot change the pixel:
                                   tmax <= tmin, or cos(wi) <= 0 (rtcommon.h:93-95) */
     uint64_t clocks_shade;     /* shader clocks waves spent advancing paths (counting launches) */
-    uint64_t pixels_deferred;  /* box pixels whose shadow rays were deferred (k_defer_shadow) */
+    uint64_t pixels_long;      /* sample-split render: long chains (box pixels) run on their own stream */
 } rt_counters;
 
 /* ---- lifetime: RayTracerCL::RayTracerCL / init / ~RayTracerCL (RayTracerCL.cpp:52-145) ---- */
@@ -191,8 +191,8 @@ int rt_set_counting(rt_ctx *ctx, int enable);             /* count nodes/tris in
 /* Device time of the last render's kernel (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(const rt_ctx *ctx, float *ms);
 /* The same time split at the start of the main path kernel: the camera-ray candidate-list
-   pre-pass of a triangle render (0 without one), then k_tris (+ the deferred-shadow
-   kernels), ms. */
+   pre-pass of a triangle render (0 without one), then k_tris (+ a sample-split render's seed
+   passes and in-order sums), ms. */
 int rt_last_kernel_split_ms(const rt_ctx *ctx, float *prepass_ms, float *main_ms);
 
 /* What the last render did beyond the reference's launch (the triangle kernel's own
@@ -206,7 +206,7 @@ typedef struct rt_render_info {
     uint64_t list_records;     /* records the pixels' lists took (read on the first call) */
     uint32_t list_pixels_tree; /* pixels without a list (over RT_LIST_MAX candidates, a deep
                                   frustum stack, or the area full): their camera rays took the tree */
-    uint32_t pixels_deferred;  /* box pixels whose shadow rays were deferred */
+    uint32_t pixels_long;      /* sample-split render: long chains (box pixels) run on their own stream */
     uint32_t schedule_rebuilt; /* 1: the cost probe, LPT order and pixel classes were recomputed
                                   (camera, mesh, frame, tile or parameters changed) */
     uint32_t lists_rebuilt;    /* 1: the lists were built for this render (0: the previous render's,

@@ -105,7 +105,7 @@ class RtCounters(ctypes.Structure):
         ("pixel_steps_max", ctypes.c_uint64),
         ("rays_skipped", ctypes.c_uint64),
         ("clocks_shade", ctypes.c_uint64),
-        ("pixels_deferred", ctypes.c_uint64),
+        ("pixels_long", ctypes.c_uint64),
     ]
 
 
@@ -118,7 +118,7 @@ class RtRenderInfo(ctypes.Structure):
         ("list_capacity", ctypes.c_uint64),
         ("list_records", ctypes.c_uint64),
         ("list_pixels_tree", ctypes.c_uint32),
-        ("pixels_deferred", ctypes.c_uint32),
+        ("pixels_long", ctypes.c_uint32),
         ("schedule_rebuilt", ctypes.c_uint32),
         ("lists_rebuilt", ctypes.c_uint32),
         ("schedule_host_ms", ctypes.c_double),

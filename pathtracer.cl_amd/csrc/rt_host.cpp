@@ -114,24 +114,16 @@ struct rt_ctx {
     uint32_t order_cap = 0;
     uint32_t *d_flags = nullptr; /* cost probe per pixel (k_probe_cost) */
     RtSchedScratch sched;        /* the device-side schedule (rt_sched.hip) */
-    /* deferred shadow rays of box pixels (k_tris -> k_defer_shadow -> k_defer_finish) */
-    int32_t *d_class = nullptr;  /* per pixel: -1 mesh, -2 box, >= 0 box with a defer slot */
+    int32_t *d_class = nullptr;  /* per pixel: -1 mesh, -2 box, >= 0 a long chain's slot (sample-split) */
     size_t class_bytes = 0;
-    uint32_t *d_defer_pixel = nullptr; /* per slot: yl * W + x */
-    float *d_defer_rec = nullptr;
-    uint8_t *d_defer_seg = nullptr, *d_defer_vis = nullptr;
-    uint32_t *d_defer_queue = nullptr, *d_defer_qcount = nullptr;
-    size_t defer_rec_cap = 0, defer_seg_cap = 0, defer_slot_cap = 0; /* allocated entries */
-    uint32_t n_defer = 0;
-    int defer = -1;          /* RT_DEFER: 1 on, 0 off, unset = auto (on when the launch has fewer than
-                                2 pixels per resident lane at sampleRate >= 4: tiles of a multi-GPU
-                                many-sample frame) */
-    size_t defer_mb = 16384; /* RT_DEFER_MB: device memory cap of the defer (or sample-split) buffers */
+    size_t split_mb = 16384; /* RT_SPLIT_MB: device memory cap of the sample-split buffers */
     /* sample-split tiles (k_split_seeds -> k_tris chunks -> k_split_finish) */
-    int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (see split_wanted) */
-    bool seed_coop = true;            /* RT_SEED_COOP=0: the seed pass with one lane per query (A/B) */
-    uint32_t split_probe = 4;         /* RT_SPLIT_PROBE: probe rays per pixel side in a split render (A/B) */
-    uint32_t split_gpw = 0;           /* RT_SPLIT_GPW: box-pixel chains per seed-pass wave (A/B) */
+    int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (split_wanted) */
+    /* the long chains' seed pass with 4 lanes per query (one lane per query: 8-way tile 24 -> 19 ms
+       for the chains); 4 x 4 probe rays per pixel to find them */
+    bool seed_coop = true;
+    uint32_t split_probe = 4;
+    uint32_t split_gpw = 0; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
     float *d_split_col = nullptr;     /* per sample and pixel: its radiance */
     uint32_t *d_split_counter = nullptr; /* [0]: the seed pass's cursor, [32]: the box pixels' (own line) */
@@ -184,7 +176,7 @@ struct rt_ctx {
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
     rt_counters last = {};
-    uint32_t last_deferred = 0; /* deferred box pixels of the last triangle launch */
+    uint32_t last_long = 0; /* long chains run apart by the last triangle launch (sample-split) */
     bool have_timing = false;
     const float *last_out = nullptr; /* device framebuffer of the last render (rt_read) */
     size_t last_bytes = 0;
@@ -397,51 +389,18 @@ int grid_blocks(rt_ctx *c, int trav, bool count, int form, int *out)
     return RT_OK;
 }
 
-/* Deferred-shadow buffers for n slots: per slot, one 32-B record per (sample, segment, light),
-   a segment-kind byte per (sample, segment), a visibility byte and a queue entry per record. */
-int ensure_defer(rt_ctx *c, uint64_t n, uint64_t recs, uint64_t segs)
-{
-    if (c->defer_slot_cap < n) {
-        free_dev(c->d_defer_pixel);
-        c->d_defer_pixel = nullptr;
-        c->defer_slot_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_defer_pixel, n * 4));
-        c->defer_slot_cap = n;
-    }
-    if (c->defer_rec_cap < n * recs) {
-        free_dev(c->d_defer_rec);
-        free_dev(c->d_defer_vis);
-        free_dev(c->d_defer_queue);
-        c->d_defer_rec = nullptr;
-        c->d_defer_vis = nullptr;
-        c->d_defer_queue = nullptr;
-        c->defer_rec_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_defer_rec, n * recs * 32));
-        HIPCHK(c, hipMalloc(&c->d_defer_vis, n * recs));
-        HIPCHK(c, hipMalloc(&c->d_defer_queue, n * recs * 4));
-        c->defer_rec_cap = n * recs;
-    }
-    if (c->defer_seg_cap < n * segs) {
-        free_dev(c->d_defer_seg);
-        c->d_defer_seg = nullptr;
-        c->defer_seg_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_defer_seg, n * segs));
-        c->defer_seg_cap = n * segs;
-    }
-    if (!c->d_defer_qcount) HIPCHK(c, hipMalloc(&c->d_defer_qcount, 2 * sizeof(uint32_t)));
-    return RT_OK;
-}
-
 /* Sample-split tiles (RT_SPLIT): when a launch has fewer pixels than about two
    per resident lane — a multi-GPU tile of a many-sample frame — every lane holds one pixel
    from the start and the launch lasts as long as its slowest pixel's serial sample chain.
    Splitting each pixel's samples into chunks (seeded by a closest-hit-only pass) turns it back
-   into a queue of many short tasks. */
+   into a queue of many short tasks.  Automatic below two pixels per lane at sampleRate >= 4
+   (dragon class, 1920x1080 at 256 spp, one rank's row-stripe tile: 4-way 42.1 -> 35.6 ms, 8-way
+   29.2 -> 24.8 ms; 2-way 59.3 -> 68.3 and the whole frame 96.5 -> 127.4 ms would lose:
+   profiles/r03v). */
 bool split_wanted(const rt_ctx *c, uint64_t npx, uint64_t lanes)
 {
-    (void)npx;
-    (void)lanes;
-    return c->split == 1 && c->sample_rate >= 2;
+    if (c->sample_rate < 2) return false;
+    return c->split == 1 || (c->split < 0 && npx < 2 * lanes && c->sample_rate >= 4);
 }
 
 /* Sample-split buffers: per pixel (nch + 1) seed pairs, per sample and pixel an RGB radiance. */
@@ -502,7 +461,6 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         if (e) return hip_fail(c, (hipError_t)e, "box-pixel split launches");
         HIPCHK(c, hipEventRecord(c->ev_box, c->stream2));
     }
-    if (n_box && getenv("RT_SPLIT_SERIAL")) HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0)); /* diagnostics */
     RtTriLaunch m = a; /* the mesh pixels' seed pass: short chains, one lane each */
     m.split_coop = 0;
     int e = rt_launch_split_seeds(m, st);
@@ -516,27 +474,25 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
    camera ray that hits the mesh ends after one shadow query per light (rtcommon.h:411-421),
    one that misses bounces off the box up to maxDepth+1 times with shadow queries at each
    (rtcommon.h:425-461), and each query costs its traversal steps.  A probe (k_probe_cost)
-   traces a 2x2 grid of camera rays per pixel and, on mesh hits, their shadow rays toward the
-   light centres with the real traversal, counting steps.  From it the device computes the
-   tile costs, the LPT order (most expensive 8x8 tiles first, so the launch does not end on a
-   tail of long pixels) and the pixel classes (rt_sched.hip) — no host round trip, except one
-   4-byte read of the box-pixel count when the launch defers shadow rays (to size the
-   buffers).  Box pixels (some probe ray missed the mesh: the long serial chains) get a slot
-   in the deferred-shadow buffers in pixel order up to RT_DEFER_MB of device
-   memory; further box pixels trace their shadow rays inline (class -2).  Scheduling only:
-   every pixel's result is independent of when it is rendered.  Cached until camera, mesh,
-   traversal, frame, tile or path parameters change. */
+   traces a grid of camera rays per pixel (2x2; 4x4 for a sample-split render) and, on mesh
+   hits, their shadow rays toward the light centres with the real traversal, counting steps.
+   From it the device computes the tile costs, the LPT order (most expensive 8x8 tiles first,
+   so the launch does not end on a tail of long pixels) and the pixel classes (rt_sched.hip).
+   A sample-split render (split_wanted) also takes its long chains from it — the box pixels
+   (some probe ray missed the mesh) and the mesh pixels whose probe took more than 96 steps per
+   ray — at the price of one 4-byte read (their count, to size the slot list).  Scheduling
+   only: every pixel's result is independent of when and where it is rendered.  Cached until
+   camera, mesh, traversal, frame, tile or path parameters change. */
 int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
 {
     const uint32_t W = a.W, hl = a.Hl;
-    /* everything the order, the pixel classes and the defer slots depend on — including the
-       traversal (only the compressed tree is probed and only its kernel form records deferred
-       shadow rays: a key without it would hand a BVH4F / linear launch the stale slots) */
+    /* everything the order and the pixel classes depend on — including the traversal (only
+       the compressed tree is probed: a key without it would hand a BVH4F / linear launch stale
+       classes) */
     const uintptr_t np = reinterpret_cast<uintptr_t>(a.nodes);
     std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
                                  (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks,
-                                 c->sample_rate, (uint32_t)(c->defer + 1), (uint32_t)(c->split + 1),
-                                 (uint32_t)trav_kind(c), (uint32_t)np,
+                                 c->sample_rate, (uint32_t)(c->split + 1), (uint32_t)trav_kind(c), (uint32_t)np,
                                  (uint32_t)((uint64_t)np >> 32)};
     const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
@@ -544,7 +500,7 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     c->schedule_rebuilt = false;
     if (key == c->order_key) return RT_OK;
     c->order_key.clear();
-    c->n_defer = 0;
+    c->n_split_box = 0;
     if (trav_kind(c) != RT_TRAV_BVH4Q || a.nodes != reinterpret_cast<const float *>(c->d_nodes4q)) {
         /* the probe walks the compressed tree with its spill layout: other traversal kinds
            (measurement variants) keep the row-major queue and no classes */
@@ -576,48 +532,18 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         HIPCHK(c, hipMalloc(&c->d_order, n_t * sizeof(uint32_t)));
         c->order_cap = n_t;
     }
+    const bool split = split_wanted(c, npx, (uint64_t)blocks * RT_BLOCK);
     RtTriLaunch pa = a;
-    /* a sample-split render also takes its box pixels (whose long chains run apart) from the
-       probe: a denser grid finds more of the silhouette pixels whose samples partly miss */
-    pa.probe_n = split_wanted(c, (uint64_t)W * hl, (uint64_t)blocks * RT_BLOCK) && c->sample_rate >= 4
-                     ? c->split_probe
-                     : probe_n(c->sample_rate);
+    pa.probe_n = split && c->sample_rate >= 4 ? c->split_probe : probe_n(c->sample_rate);
     const uint32_t pn2 = pa.probe_n * pa.probe_n;
     int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
     e = rt_sched_order(c->sched, c->d_flags, W, hl, pn2, (uint32_t)c->lights.size(), c->max_depth, c->d_order, st);
     if (e) return hip_fail(c, (hipError_t)e, "tile order");
-    /* a sample-split render also runs the probe's long mesh chains (more than 96 steps per probe
-       ray: grazing camera rays without a candidate list) beside the box pixels' */
-    const bool split = split_wanted(c, npx, (uint64_t)blocks * RT_BLOCK);
     e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? 96u * pn2 : 0u, st);
     if (e) return hip_fail(c, (hipError_t)e, "box-pixel scan");
-    /* Deferral shortens the box chains but moves their shadow queries into a second launch
-       that cannot use the tail of the first: it pays where the chains set the frame time (a
-       tile with few pixels per lane) of a many-sample frame, not on a full frame (dragon
-       1920x1080: 161.7 -> 173.8 ms; its N = 2 tiles 110 -> 96 ms; profiles/r02g) nor on short
-       chains (bunny class 1024^2 at 1 spp: 0.95 -> 1.35 ms, r02u).  (r02z, with the candidate
-       lists: the 2-way dragon tile, 1.04M pixels, 65.5 ms deferred against 60.7 inline; the
-       4-way 39 vs 46 ms, the 8-way 30 vs 44 ms: the line sits below two pixels per resident
-       lane.) */
-    const uint64_t lanes = (uint64_t)blocks * RT_BLOCK;
-    const bool use = !split_wanted(c, npx, lanes) &&
-                     (c->defer == 1 || (c->defer < 0 && npx < 2 * lanes && c->sample_rate >= 4));
-    const uint64_t spp = (uint64_t)c->sample_rate * c->sample_rate, nd = c->max_depth + 1u;
-    const uint64_t nl = c->lights.size();
-    const uint64_t recs = spp * nd * nl; /* records per slot */
-    uint64_t max_slots = 0;
-    if (use && nl > 0 && spp > 0 && spp <= 1024 && recs > 0) {
-        const uint64_t bytes_per_slot = recs * (32 + 1 + 4) + spp * nd + 4;
-        max_slots = ((uint64_t)c->defer_mb << 20) / bytes_per_slot;
-        max_slots = std::min<uint64_t>(max_slots, 0xffffffffull / recs);
-    }
-    uint64_t n = 0;
-    c->n_split_box = 0;
-    if (split) {
-        /* sample-split tiles: every box pixel (some probe ray missed the mesh: the long chains)
-           gets a slot; their seed pass and chunks run on a stream of their own */
-        uint32_t n_box = 0;
+    uint32_t n_box = 0;
+    if (split) { /* every long chain gets a slot: their seed pass and chunks run on a stream of their own */
         HIPCHK(c, hipMemcpyAsync(&n_box, c->sched.scan + npx, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (c->split_box_cap < n_box) {
@@ -627,27 +553,10 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
             HIPCHK(c, hipMalloc(&c->d_split_box, (size_t)n_box * 4));
             c->split_box_cap = n_box;
         }
-        e = rt_sched_classify(c->sched, (uint32_t)npx, n_box, c->d_class, c->d_split_box, st);
-        if (e) return hip_fail(c, (hipError_t)e, "pixel classes");
-        c->n_split_box = n_box;
-        c->n_defer = 0;
-        c->order_key = key;
-        c->schedule_rebuilt = true;
-        return RT_OK;
     }
-    if (max_slots) {
-        uint32_t n_box = 0; /* the one host read: the buffers are sized to the box pixels */
-        HIPCHK(c, hipMemcpyAsync(&n_box, c->sched.scan + npx, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(c, hipStreamSynchronize(st));
-        n = std::min<uint64_t>(n_box, max_slots);
-        if (n) {
-            const int r = ensure_defer(c, n, recs, spp * nd);
-            if (r != RT_OK) return r;
-        }
-    }
-    e = rt_sched_classify(c->sched, (uint32_t)npx, (uint32_t)n, c->d_class, c->d_defer_pixel, st);
+    e = rt_sched_classify(c->sched, (uint32_t)npx, n_box, c->d_class, c->d_split_box, st);
     if (e) return hip_fail(c, (hipError_t)e, "pixel classes");
-    c->n_defer = (uint32_t)n;
+    c->n_split_box = n_box;
     c->order_key = key;
     c->schedule_rebuilt = true;
     return RT_OK;
@@ -688,12 +597,8 @@ int rt_create(int device, rt_ctx **out)
     c->rng.seed(1);
     /* A/B and capacity knobs (none changes a result bit) */
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0";
-    if (const char *v = getenv("RT_DEFER")) c->defer = atoi(v) != 0 ? 1 : 0;
-    if (const char *v = getenv("RT_DEFER_MB")) c->defer_mb = (size_t)std::max(0L, atol(v));
+    if (const char *v = getenv("RT_SPLIT_MB")) c->split_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
-    if (const char *v = getenv("RT_SEED_COOP")) c->seed_coop = atoi(v) != 0;
-    if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v));
-    if (const char *v = getenv("RT_SPLIT_PROBE")) c->split_probe = (uint32_t)std::min(5, std::max(1, atoi(v)));
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -720,12 +625,6 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_order);
     free_dev(c->d_flags);
     free_dev(c->d_class);
-    free_dev(c->d_defer_pixel);
-    free_dev(c->d_defer_rec);
-    free_dev(c->d_defer_seg);
-    free_dev(c->d_defer_vis);
-    free_dev(c->d_defer_queue);
-    free_dev(c->d_defer_qcount);
     free_dev(c->d_split_seed);
     free_dev(c->d_split_col);
     free_dev(c->d_split_counter);
@@ -1086,27 +985,22 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         const int trav = trav_kind(c);
         const uint64_t items = (uint64_t)((W + 7) / 8) * ((hl + 7) / 8) * 64;
         const uint64_t item_blocks = (items + RT_BLOCK - 1) / RT_BLOCK;
-        /* persistent grids: the plain form's and the deferred-shadow form's own occupancy
-           (RT_TRIS_WAVES_DEFER), each at most one block per RT_BLOCK queue items */
-        int blocks = 0, blocks_defer = 0, blocks_split = 0;
+        /* persistent grids: the plain form's and the sample-split form's own occupancy, the
+           plain one at most one block per RT_BLOCK queue items */
+        int blocks = 0, blocks_split = 0;
         int r = grid_blocks(c, trav, c->counting, RT_FORM_PLAIN, &blocks);
         if (r != RT_OK) return r;
         blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks, item_blocks));
         if (trav == RT_TRAV_BVH4Q) {
-            r = grid_blocks(c, trav, c->counting, RT_FORM_DEFER, &blocks_defer);
-            if (r != RT_OK) return r;
-            blocks_defer = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks_defer, item_blocks));
             r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
             if (r != RT_OK) return r;
         }
-        /* the spill area is indexed by blockIdx: sized for the larger of the grids any kernel of
-           this render (probe, k_tris in either form, k_defer_shadow) may run with */
+        /* the spill area is indexed by blockIdx: sized for twice the larger grid any kernel of
+           this render may run with (a sample-split render runs two streams side by side, each on
+           its own part of the area) */
         a.spill_cap = spill_cap(c);
         if (a.spill_cap) {
-            /* twice the largest grid: a sample-split render runs two streams side by side, each
-               on its own part of the area */
-            const int rs = ensure_spill(
-                c, (size_t)std::max(blocks, std::max(blocks_defer, blocks_split)) * 2 * RT_BLOCK * a.spill_cap);
+            const int rs = ensure_spill(c, (size_t)std::max(blocks, blocks_split) * 2 * RT_BLOCK * a.spill_cap);
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
@@ -1128,7 +1022,6 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         a.tile_order = nullptr;
         a.pixel_flags = nullptr;
         a.pixel_class = nullptr;
-        a.n_defer = 0;
         const auto h0 = std::chrono::steady_clock::now();
         c->schedule_rebuilt = false;
         if (c->schedule) {
@@ -1137,28 +1030,16 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             a.tile_order = c->d_order;
             a.pixel_flags = a.tile_order ? c->d_flags : nullptr;
             a.pixel_class = a.tile_order ? c->d_class : nullptr;
-            /* only the compressed tree's kernel form records deferred shadow rays */
-            if (a.pixel_class && c->n_defer && trav == RT_TRAV_BVH4Q) {
-                a.n_defer = c->n_defer;
-                a.defer_rec = c->d_defer_rec;
-                a.defer_seg = c->d_defer_seg;
-                a.defer_vis = c->d_defer_vis;
-                a.defer_queue = c->d_defer_queue;
-                a.defer_qcount = c->d_defer_qcount;
-                a.defer_pixel = c->d_defer_pixel;
-                HIPCHK(c, hipMemsetAsync(c->d_defer_qcount, 0, 2 * sizeof(uint32_t), st));
-                blocks = blocks_defer;
-            }
         }
-        /* sample-split tiles: chunks of about spp / 16 samples; the buffers within RT_DEFER_MB */
+        /* sample-split tiles: chunks of about spp / 16 samples; the buffers within RT_SPLIT_MB */
         a.split_chunks = 0;
-        if (a.tile_order && !a.n_defer && trav == RT_TRAV_BVH4Q &&
+        if (a.tile_order && trav == RT_TRAV_BVH4Q &&
             split_wanted(c, (uint64_t)W * hl, (uint64_t)blocks * RT_BLOCK)) {
             const uint32_t spp = c->sample_rate * c->sample_rate;
             const uint32_t csz = (spp + 15u) / 16u, nch = (spp + csz - 1u) / csz;
             const size_t npx_s = (size_t)W * hl;
             const size_t seed_bytes = npx_s * (nch + 1u) * 8u, col_bytes = npx_s * spp * 12u;
-            if (seed_bytes + col_bytes <= (c->defer_mb << 20)) {
+            if (seed_bytes + col_bytes <= (c->split_mb << 20)) {
                 const int rs = ensure_split(c, seed_bytes, col_bytes);
                 if (rs != RT_OK) return rs;
                 a.split_chunks = nch;
@@ -1185,9 +1066,9 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
             fprintf(stderr,
-                    "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p, defer %u, split %u x %u\n",
+                    "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p, split %u x %u, long %u\n",
                     (void *)c, trav, (int)c->counting, blocks, RT_BLOCK, a.spill_cap, (const void *)a.tile_order,
-                    a.n_defer, a.split_chunks, a.split_chunk);
+                    a.split_chunks, a.split_chunk, a.split_n_box);
         /* diagnostics: per-pixel start/finish clocks (+ queries, steps and the wall clocks
            by phase in a counting launch: 8 x u32 per pixel), dumped raw to $RT_PIXEL_STATS */
         const char *stats_path = getenv("RT_PIXEL_STATS");
@@ -1286,8 +1167,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         }
         if (!e && a.split_chunks) e = split_render(c, a, blocks, st);
         else if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
-        if (!e && a.n_defer) e = rt_launch_defer(a, c->counting, blocks, st);
-        c->last_deferred = a.n_defer;
+        c->last_long = a.split_chunks ? a.split_n_box : 0u;
         HIPCHK(c, hipEventRecord(c->ev1, st));
         c->info = rt_render_info{};
         c->info.kernel = RT_KERNEL_TRIS;
@@ -1297,7 +1177,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info.lists_rebuilt = build_lists ? 1u : 0u;
         c->info.list_capacity = lists ? list_cap : 0;
         c->info_list_px = lists ? (size_t)npx : 0u;
-        c->info.pixels_deferred = a.n_defer;
+        c->info.pixels_long = c->last_long;
         c->info.split_chunks = a.split_chunks;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
@@ -1367,7 +1247,7 @@ int rt_synchronize(rt_ctx *c)
     c->last.pixel_clocks_max = h[10];
     c->last.pixel_rays_max = h[11];
     c->last.pixel_steps_max = h[12];
-    c->last.pixels_deferred = c->last_deferred;
+    c->last.pixels_long = c->last_long;
     return RT_OK;
 }
 

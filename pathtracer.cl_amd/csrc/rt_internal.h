@@ -40,12 +40,6 @@
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif
-#ifndef RT_TRIS_WAVES_DEFER
-/* the deferred-shadow form runs tiles, whose time is the serial chains of their box pixels:
-   4 waves per SIMD leave it 120 VGPRs and no spill reloads in the path advance (8-way tiles
-   36.5 -> 33.2 ms; a whole frame, throughput-bound, prefers 5: 129.2 vs 131.3 ms) */
-#define RT_TRIS_WAVES_DEFER 4
-#endif
 #ifndef RT_SHADOW_REDO
 #define RT_SHADOW_REDO 1 /* k_tris: shadow rays answered without traversal are consumed in the same D pass (-3.9 %) */
 #endif
@@ -147,19 +141,8 @@ struct RtTriLaunch {
     uint32_t diag_k;            /* pixels of its 8 x 8 tile are rendered (from it on, in-tile order) */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =
                                    start / finish (s_memrealtime, 100 MHz, low 32 bits), queries, steps */
-    /* Deferred shadow rays of box pixels (DESIGN.md §5 "Deferred shadow rays"): a box pixel's
-       random-number chain depends only on its closest-hit queries, so its shadow rays are
-       recorded (k_tris), traced afterwards in parallel (k_defer_shadow) and its colour is
-       replayed in the reference's operation order (k_defer_finish). */
-    const int32_t *pixel_class; /* per pixel (W x Hl): -1 mesh pixel, -2 box pixel without a slot, >= 0
-                                   box pixel with deferred-shadow slot (NULL: no probe) */
-    float *defer_rec;           /* per slot and (sample, segment, light): (o.xyz, tmax), (d.xyz, cos wi) */
-    uint8_t *defer_seg;         /* per slot and (sample, segment): RT_SEG_* */
-    uint8_t *defer_vis;         /* per record: 1 = unoccluded (k_defer_shadow) */
-    uint32_t *defer_queue;      /* record indices whose shadow ray needs a traversal */
-    uint32_t *defer_qcount;     /* [0] queue length (k_tris), [1] consumer cursor (k_defer_shadow) */
-    const uint32_t *defer_pixel; /* per slot: yl * W + x */
-    uint32_t n_defer;           /* slots in use */
+    const int32_t *pixel_class; /* per pixel (W x Hl): -1 mesh pixel, -2 box pixel, >= 0 a long chain's slot
+                                   in a sample-split render (NULL: no probe) */
     /* Camera-ray candidate lists (k_pixel_lists): per pixel the triangles any of its sample
        rays could accept, RT_LIST_MAX at most, their records copied into the triangle buffer's
        slots [list_base, list_base + list_cap).  Each 8x8 tile's lists are one block (one
@@ -207,8 +190,6 @@ enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
 /* list code = (offset in the tile's block / 8) << RT_LIST_BITS | (count - 1): the offset is below
    64 * RT_LIST_MAX, so a code stays below RT_LIST_EMPTY */
 static_assert(((64u * RT_LIST_MAX / 8u - 1u) << RT_LIST_BITS | (RT_LIST_MAX - 1u)) < 0xfffeu, "list code range");
-/* segment kinds of a deferred pixel's path (trace_path_tri, rtcommon.h:378-468) */
-enum { RT_SEG_BOX = 0, RT_SEG_TRI = 1, RT_SEG_NONE = 2 };
 
 struct RtSphLaunch {
     float *out;
@@ -235,9 +216,6 @@ int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream);
 int rt_launch_trace_rays(const float *nodes, const float *tris, uint32_t n_tris, const rt_ray *rays, uint32_t n,
                          int any_hit, int trav, int32_t *spill, uint32_t spill_cap, int32_t *out_idx, float *out_t,
                          unsigned long long *counters, void *stream); /* counters: NULL, or counting (queries, nodes, tests, leaves) */
-/* Deferred shadow rays: trace the queued records (persistent grid), then replay the deferred
-   pixels' colours and write them (one wave per slot).  Same stream as k_tris, after it. */
-int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *stream);
 /* Camera-ray candidate lists for the launch's pixels (writes a.pixel_lists and the list
    records in the triangle buffer at a.list_base); nodes4 = full-precision 4-wide tree,
    q4 = compressed nodes (their normal boxes; may be NULL). */
@@ -247,7 +225,7 @@ int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint3
    their queries (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
 /* The pixel-queue schedule from the probe, on the device (rt_sched.hip): LPT tile order, box
-   flags and their exclusive scan, pixel classes with deferred-shadow slots. */
+   flags and their exclusive scan, pixel classes with the long chains' slots. */
 struct RtSchedScratch {
     void *tmp = nullptr; /* hipCUB temporary storage */
     size_t tmp_bytes = 0;
@@ -262,14 +240,14 @@ int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_
                    uint32_t max_depth, uint32_t *order, void *stream);
 int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, uint32_t step_max,
                       void *stream);
-int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *defer_pixel,
+int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *slot_pixel,
                       void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed
    buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,
                         uint32_t *buf, bool unpack, void *stream);
 /* Persistent-grid size for the triangle kernel on this device; form: RT_FORM_*. */
-enum { RT_FORM_PLAIN = 0, RT_FORM_DEFER = 1, RT_FORM_SPLIT = 2 };
+enum { RT_FORM_PLAIN = 0, RT_FORM_SPLIT = 1 };
 int rt_tris_grid_blocks(int device, int trav, bool count, int form, int *blocks);
 
 #endif /* RT_INTERNAL_H */

@@ -610,9 +610,8 @@ __device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uin
    query together — at a node each lane tests one child box, at a leaf (or a candidate-list
    block) each lane tests one triangle — so a step's work is a quarter of the per-lane step's
    and a leaf of up to 4 triangles takes one memory round trip instead of one per triangle.  The
-   group's stack lives in LDS (kCoopStack entries per group).  The result is the reference's
+   group's stack lives in LDS (RT_COOP_STACK entries per group).  The result is the reference's
    closest hit (minimum t, ties to the highest original index: an order-free rule). */
-constexpr int kCoopStack = RT_COOP_STACK; /* entries per group: the per-lane LDS stack's words */
 /* quad (4-lane group) exchanges through DPP quad_perm: a VALU modifier, not an LDS round trip
    like ds_bpermute (__shfl), whose latency a lone chain's wave cannot hide */
 template <int CTRL>
@@ -1010,8 +1009,8 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         the iteration (the reference loop, wave-uniform).
    SPLIT: a queue item is one chunk of a pixel's samples, started from the seed the seed pass
    (k_split_seeds) stored for it; each sample's radiance is stored for k_split_finish. */
-template <int TRAV, bool COUNT, bool DEFER, bool SPLIT = false>
-__global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
+template <int TRAV, bool COUNT, bool SPLIT = false>
+__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
     constexpr bool RESUME = TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
@@ -1046,7 +1045,6 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
     float4 *__restrict__ out = reinterpret_cast<float4 *>(a.out);
-    const int lane = (int)(threadIdx.x & 63);
     const uint32_t spp = a.sample_rate * a.sample_rate;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3;
@@ -1075,8 +1073,8 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
     float stmax = 0.0f;
     bool tri_hit = false;
     bool running = false; /* a resumable query is in flight */
-    /* the pixel's class from the probe: -1 mesh pixel, -2 box pixel (long sample chain), >= 0 box
-       pixel whose shadow rays are deferred (its slot in the defer buffers) */
+    /* the pixel's class from the probe: -1 mesh pixel; a box pixel (long sample chain): -2, or
+       its slot >= 0 among the long chains of a sample-split render */
     int pclass = -1;
     bool fin = false;     /* the lane's query completed: ts.best / ts.best_t hold its result */
     TravState ts;
@@ -1128,9 +1126,6 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                         sample_done = true; /* path terminates (rtcommon.h:463-466) */
                     }
                 }
-                if (DEFER && pclass >= 0) /* deferred pixel: the segment's kind, for the colour replay */
-                    a.defer_seg[((size_t)pclass * spp + sample) * (a.max_depth + 1u) + depth] =
-                        (uint8_t)(surface ? (tri_hit ? RT_SEG_TRI : RT_SEG_BOX) : RT_SEG_NONE);
                 if (surface) { /* sample_direct_illumination_tri, rtcommon.h:78-105 */
                     /* the shadow-ray origin (so) becomes the query origin */
                     qo = v3(hp.x + hn.x * RT_SMALL_F, hp.y + hn.y * RT_SMALL_F, hp.z + hn.z * RT_SMALL_F);
@@ -1235,7 +1230,7 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
                 ++sample;
                 mode = M_NEWSAMPLE;
                 if (sample >= spp) { /* raytracer.cl:234-242 */
-                    if (!DEFER || pclass < 0) { /* a deferred pixel's colour is written by k_defer_finish */
+                    {
                         const float n = (float)spp;
                         const float acc_x = ACC_GET(0), acc_y = ACC_GET(1), acc_z = ACC_GET(2);
                         float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
@@ -1282,33 +1277,12 @@ __global__ __launch_bounds__(RT_BLOCK, DEFER ? RT_TRIS_WAVES_DEFER : RT_TRIS_WAV
         const float cw_q = qd.x * hn.x + qd.y * hn.y + qd.z * hn.z;
         const bool issued = mode == M_SHADOW && !fin && !running;
         const bool need_trav = stmax > RT_SMALL_F && cw_q > 0;
-        /* a deferred pixel's shadow ray is recorded (and queued for k_defer_shadow when it
-           needs a traversal) and its path moves on at once: the ray's answer only enters the
-           colour, which k_defer_finish replays; the random-number chain never depends on it */
-        const bool redo = issued && ((DEFER && pclass >= 0) || !need_trav);
+        const bool redo = issued && !need_trav;
         if (!__any(redo)) break;
-        const bool queue = DEFER && redo && pclass >= 0 && need_trav;
-        uint32_t ridx = 0;
-        if (DEFER && redo && pclass >= 0) {
-            ridx = ((((uint32_t)pclass * spp + sample) * (a.max_depth + 1u) + depth) * n_lights + light);
-            float4 *r = reinterpret_cast<float4 *>(a.defer_rec) + 2u * (size_t)ridx;
-            r[0] = make_float4(qo.x, qo.y, qo.z, stmax);
-            r[1] = make_float4(qd.x, qd.y, qd.z, cw_q);
-        }
-        const unsigned long long qb = DEFER ? __ballot(queue) : 0ull;
-        if (DEFER && qb) {
-            const int leader = __ffsll((long long)qb) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.defer_qcount, (uint32_t)__popcll(qb));
-            base = __shfl(base, leader);
-            if (queue)
-                a.defer_queue[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(qb >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)qb, 0u))] = ridx;
-        }
         if (redo) {
             ts.best = -1;
             fin = true;
-            if (!queue) ++cnt[RT_CNT_SKIPPED];
+            ++cnt[RT_CNT_SKIPPED];
         }
         }
 
@@ -1819,158 +1793,6 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
     }
 }
 
-/* Deferred shadow rays, step 2: the queued records' any-hit queries (visibility_test_tri,
-   rtcommon.h:59-68), one lane per query with the per-lane compressed traversal; lanes whose
-   query completed take the next record (one ballot + atomic per wave), so no lane idles
-   until its wave's longest query ends.  Persistent grid (k_tris's: its spill area serves). */
-template <bool COUNT>
-__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_defer_shadow(RtTriLaunch a)
-{
-    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
-    Stack stk;
-    stk.init(s_stack, a.spill, a.spill_cap);
-    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
-    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
-    const float4 *__restrict__ rec = reinterpret_cast<const float4 *>(a.defer_rec);
-    const uint32_t qlen = __builtin_amdgcn_readfirstlane(a.defer_qcount[0]);
-    const int lane = (int)(threadIdx.x & 63);
-    bool running = false, drained = false;
-    uint32_t item = 0;
-    V3 o = v3(0.0f, 0.0f, 0.0f), d = o;
-    TravState ts;
-    unsigned long long n_nodes = 0, n_tests = 0, n_leaves = 0;
-    for (;;) {
-        const unsigned long long idle = __ballot(!running);
-        if (idle && !drained) {
-            const int leader = __ffsll((long long)idle) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.defer_qcount + 1, (uint32_t)__popcll(idle));
-            base = __shfl(base, leader);
-            drained = base + (uint32_t)__popcll(idle) >= qlen;
-            if (!running) {
-                const uint32_t q = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (q < qlen) {
-                    item = a.defer_queue[q];
-                    const float4 r0 = rec[2u * (size_t)item], r1 = rec[2u * (size_t)item + 1u];
-                    o = v3(r0.x, r0.y, r0.z);
-                    d = v3(r1.x, r1.y, r1.z);
-                    trav_begin(ts, stk, o, d, r0.w);
-                    running = true;
-                }
-            }
-        }
-        if (!__any(running)) break;
-#pragma unroll
-        for (int u = 0; u < RT_STEP_UNROLL; ++u) {
-            if (running) {
-                TravCounts tc = {0u, 0u, 0u};
-                if (trav_step_q<COUNT>(nodes, tris, ts, stk, o, d, RT_SMALL_F, true, tc)) {
-                    running = false;
-                    a.defer_vis[item] = ts.best < 0 ? 1 : 0;
-                }
-                if (COUNT) {
-                    n_nodes += tc.nodes;
-                    n_tests += tc.tests;
-                    n_leaves += tc.leaves;
-                }
-            }
-        }
-    }
-    if (COUNT) {
-        const unsigned long long w2 = wave_sum(n_nodes), w3 = wave_sum(n_tests), w4 = wave_sum(n_leaves);
-        if (lane == 0) {
-            atomicAdd(&a.counters[2], w2);
-            atomicAdd(&a.counters[3], w3);
-            atomicAdd(&a.counters[4], w4);
-        }
-    }
-}
-
-/* Deferred shadow rays, step 3: one wave per deferred pixel replays its colour exactly as
-   trace_path_tri accumulates it (rtcommon.h:78-105, :411-461): per sample, per segment,
-   direct += emission * cos(wi) for each unoccluded light in order, then pixelColor +=
-   prop * direct / pi (* 0.7 on the mesh; prop *= 0.7 first on the box); the lanes form the
-   samples' colours, then one lane sums them in sample order (raytracer.cl:228-230) and
-   writes the pixel (:234-242).  Same operations on the same values: the same bits. */
-constexpr uint32_t kDeferMaxSpp = 1024;
-__global__ __launch_bounds__(64) void k_defer_finish(RtTriLaunch a)
-{
-    __shared__ float s_col[kDeferMaxSpp * 3];
-    __shared__ float s_em[kMaxLights * 3];
-    const uint32_t slot = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
-    const uint32_t nl = a.n_lights < (uint32_t)kMaxLights ? a.n_lights : (uint32_t)kMaxLights;
-    if (lane < nl) {
-        s_em[lane * 3 + 0] = a.lights[lane].mat.emission.x;
-        s_em[lane * 3 + 1] = a.lights[lane].mat.emission.y;
-        s_em[lane * 3 + 2] = a.lights[lane].mat.emission.z;
-    }
-    __syncthreads();
-    const uint32_t spp = a.sample_rate * a.sample_rate, nd = a.max_depth + 1u;
-    const float4 *__restrict__ rec = reinterpret_cast<const float4 *>(a.defer_rec);
-    const float scale = 1.0f * RT_M_1_PI_F;
-    for (uint32_t s = lane; s < spp; s += 64u) {
-        float col_x = 0.0f, col_y = 0.0f, col_z = 0.0f;
-        V3 prop = v3(1.0f, 1.0f, 1.0f);
-        const size_t seg0 = ((size_t)slot * spp + s) * nd;
-        for (uint32_t dd = 0; dd < nd; ++dd) {
-            const uint32_t kind = a.defer_seg[seg0 + dd];
-            if (kind == RT_SEG_NONE) break;
-            V3 direct = v3(0.0f, 0.0f, 0.0f);
-            for (uint32_t l = 0; l < nl; ++l) {
-                const size_t idx = (seg0 + dd) * nl + l;
-                const float tmax = rec[2 * idx].w, cw = rec[2 * idx + 1].w;
-                /* queued (and traced) iff tmax > tmin and cos(wi) > 0; otherwise the ray is
-                   unoccluded (tmax <= tmin) or its term is dropped (cos(wi) <= 0) */
-                const bool traced = tmax > RT_SMALL_F && cw > 0;
-                const bool unocc = traced ? a.defer_vis[idx] != 0 : true;
-                if (unocc && cw > 0) {
-                    direct.x += s_em[l * 3 + 0] * cw;
-                    direct.y += s_em[l * 3 + 1] * cw;
-                    direct.z += s_em[l * 3 + 2] * cw;
-                }
-            }
-            if (kind == RT_SEG_TRI) {
-                col_x += prop.x * direct.x * scale * 0.7f;
-                col_y += prop.y * direct.y * scale * 0.7f;
-                col_z += prop.z * direct.z * scale * 0.7f;
-                break;
-            }
-            prop.x *= 0.7f;
-            prop.y *= 0.7f;
-            prop.z *= 0.7f;
-            col_x += prop.x * direct.x * scale;
-            col_y += prop.y * direct.y * scale;
-            col_z += prop.z * direct.z * scale;
-        }
-        s_col[s * 3 + 0] = col_x;
-        s_col[s * 3 + 1] = col_y;
-        s_col[s * 3 + 2] = col_z;
-    }
-    __syncthreads();
-    if (lane == 0) {
-        float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
-        for (uint32_t s = 0; s < spp; ++s) {
-            acc_x += s_col[s * 3 + 0];
-            acc_y += s_col[s * 3 + 1];
-            acc_z += s_col[s * 3 + 2];
-        }
-        const float n = (float)spp;
-        float4 p = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
-        float4 *dst = reinterpret_cast<float4 *>(a.out) + a.defer_pixel[slot];
-        if (a.progressive > 0) {
-            const float4 old = *dst;
-            const float t = 1.0f / (float)a.progressive;
-            p.x = old.x + (p.x - old.x) * t;
-            p.y = old.y + (p.y - old.y) * t;
-            p.z = old.z + (p.z - old.z) * t;
-            p.w = old.w + (p.w - old.w) * t;
-        }
-        *dst = p;
-    }
-}
-
 template <bool COOP>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLaunch a)
 {
@@ -2350,22 +2172,20 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
 {
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)grid_blocks), block(RT_BLOCK);
-#define RT_LAUNCH_TRIS(T, D, S)                                                                                        \
+#define RT_LAUNCH_TRIS(T, S)                                                                                           \
     do {                                                                                                               \
-        if (count) hipLaunchKernelGGL((k_tris<T, true, D, S>), grid, block, 0, st, a);                                 \
-        else hipLaunchKernelGGL((k_tris<T, false, D, S>), grid, block, 0, st, a);                                      \
+        if (count) hipLaunchKernelGGL((k_tris<T, true, S>), grid, block, 0, st, a);                                    \
+        else hipLaunchKernelGGL((k_tris<T, false, S>), grid, block, 0, st, a);                                         \
     } while (0)
-    /* the deferred-shadow and sample-split forms only where they are used (their code costs a
-       full frame 1 %) */
+    /* the sample-split form only where it is used (its code costs a full frame 1 %) */
     if (trav == RT_TRAV_BVH4Q && a.split_chunks) {
         /* the chunk tasks (queue cursor a.work_counter, reset here) */
         const hipError_t e = hipMemsetAsync(a.work_counter, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return (int)e;
-        RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, false, true);
-    } else if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR, false, false);
-    else if (trav == RT_TRAV_BVH4Q && a.n_defer) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, true, false);
-    else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, false, false);
-    else RT_LAUNCH_TRIS(RT_TRAV_BVH4, false, false);
+        RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, true);
+    } else if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR, false);
+    else if (trav == RT_TRAV_BVH4Q) RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, false);
+    else RT_LAUNCH_TRIS(RT_TRAV_BVH4, false);
 #undef RT_LAUNCH_TRIS
     return (int)hipGetLastError();
 }
@@ -2425,23 +2245,14 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int form, int *blocks)
     int per_cu = 0;
     int e;
     if (trav == RT_TRAV_LINEAR)
-        e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true, false>, &per_cu)
-                  : occupancy(k_tris<RT_TRAV_LINEAR, false, false>, &per_cu);
+        e = count ? occupancy(k_tris<RT_TRAV_LINEAR, true>, &per_cu) : occupancy(k_tris<RT_TRAV_LINEAR, false>, &per_cu);
     else if (trav == RT_TRAV_BVH4Q && form == RT_FORM_SPLIT)
-        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true, false, true>, &per_cu)
-                  : occupancy(k_tris<RT_TRAV_BVH4Q, false, false, true>, &per_cu);
-    else if (trav == RT_TRAV_BVH4Q && form == RT_FORM_DEFER)
         e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true, true>, &per_cu)
                   : occupancy(k_tris<RT_TRAV_BVH4Q, false, true>, &per_cu);
     else if (trav == RT_TRAV_BVH4Q)
-        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true, false>, &per_cu)
-                  : occupancy(k_tris<RT_TRAV_BVH4Q, false, false>, &per_cu);
-    else if (form == RT_FORM_DEFER)
-        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true, true>, &per_cu)
-                  : occupancy(k_tris<RT_TRAV_BVH4, false, true>, &per_cu);
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4Q, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4Q, false>, &per_cu);
     else
-        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true, false>, &per_cu)
-                  : occupancy(k_tris<RT_TRAV_BVH4, false, false>, &per_cu);
+        e = count ? occupancy(k_tris<RT_TRAV_BVH4, true>, &per_cu) : occupancy(k_tris<RT_TRAV_BVH4, false>, &per_cu);
     if (e) return e;
     int n_cu = 0;
     const hipError_t he = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device);
@@ -2452,19 +2263,6 @@ int rt_tris_grid_blocks(int device, int trav, bool count, int form, int *blocks)
     if (per_cu < 1) per_cu = 1;
     *blocks = per_cu * n_cu;
     return 0;
-}
-
-int rt_launch_defer(const RtTriLaunch &a, bool count, int grid_blocks, void *stream)
-{
-    hipStream_t st = (hipStream_t)stream;
-    if (a.n_defer == 0) return 0;
-    if (a.sample_rate * a.sample_rate > kDeferMaxSpp) return (int)hipErrorInvalidValue;
-    if (count) hipLaunchKernelGGL(k_defer_shadow<true>, dim3((unsigned)grid_blocks), dim3(RT_BLOCK), 0, st, a);
-    else hipLaunchKernelGGL(k_defer_shadow<false>, dim3((unsigned)grid_blocks), dim3(RT_BLOCK), 0, st, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_defer_finish, dim3(a.n_defer), dim3(64), 0, st, a);
-    return (int)hipGetLastError();
 }
 
 int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint32_t *q4, uint16_t *codes,

@@ -12,9 +12,10 @@
  *      tile's last lane finishes with it — and its mean; a probe ray that misses the mesh
  *      stands for a box path of (1 + lights) x (maxDepth + 1) queries),
  *   3. the LPT order: tiles by cost, most expensive first (hipCUB radix sort, stable),
- *   4. the pixel classes (k_classify): mesh pixel -1; box pixel (some probe ray missed)
- *      with a deferred-shadow slot >= 0 in pixel order up to the slot budget (an exclusive
- *      scan of the box flags), -2 beyond it.
+ *   4. the pixel classes (k_classify): mesh pixel -1; box pixel (some probe ray missed,
+ *      or — for a sample-split render — a mesh pixel whose probe took over 96 steps per ray)
+ *      with a slot >= 0 in pixel order up to the slot budget (an exclusive scan of the box
+ *      flags), -2 beyond it; a sample-split render runs the slotted long chains apart.
  * Scheduling only: no pixel's result depends on when or where it is rendered.  This
  * replaced an 8 MB device-to-host copy, a host loop and a host sort per camera change
  * (every arrow key or drag of GlutCLWindow.cpp:229-279 restarts the refinement).
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void k_box_flags(const uint32_t *__restrict__ 
 
 __global__ __launch_bounds__(256) void k_classify(const uint32_t *__restrict__ box, const uint32_t *__restrict__ scan,
                                                   uint32_t npx, uint32_t slots, int32_t *__restrict__ cls,
-                                                  uint32_t *__restrict__ defer_pixel)
+                                                  uint32_t *__restrict__ slot_pixel)
 {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= npx) return;
@@ -114,7 +115,7 @@ __global__ __launch_bounds__(256) void k_classify(const uint32_t *__restrict__ b
         const uint32_t s = scan[p];
         if (s < slots) {
             c = (int32_t)s;
-            defer_pixel[s] = p;
+            slot_pixel[s] = p;
         } else {
             c = -2;
         }
@@ -207,10 +208,10 @@ int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, ui
     return (int)e;
 }
 
-int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *defer_pixel,
+int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *slot_pixel,
                       void *stream)
 {
     hipLaunchKernelGGL(k_classify, dim3((npx + 255u) / 256u), dim3(256), 0, (hipStream_t)stream, s.box, s.scan, npx,
-                       slots, cls, defer_pixel);
+                       slots, cls, slot_pixel);
     return (int)hipGetLastError();
 }

@@ -256,7 +256,7 @@ class RayTracer:
         return pre.value, main.value
 
     def renderInfo(self) -> dict:
-        """rt_last_render_info: the last render's lists, deferral and schedule (no result depends
+        """rt_last_render_info: the last render's lists, sample split and schedule (no result depends
         on any of it)."""
         fn = getattr(self._lib, "rt_last_render_info", None)
         if fn is None:  # an older library loaded for an A/B run

@@ -3,8 +3,9 @@
 With librtmi built -DRT_DIAG_ONE_PIXEL=1 (profiles/build_variant.sh), k_tris renders only the
 pixel RT_DIAG_PIXEL=x,y names: its lane is the only live lane of its wave and of the chip, so
 the main kernel's time is that pixel's chain at the megakernel's best (no other lane holds a
-stepping round open, no other wave competes).  Printed per pixel, inline and with its shadow
-rays deferred (RT_DEFER=1): main-kernel ms, queries, traversal steps, us per query and step.
+stepping round open, no other wave competes).  Printed per pixel: main-kernel ms, queries,
+traversal steps, us per query and step.  (Until r03 the chains were also timed with their
+shadow rays deferred — profiles/r03c; deferral was replaced by sample-split tiles.)
 
     RTMI_LIB=build_ab/diag1.so python profiles/chain_alone.py [--pixels 1844,198 1807,633]
 """
@@ -36,8 +37,7 @@ def main():
     verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
     seeds = sc.default_seeds(Wp, Hp)
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
-    for defer in ("0", "1"):
-        os.environ["RT_DEFER"] = defer
+    for defer in ("0",):
         rt = pt.RayTracer(0)
         rt.setSpheres(sc.ply_scene())
         c = sc.PLY_CAMERA

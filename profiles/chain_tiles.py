@@ -20,6 +20,7 @@ def main():
 
     dump = "/tmp/rt_pixel_stats_tiles.bin"
     os.environ["RT_PIXEL_STATS"] = dump
+    os.environ["RT_SPLIT"] = "0"  # whole-pixel tasks: the per-pixel chains these clocks describe
     pt = ptload.load()
     sc = pt.scenes
     W, H, sr = 1920, 1080, 16
@@ -49,7 +50,7 @@ def main():
         start = ((s[:, 0] - t0) & 0xFFFFFFFF) / 1e5
         timeline = {f"end_p{q}": round(float(np.percentile(end, q)), 2) for q in (50, 90, 99, 99.9, 100)}
         timeline["costliest_start_ms"] = [round(float(start[i]), 2) for i in top]
-        print(json.dumps({name: {"kernel_ms": round(ms, 2), "pixels_deferred": cn["pixels_deferred"],
+        print(json.dumps({name: {"kernel_ms": round(ms, 2), "pixels_long": cn["pixels_long"],
                                  "steps_per_query": round((cn["nodes_visited"] + cn["leaves_visited"]) /
                                                           max(cn["rays_closest"] + cn["rays_shadow"], 1), 2),
                                  "timeline": timeline,

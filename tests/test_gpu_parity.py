@@ -978,10 +978,11 @@ def test_candidate_lists_reused_across_frames(pt, oracle, monkeypatch):
 
 
 def test_traversal_switch_on_a_context_keeps_results(pt, oracle):
-    """the cached schedule (LPT order, pixel classes, deferred-shadow slots)
-    belongs to one traversal.  One context renders the same tile at sampleRate 4 (deferral on:
-    few pixels per lane) with the compressed tree, then the full-precision tree, then the linear
-    loop, then the compressed tree again; every render equals the oracle on the tile's rows."""
+    """the cached schedule (LPT order, pixel classes, the long chains' slots)
+    belongs to one traversal.  One context renders the same tile at sampleRate 4 (a
+    sample-split render: few pixels per lane) with the compressed tree, then the full-precision
+    tree, then the linear loop, then the compressed tree again; every render equals the oracle
+    on the tile's rows."""
     sc = pt.scenes
     W, H, sr, tile = 96, 64, 4, (8, 4, 1)
     Wp, Hp = sc.padded_dims(W, H)
@@ -1000,19 +1001,19 @@ def test_traversal_switch_on_a_context_keeps_results(pt, oracle):
     rt.setSampleRate(sr)
     rt.setMaxPathDepth(6)
     rt.setMesh(verts, idx)
-    deferred = []
+    split = []
     for trav in ("bvh", "bvh4f", "linear", "bvh"):
         rt.setTraversal(trav)
         rt.setSeeds(Wp, Hp, seeds)
         got = np.zeros(len(rows) * W * 4, np.float32)
         rt.rayTrace(got, W, H, 0, kernel=2, tile=tile)
-        deferred.append(rt.counters()["pixels_deferred"])
+        split.append(rt.renderInfo()["split_chunks"])
         np.testing.assert_array_equal(bits(got), bits(exp_tile), err_msg=trav)
         s_got = rt.getSeeds()
         sl = pix.astype(np.int64) // W * Wp + pix % W
         np.testing.assert_array_equal(s_got[sl], sd[sl], err_msg=trav)
     rt.close()
-    assert deferred[0] > 0 and deferred[1] == 0 and deferred[2] == 0 and deferred[3] > 0, deferred
+    assert split[0] > 0 and split[1] == 0 and split[2] == 0 and split[3] > 0, split
 
 
 @pytest.mark.parametrize("sr", [2, 3, 5])
@@ -1287,19 +1288,20 @@ def test_huge_coordinates_fall_back_to_full_precision_nodes(tracer, pt):
 def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     """The pixel queue's order (step-counting probe, LPT key) and the box-wave priority are
     scheduling only: a frame with box and mesh pixels, 16 spp, renders to the same bits and
-    seeds with the queue row-major (RT_SCHEDULE=0), with the default schedule, with the box
-    pixels' shadow rays traced inline (RT_DEFER=0) or deferred for only the few box pixels 1 MB
-    of slots holds, with camera rays traversing the tree instead of their candidate lists
-    (RT_PIXEL_LISTS=0), and with a list area too small for every pixel (RT_LIST_MB=2)."""
+    seeds with the queue row-major (RT_SCHEDULE=0), with the default schedule (a sample-split
+    render: few pixels per lane), with whole-pixel tasks (RT_SPLIT=0), with the split forced
+    on, with split buffers too small for the frame (RT_SPLIT_MB=1: whole pixels again), with
+    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0), and
+    with a list area too small for every pixel (RT_LIST_MB=2)."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
     verts, idx = sc.make_mesh(20_000)
     seeds = sc.default_seeds(Wp, Hp, skip=7)
     frames = []
-    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_DEFER": "0"}, {"RT_DEFER": "1", "RT_DEFER_MB": "1"},
+    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_SPLIT": "0"}, {"RT_SPLIT": "1"}, {"RT_SPLIT": "1", "RT_SPLIT_MB": "1"},
                 {"RT_PIXEL_LISTS": "0"}, {"RT_LIST_MB": "2"}):
-        for k in ("RT_SCHEDULE", "RT_DEFER", "RT_DEFER_MB", "RT_PIXEL_LISTS", "RT_LIST_MB"):
+        for k in ("RT_SCHEDULE", "RT_SPLIT", "RT_SPLIT_MB", "RT_PIXEL_LISTS", "RT_LIST_MB"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -1318,39 +1320,6 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     for f, s in frames[1:]:
         np.testing.assert_array_equal(f, frames[0][0])
         np.testing.assert_array_equal(s, frames[0][1])
-
-
-def test_deferred_shadow_rays_at_full_size(tracer, pt, monkeypatch):
-    """Deferred shadow rays (k_tris records, k_defer_shadow traces, k_defer_finish replays the
-    colour) on the dragon-class frame at full size, sampleRate 4, forced on (RT_DEFER=1: the
-    automatic policy defers only on tiles), as a whole frame and as a row-stripe tile of 8:
-    the same bits and seeds as inline shadow rays (RT_DEFER=0), which the oracle pins."""
-    sc = pt.scenes
-    W, H, sr = 1920, 1080, 4
-    Wp, Hp = sc.padded_dims(W, H)
-    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
-    seeds = sc.default_seeds(Wp, Hp, skip=2)
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("RT_DEFER", mode)
-        rt = pt.RayTracer(0)
-        rt.setSpheres(sc.ply_scene())
-        rt.setCamera(sc.camera_spherical(W, **sc.PLY_CAMERA))
-        rt.setSampleRate(sr)
-        rt.setMaxPathDepth(6)
-        rt.setMesh(verts, idx)
-        for tile in (None, (8, 8, 3)):
-            rows = H if tile is None else len(np.arange(H)[(np.arange(H) // 8) % 8 == 3])
-            rt.setSeeds(Wp, Hp, seeds)
-            out = np.zeros(W * rows * 4, np.float32)
-            rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
-            res[(mode, tile)] = (bits(out).copy(), rt.getSeeds().copy())
-            n_def = rt.counters()["pixels_deferred"]
-            assert (n_def > 1000) if mode == "1" else (n_def == 0)
-        rt.close()
-    for tile in (None, (8, 8, 3)):
-        np.testing.assert_array_equal(res[("1", tile)][0], res[("0", tile)][0])
-        np.testing.assert_array_equal(res[("1", tile)][1], res[("0", tile)][1])
 
 
 def test_sample_split_at_full_size(tracer, pt, monkeypatch):

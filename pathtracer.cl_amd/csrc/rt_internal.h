@@ -161,9 +161,11 @@ struct RtTriLaunch {
        queries alone and stores the seed at the first sample of each chunk; k_tris then renders
        the chunks as independent tasks, each sample's radiance stored, and k_split_finish sums
        them in sample order and writes the pixel and its final seed. */
-    uint32_t split_chunks;    /* chunks per pixel (0: pixels are whole tasks) */
-    uint32_t split_chunk;     /* samples per chunk */
-    uint32_t *split_seed;     /* per pixel (yl * W + x) and chunk 0..split_chunks: 2 words; the last = the final seed */
+    uint32_t split_chunks;    /* chunks per pixel of this launch (0: pixels are whole tasks) */
+    uint32_t split_chunk;     /* samples per chunk of this launch (a multiple of split_fine) */
+    uint32_t split_fine;      /* samples between the stored seeds */
+    uint32_t split_nseed;     /* stored seeds per pixel: one per split_fine samples, then the final seed */
+    uint32_t *split_seed;     /* per pixel (yl * W + x): split_nseed seeds of 2 words */
     float *split_col;         /* per sample s and pixel p: radiance at ((s * W * Hl) + p) * 3 */
     uint32_t *split_counter;  /* the seed pass's queue cursor */
     uint32_t split_seed_blocks; /* grid of the seed pass */

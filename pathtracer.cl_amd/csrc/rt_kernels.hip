@@ -603,7 +603,7 @@ __device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uin
 }
 
 #ifndef RT_SEED_UNROLL
-#define RT_SEED_UNROLL 2 /* seed-pass traversal steps per loop iteration */
+#define RT_SEED_UNROLL 4 /* seed-pass traversal steps per loop iteration */
 #endif
 
 /* Cooperative closest-hit query: the 4 lanes of a group (lanes 4g..4g+3 of a wave) advance ONE
@@ -799,7 +799,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     gst.base = (lds_int *)(s_stack + (threadIdx.x & ~63u) + (uint32_t)gbase);
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
-    const uint32_t spp = a.sample_rate * a.sample_rate, nch = a.split_chunks, csz = a.split_chunk;
+    const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
     const uint32_t n_items = a.split_which == RT_SPLIT_BOX ? a.split_n_box : tiles_x * tiles_y * 64u;
@@ -871,10 +871,9 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
         /* a new sample: the chunk's first seed, then the camera ray and its query */
         if (next) {
             next = false;
-            if ((sample == spp || sample % csz == 0u) && lane == gbase) {
-                const uint32_t c = sample == spp ? nch : sample / csz;
-                reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * (nch + 1u) + c] =
-                    make_uint2(seed.x, seed.y);
+            if ((sample == spp || sample % fine == 0u) && lane == gbase) {
+                const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
+                reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
             }
             if (sample == spp) {
                 have = false;
@@ -1336,7 +1335,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                     if (SPLIT && take) { /* the chunk's first seed, from the seed pass */
                         const uint2 sd = reinterpret_cast<const uint2 *>(
-                            a.split_seed)[(size_t)(yl * a.W + x) * (a.split_chunks + 1u) + chunk];
+                            a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + chunk * a.split_chunk / a.split_fine];
                         seed.x = sd.x;
                         seed.y = sd.y;
                         sample = chunk * a.split_chunk;
@@ -1808,7 +1807,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_split_finish(RtTriLaunch a)
     const uint32_t npx = a.W * a.Hl;
     const uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x;
     if (p >= npx) return;
-    const uint32_t spp = a.sample_rate * a.sample_rate, nch = a.split_chunks;
+    const uint32_t spp = a.sample_rate * a.sample_rate;
     float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
     for (uint32_t s = 0; s < spp; ++s) {
         const float *c = a.split_col + ((size_t)s * npx + p) * 3u;
@@ -1830,7 +1829,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_split_finish(RtTriLaunch a)
     *dst = px;
     const uint32_t x = p % a.W, yl = p / a.W;
     const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
-    const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * (nch + 1u) + nch];
+    const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * a.split_nseed + a.split_nseed - 1u];
     a.seeds[slot] = sd.x;
     a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
 }

@@ -26,6 +26,9 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def pt():
+    # torch's HIP runtime first: a process whose first HIP call came from librtmi (the system
+    # ROCm) sees no device through torch afterwards, whichever GPU test happens to run first
+    gpu_available()
     lib = ROOT / "pathtracer.cl_amd" / "librtmi.so"
     if not lib.exists():
         subprocess.run(["make", "-s", "-C", str(ROOT / "pathtracer.cl_amd" / "csrc")], check=True)

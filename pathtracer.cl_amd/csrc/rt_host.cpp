@@ -121,7 +121,7 @@ struct rt_ctx {
     int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (split_wanted) */
     /* the long chains' seed pass with 4 lanes per query (one lane per query: 8-way tile 24 -> 19 ms
        for the chains); 4 x 4 probe rays per pixel to find them */
-    bool seed_coop = true;
+    uint32_t seed_width = 4; /* lanes per seed-pass query of the long chains (1 or 4) */
     uint32_t split_probe = 4;
     uint32_t split_gpw = 0; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
@@ -427,12 +427,11 @@ int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
     return RT_OK;
 }
 
-/* The box pixels' seed-pass grid: one chain per lane (COOP: per 4-lane group; RT_SPLIT_GPW per
-   wave), at most a quarter of the full grid (further chains queue behind the first); full_grid
-   0: unbounded. */
-int split_box_blocks(const rt_ctx *c, bool coop, int full_grid)
+/* The long chains' seed-pass grid: one chain per group of `width` lanes, at most a quarter of
+   the full grid (further chains queue behind the first); full_grid 0: unbounded. */
+int split_box_blocks(const rt_ctx *c, uint32_t width, int full_grid)
 {
-    const uint32_t per_wave = c->split_gpw ? c->split_gpw : (coop ? 16u : 64u);
+    const uint32_t per_wave = c->split_gpw ? c->split_gpw : 64u / std::max(1u, width);
     int n = (int)((c->n_split_box + per_wave * 4u - 1u) / (per_wave * 4u));
     if (full_grid > 0) n = std::min(n, std::max(1, full_grid / 4));
     return n;
@@ -1058,12 +1057,15 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 a.split_which = c->n_split_box ? RT_SPLIT_MESH : RT_SPLIT_ALL;
                 a.split_box = c->d_split_box;
                 a.split_n_box = c->n_split_box;
+                a.n_nodes4 = c->bvh.n_nodes4;
                 /* 4 lanes per seed-pass query where the tree's worst stack (plus a candidate
                    list's blocks) fits a group's LDS stack */
-                a.split_coop = c->seed_coop && c->bvh.stack4 + 4 <= RT_COOP_STACK ? 1u : 0u;
+                /* 4 lanes per long-chain query where the group's LDS stack holds the tree's worst
+                   depth-first stack (+ a candidate list's blocks), else one */
+                a.split_coop = c->seed_width >= 4 && c->bvh.stack4 + 4 <= RT_COOP_STACK ? 4u : 0u;
                 /* the box pixels' seed pass (one lane per pixel) keeps its blocks resident beside
                    the mesh pixels' kernels, whose grids leave room for it */
-                const int box_blocks = c->n_split_box ? split_box_blocks(c, a.split_coop != 0, blocks) : 0;
+                const int box_blocks = c->n_split_box ? split_box_blocks(c, std::max(1u, a.split_coop), blocks) : 0;
                 c->split_box_grid = box_blocks;
                 a.split_seed_blocks = (uint32_t)std::max(1, blocks - box_blocks);
                 blocks = std::max(1, std::min((int)std::min<uint64_t>((uint64_t)blocks_split, item_blocks * nch),
@@ -1173,7 +1175,10 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                     (unsigned long long)b[3], (unsigned long long)b[4], (unsigned long long)b[5],
                     (unsigned long long)b[6], nl ? (double)sum / (double)nl : 0.0);
         }
-        if (!e && a.split_chunks) e = split_render(c, a, blocks, st);
+        if (!e && a.split_chunks) {
+            a.n_recs = (uint32_t)std::min<size_t>(c->tris_cap, 0xffffffffu); /* the list area included */
+            e = split_render(c, a, blocks, st);
+        }
         else if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
         c->last_long = a.split_chunks ? a.split_n_box : 0u;
         HIPCHK(c, hipEventRecord(c->ev1, st));

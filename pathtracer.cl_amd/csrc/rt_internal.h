@@ -172,7 +172,9 @@ struct RtTriLaunch {
     uint32_t split_which;     /* RT_SPLIT_ALL, or the mesh pixels / the box pixels of a two-stream split */
     const uint32_t *split_box; /* RT_SPLIT_BOX: the box pixels (yl * W + x), split_n_box of them */
     uint32_t split_n_box;
-    uint32_t split_coop;      /* seed pass: 4 lanes per query (the tree's stack fits the group's LDS stack) */
+    uint32_t split_coop;      /* seed pass: lanes per long-chain query, 4 (0: one) */
+    uint32_t n_nodes4, n_recs; /* compressed nodes and triangle records (mesh + lists): the cooperative
+                                  seed pass checks every index against them */
     uint32_t split_gpw;       /* seed pass: queries (chains) per wave, 0 = all lanes / groups */
 };
 enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };

@@ -637,10 +637,17 @@ __device__ __forceinline__ int quad_bcast(int v, int k)
 /* The 4-lane group's stack in the block's LDS stack area, inside the words its wave's lanes own
    in the per-lane layout ([depth][lane], RT_BLOCK words per depth): entry e of group g of wave w
    is word RT_BLOCK * (e / 4) + 64 w + 4 g + e % 4 (2-way bank conflicts between the groups). */
-struct CoopStack {
-    lds_int *base; /* word 64 w + 4 g */
-    __device__ __forceinline__ lds_int &operator[](int e) const { return base[RT_BLOCK * (e >> 2) + (e & 3)]; }
+template <int G>
+struct CoopStackG {
+    static constexpr int kCap = RT_STACK_DEPTH * G; /* entries: the group's words of its wave's columns */
+    lds_int *base; /* word 64 w + G g */
+    __device__ __forceinline__ lds_int &operator[](int e) const
+    {
+        e = e < 0 ? 0 : e >= kCap ? kCap - 1 : e; /* never outside the group's words */
+        return base[RT_BLOCK * (e / G) + (e % G)];
+    }
 };
+typedef CoopStackG<4> CoopStack;
 
 struct CoopQuery {
     int node, best, best_orig, sp;
@@ -661,13 +668,16 @@ __device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
 
 /* one step; true when the query is complete */
 __device__ __forceinline__ bool coop_step(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
-                                          CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin)
+                                          CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
+                                          uint32_t n_nodes, uint32_t n_recs)
 {
     const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
     const int node = q.node;
     const bool leaf = node < 0;
     const uint32_t enc = (uint32_t)(~node);
     const uint32_t first = enc >> 3, cnt = (enc & 7u) + 1u;
+    /* every record index is checked (a defect ends the query instead of reading outside the tree) */
+    if (leaf ? first + cnt > n_recs : (uint32_t)node >= n_nodes) return true;
     const bool tri_ok = leaf && (uint32_t)sub < cnt;
     const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (first + (tri_ok ? (uint32_t)sub : 0u))
                             : reinterpret_cast<const uint4 *>(nodes) + 4 * node;
@@ -789,14 +799,17 @@ __device__ __forceinline__ bool coop_step(const float4 *__restrict__ nodes, cons
    sample of every chunk and after the last one.  The queries are resumable: the wave steps
    every running query and a lane whose query completed advances at once, so no chain waits for
    its neighbours'. */
-template <bool COOP>
+template <int G> /* lanes per query: 1 (trav_step_q) or 4 (coop_step) */
 __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
 {
+    constexpr bool COOP = G > 1;
     Stack stk;
     stk.init(s_stack, a.spill, a.spill_cap);
-    const int lane = (int)(threadIdx.x & 63), gbase = COOP ? (lane & ~3) : lane;
+    const int lane = (int)(threadIdx.x & 63), gbase = lane & ~(G - 1);
     CoopStack gst;
     gst.base = (lds_int *)(s_stack + (threadIdx.x & ~63u) + (uint32_t)gbase);
+    if (COOP) /* the wave's stack words start as the root: an entry read before it is written is a node */
+        for (int k = 0; k < RT_STACK_DEPTH; ++k) s_stack[k * RT_BLOCK + threadIdx.x] = 0;
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
     const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
@@ -822,11 +835,12 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     CoopQuery cq;
     coop_begin(cq, qo, qd, kInf);
     uint32_t st_steps = 0, st_box = 0, st_t0 = 0; /* diagnostics (RT_PIXEL_STATS): per pixel */
+    uint32_t q_steps = 0;                          /* rounds of the current query */
     for (;;) {
         /* lanes (COOP: groups) without a pixel take the next ones of the queue */
         /* takers: the first split_gpw lanes (COOP: 4-lane groups) of the wave */
-        const uint32_t gpw = a.split_gpw ? a.split_gpw : (COOP ? 16u : 64u);
-        const unsigned long long idle = __ballot(!have && lane == gbase && (uint32_t)(COOP ? lane >> 2 : lane) < gpw);
+        const uint32_t gpw = a.split_gpw ? a.split_gpw : 64u / G;
+        const unsigned long long idle = __ballot(!have && lane == gbase && (uint32_t)(lane / G) < gpw);
         if (idle && !drained) {
             /* a batch per wave of as many items as it has takers */
             uint32_t item = batch_take(a.split_counter, idle, bnext, bend, gpw);
@@ -895,6 +909,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 depth = 0;
                 if (COOP) coop_begin(cq, qo, qd, kInf);
                 else trav_begin(ts, stk, qo, qd, kInf);
+                q_steps = 0;
                 running = true;
                 if (a.list_code) { /* the pixel's candidate list, as k_tris takes it */
                     const uint32_t code = a.list_code[yl * a.W + x];
@@ -930,14 +945,17 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
         for (int u = 0; u < RT_SEED_UNROLL; ++u) {
             if (running) {
                 ++st_steps;
+                ++q_steps;
                 bool done;
-                if (COOP) {
-                    done = coop_step(nodes, tris, cq, gst, qo, qd, RT_SMALL_F);
+                if constexpr (G == 4) {
+                    done = coop_step(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
                     done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
                 }
-                if (done) {
+                /* a query never takes 2^14 rounds (a ray meets far fewer nodes than that):
+                   a bound every wave reaches, whatever a defect would do to a stack */
+                if (done || q_steps > (1u << 14)) {
                     running = false;
                     fin = true;
                 }
@@ -976,6 +994,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         sample_done = false;
                         if (COOP) coop_begin(cq, qo, qd, kInf);
                         else trav_begin(ts, stk, qo, qd, kInf);
+                        q_steps = 0;
                         running = true;
                     }
                 }
@@ -1792,11 +1811,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
     }
 }
 
-template <bool COOP>
+template <int G>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLaunch a)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
-    seed_pass<COOP>(a, s_stack);
+    seed_pass<G>(a, s_stack);
 }
 
 /* Sample-split tiles, step 3: per pixel, the samples' radiance summed in sample order
@@ -2194,8 +2213,8 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
     hipStream_t st = (hipStream_t)stream;
     const hipError_t e = hipMemsetAsync(a.split_counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
-    if (a.split_coop) hipLaunchKernelGGL(k_split_seeds<true>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
-    else hipLaunchKernelGGL(k_split_seeds<false>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
+    if (a.split_coop) hipLaunchKernelGGL(k_split_seeds<4>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
+    else hipLaunchKernelGGL(k_split_seeds<1>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
     return (int)hipGetLastError();
 }
 

@@ -1058,11 +1058,12 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 a.split_box = c->d_split_box;
                 a.split_n_box = c->n_split_box;
                 a.n_nodes4 = c->bvh.n_nodes4;
-                /* 4 lanes per seed-pass query where the tree's worst stack (plus a candidate
-                   list's blocks) fits a group's LDS stack */
                 /* 4 lanes per long-chain query where the group's LDS stack holds the tree's worst
                    depth-first stack (+ a candidate list's blocks), else one */
                 a.split_coop = c->seed_width >= 4 && c->bvh.stack4 + 4 <= RT_COOP_STACK ? 4u : 0u;
+                /* a round of 4 nodes adds at most 12 entries and a one-item depth-first walk at
+                   most the tree's worst stack: rounds take 4 items up to this depth (coop_round) */
+                a.coop_multi_sp = std::max(0, (int)RT_COOP_STACK - 12 - (int)c->bvh.stack4);
                 /* the box pixels' seed pass (one lane per pixel) keeps its blocks resident beside
                    the mesh pixels' kernels, whose grids leave room for it */
                 const int box_blocks = c->n_split_box ? split_box_blocks(c, std::max(1u, a.split_coop), blocks) : 0;

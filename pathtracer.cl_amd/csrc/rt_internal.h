@@ -176,6 +176,8 @@ struct RtTriLaunch {
     uint32_t n_nodes4, n_recs; /* compressed nodes and triangle records (mesh + lists): the cooperative
                                   seed pass checks every index against them */
     uint32_t split_gpw;       /* seed pass: queries (chains) per wave, 0 = all lanes / groups */
+    int32_t coop_multi_sp;    /* cooperative seed pass: rounds take 4 stack items while the group's stack holds
+                                 at most this many entries, else one (coop_round) */
 };
 enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
 #define RT_COOP_STACK (RT_STACK_DEPTH * 4) /* LDS stack entries of a 4-lane query group (k_split_seeds) */

@@ -217,17 +217,106 @@ __device__ __forceinline__ float half_of(uint32_t w, int hi)
     return (float)__builtin_bit_cast(_Float16, b);
 }
 
+/* The 4 child boxes of a compressed node (rt_quant.h; the record as its four dwordx4 words)
+   against the ray: c[] the children by their sort key t[] ascending (misses last, kInf); returns
+   how many were hit (0 also when the determinant cull skips the subtree).  Culling only. */
+__device__ __forceinline__ int node_children(uint4 q0, uint4 q1, uint4 q2, uint4 q3, V3 inv, V3 oi, V3 d,
+                                         float best_t, bool any_hit, bool longest, float (&t)[4], int (&c)[4])
+{
+    const float tmin_c = -1e-3f;
+    const float tmax_c = t_slack(best_t);
+    const uint32_t w = q0.w;
+    constexpr int kExpBias = RT_QEXP_MIN + 24; /* scales carry the 2^24 of the f16-subnormal planes */
+    const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + kExpBias);
+    const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + kExpBias);
+    const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + kExpBias);
+    const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
+    const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
+    const float bzo = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
+    const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+    const uint32_t nxw = px ? q1.x : q1.y, fxw = px ? q1.y : q1.x;
+    const uint32_t nyw = py ? q1.z : q1.w, fyw = py ? q1.w : q1.z;
+    const uint32_t nzw = pz ? q2.x : q2.y, fzw = pz ? q2.y : q2.x;
+    int nhit = 0;
+    /* Plane bytes as f16 subnormals: v_perm_b32 spreads two bytes of a plane word into
+       the low bytes of two 16-bit halves (0x00bb = b * 2^-24 as f16, exact), and
+       v_fma_mix_f32 converts a half and does the FMA in one instruction, with the
+       2^24 folded into the scale's exponent: (b * 2^-24) * (s * 2^24) + base is exactly
+       fma(b, s, base) — the same bits as a byte convert + FMA, in 3/4 of the VALU. */
+    const float sx24 = sx, sy24 = sy, sz24 = sz;
+    const uint32_t nx01 = __builtin_amdgcn_perm(0u, nxw, 0x0c010c00u), nx23 = __builtin_amdgcn_perm(0u, nxw, 0x0c030c02u);
+    const uint32_t ny01 = __builtin_amdgcn_perm(0u, nyw, 0x0c010c00u), ny23 = __builtin_amdgcn_perm(0u, nyw, 0x0c030c02u);
+    const uint32_t nz01 = __builtin_amdgcn_perm(0u, nzw, 0x0c010c00u), nz23 = __builtin_amdgcn_perm(0u, nzw, 0x0c030c02u);
+    const uint32_t fx01 = __builtin_amdgcn_perm(0u, fxw, 0x0c010c00u), fx23 = __builtin_amdgcn_perm(0u, fxw, 0x0c030c02u);
+    const uint32_t fy01 = __builtin_amdgcn_perm(0u, fyw, 0x0c010c00u), fy23 = __builtin_amdgcn_perm(0u, fyw, 0x0c030c02u);
+    const uint32_t fz01 = __builtin_amdgcn_perm(0u, fzw, 0x0c010c00u), fz23 = __builtin_amdgcn_perm(0u, fzw, 0x0c030c02u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float tn = __builtin_fmaxf(
+            __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nx01 : nx23, i & 1), sx24, bx),
+                            __builtin_fmaf(half_of(i < 2 ? ny01 : ny23, i & 1), sy24, by)),
+            __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nz01 : nz23, i & 1), sz24, bzo), tmin_c));
+        const float tf = __builtin_fminf(
+            __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fx01 : fx23, i & 1), sx24, bx),
+                            __builtin_fmaf(half_of(i < 2 ? fy01 : fy23, i & 1), sy24, by)),
+            __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fz01 : fz23, i & 1), sz24, bzo), tmax_c));
+        const bool h = tn <= tf; /* an unused slot's inverted box never passes */
+        c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
+        /* Any hit (the answer is order-free): children whose box holds the ray origin (the
+           surface a shadow ray leaves, whose own triangles it cannot hit) are visited
+           last, and a ray leaving the mesh (`longest`) takes the others by the length of
+           its box segment, longest first — measured on the CPU model to find an occluder
+           in the fewest steps; rays from the box walls keep nearest first. */
+        const float key = longest ? tn - tf : tn;
+        t[i] = h ? (any_hit && tn <= 0.0f ? key + 1e4f : key) : kInf;
+        nhit += h ? 1 : 0;
+    }
+    /* Determinant cull (rt_quant.h): the node's normal box bounds d . N = det over its
+       subtree; below 1e-4 (with the float error bound) no triangle can be accepted, so
+       the subtree is skipped.  Culling only: the same results, fewer steps. */
+    {
+        /* v_perm_b32 picks, per axis, the hi byte (d >= 0) or the lo byte into `nb` (the box
+           corner maximising d . N) and the other into `fb`; v_cvt_f32_ubyteN converts in
+           place; the +128 byte bias folds into one per-ray term */
+        const uint32_t nlo = q2.z, nhi = q2.w;
+        const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
+        const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
+        const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
+        const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
+        const float bias = 128.0f * (d.x + d.y + d.z);
+        const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
+                                         __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu),
+                                                        __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
+        const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
+                                         __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu),
+                                                        __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
+        const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
+        /* bias rounding: |fl(128 sum d) - 128 sum d| <= 3u * 128 |d|_1, inside the margin */
+        const float bound = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
+        if (bound < 1e-4f) nhit = 0;
+    }
+    if (nhit > 0) {
+        cas(t[0], c[0], t[1], c[1]);
+        cas(t[2], c[2], t[3], c[3]);
+        cas(t[0], c[0], t[2], c[2]);
+        cas(t[1], c[1], t[3], c[3]);
+        cas(t[1], c[1], t[2], c[2]);
+    }
+    return nhit;
+}
+
 /* One step of the compressed 4-wide traversal (rt_quant.h).  Every lane fetches
    exactly one 64-B record per step — a node, or ONE triangle of its current leaf —
    with the same three dwordx4 loads, so a wave-step costs one memory round trip
    whatever mix of node and leaf lanes it holds (a leaf of k triangles takes k
-   steps; the leaf cursor is the leaf code itself: first slot and remaining count). */
-template <bool COUNT>
+   steps; the leaf cursor is the leaf code itself: first slot and remaining count).
+   PAIR (the seed pass's one-lane queries, which are mostly short candidate lists): a leaf lane
+   with two or more triangles left fetches and tests two records in the step. */
+template <bool COUNT, bool PAIR = false>
 __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                             TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
                                             TravCounts &cnt, bool longest = false)
 {
-    const float tmin_c = -1e-3f;
     const V3 inv = s.inv, oi = s.oi;
     const int node = s.node;
     const bool leaf = node < 0;
@@ -243,13 +332,21 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     /* the child links (d[12..15]) only for node lanes: the load runs under their exec mask,
        so leaf lanes add no addresses to it (-1 %) */
     v4u w3 = {0u, 0u, 0u, 0u};
-    if (!leaf) w3 = vrec[3];
+    /* PAIR: the leaf's next record is words 3..5 (its first word shares w3 with the child links) */
+    const bool two = PAIR && leaf && (enc & 7u) != 0u;
+    v4u w4 = {0u, 0u, 0u, 0u}, w5 = w4;
+    if (!leaf || two) w3 = vrec[3];
+    if (two) {
+        w4 = vrec[4];
+        w5 = vrec[5];
+    }
     /* Every lane's record arrives as whole dwordx4 loads issued together: without this
        the compiler narrows loads to the components each branch uses (x4 + x3 + x2 +
        dword) and sinks the child links below the box test, i.e. 5-6 vector-memory
        instructions per step instead of 4 (each costs the address path ~16 cycles per
        wave whatever its width) and a second dependent round trip for node lanes. */
     asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+    if (PAIR) asm volatile("" : "+v"(w4), "+v"(w5));
     const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
     const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);
     const uint4 q3 = make_uint4(w3.x, w3.y, w3.z, w3.w);
@@ -284,94 +381,50 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 }
             }
         }
+        float bound = __uint_as_float(q1.w);
+        if (PAIR && two) { /* the second record, under the same rule (an order-free minimum) */
+            if (COUNT) cnt.tests++;
+            const float4 a2 = make_float4(__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z),
+                                          __uint_as_float(w3.w));
+            const float4 b2 = make_float4(__uint_as_float(w4.x), __uint_as_float(w4.y), __uint_as_float(w4.z), 0.0f);
+            const float4 c2 = make_float4(__uint_as_float(w5.x), __uint_as_float(w5.y), __uint_as_float(w5.z), 0.0f);
+            float t2 = 0.0f;
+            if (mt_test(o, d, a2, b2, c2, t2)) {
+                if (any_hit) {
+                    if (t2 < s.best_t && t2 > tmin) {
+                        s.best = slot + 1;
+                        return true;
+                    }
+                } else if (!(t2 < tmin)) {
+                    bool acc = t2 < s.best_t;
+                    if (!acc && t2 == s.best_t)
+                        acc = s.best < 0 || __float_as_int(a2.w) > __float_as_int(tris[3 * s.best].w);
+                    if (acc) {
+                        s.best = slot + 1;
+                        s.best_t = t2;
+                    }
+                }
+            }
+            bound = __uint_as_float(w4.w);
+        }
         /* a camera candidate list (k_pixel_lists) is sorted, r1.w = the next candidate's
            earliest accept t: past the best hit, nothing later can be accepted (tree leaves: 0) */
-        if (!any_hit && s.best_t < __uint_as_float(q1.w)) return true;
-        if (enc & 7u) { /* next triangle of this leaf */
+        if (!any_hit && s.best_t < bound) return true;
+        if (PAIR && two) {
+            if ((enc & 7u) >= 2u) { /* the leaf's triangles after these two */
+                s.node = ~(int)((((enc >> 3) + 2u) << 3) | ((enc & 7u) - 2u));
+                return false;
+            }
+        } else if (enc & 7u) { /* next triangle of this leaf */
             s.node = ~(int)((((enc >> 3) + 1u) << 3) | ((enc & 7u) - 1u));
             return false;
         }
     } else {
         if (COUNT) cnt.nodes++;
-        const float tmax_c = t_slack(s.best_t);
-        const uint32_t w = q0.w;
-        constexpr int kExpBias = RT_QEXP_MIN + 24; /* scales carry the 2^24 of the f16-subnormal planes */
-        const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + kExpBias);
-        const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + kExpBias);
-        const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + kExpBias);
-        const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
-        const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
-        const float bzo = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
-        const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-        const uint32_t nxw = px ? q1.x : q1.y, fxw = px ? q1.y : q1.x;
-        const uint32_t nyw = py ? q1.z : q1.w, fyw = py ? q1.w : q1.z;
-        const uint32_t nzw = pz ? q2.x : q2.y, fzw = pz ? q2.y : q2.x;
         float t[4];
         int c[4];
-        int nhit = 0;
-        /* Plane bytes as f16 subnormals: v_perm_b32 spreads two bytes of a plane word into
-           the low bytes of two 16-bit halves (0x00bb = b * 2^-24 as f16, exact), and
-           v_fma_mix_f32 converts a half and does the FMA in one instruction, with the
-           2^24 folded into the scale's exponent: (b * 2^-24) * (s * 2^24) + base is exactly
-           fma(b, s, base) — the same bits as a byte convert + FMA, in 3/4 of the VALU. */
-        const float sx24 = sx, sy24 = sy, sz24 = sz;
-        const uint32_t nx01 = __builtin_amdgcn_perm(0u, nxw, 0x0c010c00u), nx23 = __builtin_amdgcn_perm(0u, nxw, 0x0c030c02u);
-        const uint32_t ny01 = __builtin_amdgcn_perm(0u, nyw, 0x0c010c00u), ny23 = __builtin_amdgcn_perm(0u, nyw, 0x0c030c02u);
-        const uint32_t nz01 = __builtin_amdgcn_perm(0u, nzw, 0x0c010c00u), nz23 = __builtin_amdgcn_perm(0u, nzw, 0x0c030c02u);
-        const uint32_t fx01 = __builtin_amdgcn_perm(0u, fxw, 0x0c010c00u), fx23 = __builtin_amdgcn_perm(0u, fxw, 0x0c030c02u);
-        const uint32_t fy01 = __builtin_amdgcn_perm(0u, fyw, 0x0c010c00u), fy23 = __builtin_amdgcn_perm(0u, fyw, 0x0c030c02u);
-        const uint32_t fz01 = __builtin_amdgcn_perm(0u, fzw, 0x0c010c00u), fz23 = __builtin_amdgcn_perm(0u, fzw, 0x0c030c02u);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const float tn = __builtin_fmaxf(
-                __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nx01 : nx23, i & 1), sx24, bx),
-                                __builtin_fmaf(half_of(i < 2 ? ny01 : ny23, i & 1), sy24, by)),
-                __builtin_fmaxf(__builtin_fmaf(half_of(i < 2 ? nz01 : nz23, i & 1), sz24, bzo), tmin_c));
-            const float tf = __builtin_fminf(
-                __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fx01 : fx23, i & 1), sx24, bx),
-                                __builtin_fmaf(half_of(i < 2 ? fy01 : fy23, i & 1), sy24, by)),
-                __builtin_fminf(__builtin_fmaf(half_of(i < 2 ? fz01 : fz23, i & 1), sz24, bzo), tmax_c));
-            const bool h = tn <= tf; /* an unused slot's inverted box never passes */
-            c[i] = (int)(i == 0 ? q3.x : i == 1 ? q3.y : i == 2 ? q3.z : q3.w);
-            /* Any hit (the answer is order-free): children whose box holds the ray origin (the
-               surface a shadow ray leaves, whose own triangles it cannot hit) are visited
-               last, and a ray leaving the mesh (`longest`) takes the others by the length of
-               its box segment, longest first — measured on the CPU model to find an occluder
-               in the fewest steps; rays from the box walls keep nearest first. */
-            const float key = longest ? tn - tf : tn;
-            t[i] = h ? (any_hit && tn <= 0.0f ? key + 1e4f : key) : kInf;
-            nhit += h ? 1 : 0;
-        }
-        /* Determinant cull (rt_quant.h): the node's normal box bounds d . N = det over its
-           subtree; below 1e-4 (with the float error bound) no triangle can be accepted, so
-           the subtree is skipped.  Culling only: the same results, fewer steps. */
-        {
-            /* v_perm_b32 picks, per axis, the hi byte (d >= 0) or the lo byte into `nb` (the box
-               corner maximising d . N) and the other into `fb`; v_cvt_f32_ubyteN converts in
-               place; the +128 byte bias folds into one per-ray term */
-            const uint32_t nlo = q2.z, nhi = q2.w;
-            const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
-            const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
-            const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
-            const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
-            const float bias = 128.0f * (d.x + d.y + d.z);
-            const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
-                                             __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu),
-                                                            __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
-            const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
-                                             __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu),
-                                                            __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
-            const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
-            /* bias rounding: |fl(128 sum d) - 128 sum d| <= 3u * 128 |d|_1, inside the margin */
-            const float bound = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
-            if (bound < 1e-4f) nhit = 0;
-        }
+        const int nhit = node_children(q0, q1, q2, q3, inv, oi, d, s.best_t, any_hit, longest, t, c);
         if (nhit > 0) {
-            cas(t[0], c[0], t[1], c[1]);
-            cas(t[2], c[2], t[3], c[3]);
-            cas(t[0], c[0], t[2], c[2]);
-            cas(t[1], c[1], t[3], c[3]);
-            cas(t[1], c[1], t[2], c[2]);
             if (lds_only) {
                 /* the nhit - 1 farther hits, farthest first, written unconditionally at
                    sp, sp+1, sp+2 (slots above the new top hold junk) */
@@ -396,6 +449,7 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     else s.node = stk.pop();
     return false;
 }
+
 
 /* One traversal step; returns true when the query is complete.  Closest hit:
    the result equals the reference's linear loop (minimum t, ties to the highest
@@ -602,6 +656,22 @@ __device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uin
     return ((yl / stripe) * n_ranks + rank) * stripe + (yl % stripe);
 }
 
+/* A pixel's camera-ray candidate list (k_pixel_lists) packed in one word, read when the lane takes
+   the pixel instead of before every sample's camera query (one dependent load less per sample):
+   (first slot / 8) << RT_LIST_BITS | (count - 1) — lists start on 8-record multiples and slots stay
+   below 2^28 (rt_host.cpp list_cap), so the word stays below RT_LPACK_EMPTY. */
+constexpr uint32_t RT_LPACK_NONE = 0xffffffffu, RT_LPACK_EMPTY = 0xfffffffeu;
+__device__ __forceinline__ uint32_t list_pack(const RtTriLaunch &a, uint32_t x, uint32_t yl, uint32_t tiles_x)
+{
+    if (!a.list_code) return RT_LPACK_NONE;
+    const uint32_t code = a.list_code[yl * a.W + x];
+    const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
+    if (code == RT_LIST_NONE) return RT_LPACK_NONE;
+    if (code == RT_LIST_EMPTY) return RT_LPACK_EMPTY;
+    const uint32_t first = block + ((code >> RT_LIST_BITS) << 3);
+    return ((first >> 3) << RT_LIST_BITS) | (code & (RT_LIST_MAX - 1u));
+}
+
 #ifndef RT_SEED_UNROLL
 #define RT_SEED_UNROLL 4 /* seed-pass traversal steps per loop iteration */
 #endif
@@ -788,6 +858,138 @@ __device__ __forceinline__ bool coop_step(const float4 *__restrict__ nodes, cons
     return false;
 }
 
+#ifndef RT_SEED_PAIR
+#define RT_SEED_PAIR 0 /* the one-lane seed pass tests two triangles of a leaf or list block per step */
+#endif
+
+#ifndef RT_COOP_MULTI
+#define RT_COOP_MULTI 1 /* the seed pass's 4-lane groups take one stack item per lane (coop_round) */
+#endif
+
+/* Cooperative closest-hit query, one stack ITEM per lane: each round the 4 lanes of a group take
+   the top entries of the group's stack — a node (one lane: its 4 child boxes) or the triangles of
+   a leaf or candidate-list block (one lane each) — so a round tests up to 4 records of different
+   subtrees instead of one node's boxes (scripts/sim_group_trav.cpp on box-path queries: 3.2
+   rounds per closest-hit query, against 4.9 one-record steps).  The closest hit is order-free
+   (minimum t, ties to the highest original index), so taking entries out of depth-first order
+   changes only the work; a sorted candidate list's early end takes the bound of the last record
+   tested, the latest in list order.  The group's whole query is on its stack (q.sp entries: the
+   root, or the list blocks, pushed at the start); the item assignment is computed alike in the
+   4 lanes.  Above `multi_sp` entries a round takes ONE item: 4 nodes add at most 12 entries, and
+   a one-item depth-first walk from there at most the tree's worst stack (rt_host.cpp), so the
+   stack stays inside the group's RT_COOP_STACK words. */
+__device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                           CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
+                                           uint32_t n_nodes, uint32_t n_recs, int multi_sp)
+{
+    const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
+    if (q.sp <= 0) return true;
+    const int L = q.sp <= multi_sp ? 4 : 1; /* lanes taking items this round */
+    int e[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = gst[q.sp - 1 - j]; /* read past the bottom: slot 0, unused */
+    /* entry j (from the top) takes one lane if a node, one per triangle if a leaf; a leaf only
+       partly taken stays on the stack with its first triangles removed */
+    int item = 0, off = 0, nfull = 0, cum = 0, part = 0;
+    bool act = false, partial = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (j < q.sp && cum < L) {
+            const int ej = e[j];
+            const uint32_t en = ~(uint32_t)ej;
+            const int dm = ej >= 0 ? 1 : (int)(en & 7u) + 1;
+            if (sub >= cum && sub < cum + dm && sub < L) {
+                item = ej;
+                off = sub - cum;
+                act = true;
+            }
+            if (cum + dm <= L) {
+                ++nfull;
+            } else {
+                const uint32_t used = (uint32_t)(L - cum);
+                part = ~(int)((((en >> 3) + used) << 3) | ((en & 7u) - used));
+                partial = true;
+            }
+            cum += dm;
+        }
+    }
+    const int n_act = cum < L ? cum : L; /* lanes 0 .. n_act - 1 hold an item */
+    const bool leaf = item < 0;
+    const uint32_t slot = (~(uint32_t)item >> 3) + (uint32_t)off;
+    /* every record index is checked (a defect ends the query instead of reading outside the tree) */
+    const bool bad = act && (leaf ? slot >= n_recs : (uint32_t)item >= n_nodes);
+    if ((__ballot(bad) >> gbase) & 15ull) return true;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u w0 = {0u, 0u, 0u, 0u}, w1 = w0, w2 = w0, w3 = w0;
+    if (act) {
+        const v4u *vrec = reinterpret_cast<const v4u *>(leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * slot
+                                                             : reinterpret_cast<const uint4 *>(nodes) + 4 * item);
+        w0 = vrec[0];
+        w1 = vrec[1];
+        w2 = vrec[2];
+        if (!leaf) w3 = vrec[3];
+    }
+    asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+    float ct = kInf, lbound = 0.0f;
+    int co = -1, cs = -1, nh = 0;
+    float t[4];
+    int c[4];
+    if (act && leaf) {
+        const float4 ta = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z),
+                                      __uint_as_float(w0.w));
+        const float4 tb = make_float4(__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z), 0.0f);
+        const float4 tc = make_float4(__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z), 0.0f);
+        float tt = 0.0f;
+        const bool h = mt_test(o, d, ta, tb, tc, tt);
+        const int orig = __float_as_int(ta.w);
+        if (h && !(tt < tmin) && (tt < q.best_t || (tt == q.best_t && orig > q.best_orig))) {
+            ct = tt;
+            co = orig;
+            cs = (int)slot;
+        }
+        lbound = __uint_as_float(w1.w); /* a list record: the next candidate's bound (tree leaves: 0) */
+    } else if (act) {
+        const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
+        const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w), q3 = make_uint4(w3.x, w3.y, w3.z, w3.w);
+        nh = node_children(q0, q1, q2, q3, q.inv, q.oi, d, q.best_t, false, false, t, c);
+    }
+    /* the group's best candidate: minimum t, ties to the highest original index */
+    {
+        const float ot = quad_xorf1(ct);
+        const int oo = quad_xor<1>(co), os = quad_xor<1>(cs);
+        const bool take = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
+        ct = take ? ot : ct;
+        co = take ? oo : co;
+        cs = take ? os : cs;
+    }
+    {
+        const float ot = quad_xorf2(ct);
+        const int oo = quad_xor<2>(co), os = quad_xor<2>(cs);
+        const bool take = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
+        ct = take ? ot : ct;
+        co = take ? oo : co;
+        cs = take ? os : cs;
+    }
+    if (cs >= 0) {
+        q.best = cs;
+        q.best_t = ct;
+        q.best_orig = co;
+    }
+    if (q.best_t < __int_as_float(quad_bcast(__float_as_int(lbound), n_act - 1))) return true;
+    /* the stack: the taken entries off, a partly taken leaf back on top, then each node lane's hit
+       children (lane 0's on top, each lane's nearest child last) */
+    const int h1 = quad_dpp<0x55>(nh), h2 = quad_dpp<0xAA>(nh), h3 = quad_dpp<0xFF>(nh);
+    const int total = quad_dpp<0x00>(nh) + h1 + h2 + h3;
+    const int above = (sub < 1 ? h1 : 0) + (sub < 2 ? h2 : 0) + (sub < 3 ? h3 : 0);
+    const int sp = q.sp - nfull;
+    if (partial && sub == 0) gst[sp - 1] = part;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < nh) gst[sp + above + nh - 1 - i] = c[i];
+    q.sp = sp + total;
+    return q.sp == 0;
+}
+
 /* Sample-split tiles, step 1: the seed pass.  A pixel's random numbers depend only on its
    closest hits (trace_path_tri, rtcommon.h:371-468): per surface hit two draws per light
    whatever its shadow ray finds (:88-92), two more for the Lambert bounce off the box (:459);
@@ -822,6 +1024,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
     bool have = false, next = false, running = false, fin = false, drained = false;
     uint32_t x = 0, yl = 0, sample = 0, depth = 0;
+    uint32_t lpack = RT_LPACK_NONE; /* the pixel's candidate list (list_pack) */
     uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
     Seed seed = {0u, 0u};
     V3 qo = v3(0.0f, 0.0f, 0.0f), qd = v3(0.0f, 0.0f, 1.0f);
@@ -867,6 +1070,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
+                        lpack = list_pack(a, x, yl, tiles_x);
                         sample = 0;
                         have = true;
                         next = true;
@@ -911,16 +1115,14 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 else trav_begin(ts, stk, qo, qd, kInf);
                 q_steps = 0;
                 running = true;
-                if (a.list_code) { /* the pixel's candidate list, as k_tris takes it */
-                    const uint32_t code = a.list_code[yl * a.W + x];
-                    const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
-                    const uint32_t pc = (code & (RT_LIST_MAX - 1u)) + 1u, first = block + ((code >> RT_LIST_BITS) << 3);
-                    if (code == RT_LIST_EMPTY) {
+                { /* the pixel's candidate list, as k_tris takes it */
+                    const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
+                    if (lpack == RT_LPACK_EMPTY) {
                         running = false;
                         ts.best = -1;
                         cq.best = -1;
                         fin = true;
-                    } else if (code != RT_LIST_NONE) {
+                    } else if (lpack != RT_LPACK_NONE) {
                         for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
                             const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
                             const int v = ~(int)(((first + 8u * b) << 3) | (k - 1u));
@@ -936,6 +1138,11 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         else ts.node = n0;
                     }
                 }
+                /* coop_round: the query's first entry (the root, or the list's first block) on top */
+                if (COOP && RT_COOP_MULTI && running) {
+                    if (lane == gbase) gst[cq.sp] = cq.node;
+                    ++cq.sp;
+                }
             }
         }
         /* step the running queries (the box pixels' chains at top priority: they run beside the
@@ -948,10 +1155,14 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 ++q_steps;
                 bool done;
                 if constexpr (G == 4) {
-                    done = coop_step(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs);
+                    if (RT_COOP_MULTI)
+                        done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs,
+                                          a.coop_multi_sp);
+                    else
+                        done = coop_step(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
-                    done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
+                    done = trav_step_q<false, RT_SEED_PAIR != 0>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
                 }
                 /* a query never takes 2^14 rounds (a ray meets far fewer nodes than that):
                    a bound every wave reaches, whatever a defect would do to a stack */
@@ -992,8 +1203,15 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                     ++depth;
                     if (depth <= a.max_depth) {
                         sample_done = false;
-                        if (COOP) coop_begin(cq, qo, qd, kInf);
-                        else trav_begin(ts, stk, qo, qd, kInf);
+                        if (COOP) {
+                            coop_begin(cq, qo, qd, kInf);
+                            if (RT_COOP_MULTI) { /* the root on the group's stack */
+                                if (lane == gbase) gst[0] = 0;
+                                cq.sp = 1;
+                            }
+                        } else {
+                            trav_begin(ts, stk, qo, qd, kInf);
+                        }
                         q_steps = 0;
                         running = true;
                     }
@@ -1442,6 +1660,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     trav_begin(ts, stk, qo, qd, qt);
                     running = true;
                     if (!shadow && depth == 0 && a.list_code) { /* a camera ray: the pixel's candidate list */
+                        /* (read per sample: kept per pixel in LDS, list_pack, it measured 98.2 -> 101.7 ms) */
                         const uint32_t code = a.list_code[yl * a.W + x];
                         const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
                         const uint32_t pc = (code & (RT_LIST_MAX - 1u)) + 1u, first = block + ((code >> RT_LIST_BITS) << 3);

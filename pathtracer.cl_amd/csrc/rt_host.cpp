@@ -123,7 +123,10 @@ struct rt_ctx {
        for the chains); 4 x 4 probe rays per pixel to find them */
     uint32_t seed_width = 4; /* lanes per seed-pass query of the long chains (1 or 4) */
     uint32_t split_probe = 4;
-    uint32_t split_gpw = 0; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
+#ifndef RT_SPLIT_GPW
+#define RT_SPLIT_GPW 0
+#endif
+    uint32_t split_gpw = RT_SPLIT_GPW; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
     float *d_split_col = nullptr;     /* per sample and pixel: its radiance */
     uint32_t *d_split_counter = nullptr; /* [0]: the seed pass's cursor, [32]: the box pixels' (own line) */

@@ -86,10 +86,8 @@ struct TravCounts {
     uint32_t leaves;
 };
 
-/* Leaf: the reference's triangle tests on slots [first, first+count).  The
-   records of two triangles are fetched together (6 x dwordx4) before either is
-   tested, so a leaf costs ceil(count/2) memory round trips instead of up to two
-   per triangle. */
+/* Leaf of the full-precision traversals (trav_step, traverse): the reference's triangle tests on
+   slots [first, first+count), in order, ending at an any-hit query's first occluder. */
 template <bool COUNT>
 __device__ __forceinline__ bool leaf_accept(int s, float4 a, V3 d, bool ok, float t, float tmin, float tmax,
                                             bool any_hit, int &best, int &best_orig, float &best_t, bool &done)
@@ -309,10 +307,8 @@ __device__ __forceinline__ int node_children(uint4 q0, uint4 q1, uint4 q2, uint4
    exactly one 64-B record per step — a node, or ONE triangle of its current leaf —
    with the same three dwordx4 loads, so a wave-step costs one memory round trip
    whatever mix of node and leaf lanes it holds (a leaf of k triangles takes k
-   steps; the leaf cursor is the leaf code itself: first slot and remaining count).
-   PAIR (the seed pass's one-lane queries, which are mostly short candidate lists): a leaf lane
-   with two or more triangles left fetches and tests two records in the step. */
-template <bool COUNT, bool PAIR = false>
+   steps; the leaf cursor is the leaf code itself: first slot and remaining count). */
+template <bool COUNT>
 __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                             TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
                                             TravCounts &cnt, bool longest = false)
@@ -332,21 +328,13 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
     /* the child links (d[12..15]) only for node lanes: the load runs under their exec mask,
        so leaf lanes add no addresses to it (-1 %) */
     v4u w3 = {0u, 0u, 0u, 0u};
-    /* PAIR: the leaf's next record is words 3..5 (its first word shares w3 with the child links) */
-    const bool two = PAIR && leaf && (enc & 7u) != 0u;
-    v4u w4 = {0u, 0u, 0u, 0u}, w5 = w4;
-    if (!leaf || two) w3 = vrec[3];
-    if (two) {
-        w4 = vrec[4];
-        w5 = vrec[5];
-    }
+    if (!leaf) w3 = vrec[3];
     /* Every lane's record arrives as whole dwordx4 loads issued together: without this
        the compiler narrows loads to the components each branch uses (x4 + x3 + x2 +
        dword) and sinks the child links below the box test, i.e. 5-6 vector-memory
        instructions per step instead of 4 (each costs the address path ~16 cycles per
        wave whatever its width) and a second dependent round trip for node lanes. */
     asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
-    if (PAIR) asm volatile("" : "+v"(w4), "+v"(w5));
     const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
     const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);
     const uint4 q3 = make_uint4(w3.x, w3.y, w3.z, w3.w);
@@ -381,41 +369,10 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 }
             }
         }
-        float bound = __uint_as_float(q1.w);
-        if (PAIR && two) { /* the second record, under the same rule (an order-free minimum) */
-            if (COUNT) cnt.tests++;
-            const float4 a2 = make_float4(__uint_as_float(w3.x), __uint_as_float(w3.y), __uint_as_float(w3.z),
-                                          __uint_as_float(w3.w));
-            const float4 b2 = make_float4(__uint_as_float(w4.x), __uint_as_float(w4.y), __uint_as_float(w4.z), 0.0f);
-            const float4 c2 = make_float4(__uint_as_float(w5.x), __uint_as_float(w5.y), __uint_as_float(w5.z), 0.0f);
-            float t2 = 0.0f;
-            if (mt_test(o, d, a2, b2, c2, t2)) {
-                if (any_hit) {
-                    if (t2 < s.best_t && t2 > tmin) {
-                        s.best = slot + 1;
-                        return true;
-                    }
-                } else if (!(t2 < tmin)) {
-                    bool acc = t2 < s.best_t;
-                    if (!acc && t2 == s.best_t)
-                        acc = s.best < 0 || __float_as_int(a2.w) > __float_as_int(tris[3 * s.best].w);
-                    if (acc) {
-                        s.best = slot + 1;
-                        s.best_t = t2;
-                    }
-                }
-            }
-            bound = __uint_as_float(w4.w);
-        }
         /* a camera candidate list (k_pixel_lists) is sorted, r1.w = the next candidate's
            earliest accept t: past the best hit, nothing later can be accepted (tree leaves: 0) */
-        if (!any_hit && s.best_t < bound) return true;
-        if (PAIR && two) {
-            if ((enc & 7u) >= 2u) { /* the leaf's triangles after these two */
-                s.node = ~(int)((((enc >> 3) + 2u) << 3) | ((enc & 7u) - 2u));
-                return false;
-            }
-        } else if (enc & 7u) { /* next triangle of this leaf */
+        if (!any_hit && s.best_t < __uint_as_float(q1.w)) return true;
+        if (enc & 7u) { /* next triangle of this leaf */
             s.node = ~(int)((((enc >> 3) + 1u) << 3) | ((enc & 7u) - 1u));
             return false;
         }
@@ -676,13 +633,9 @@ __device__ __forceinline__ uint32_t list_pack(const RtTriLaunch &a, uint32_t x, 
 #define RT_SEED_UNROLL 4 /* seed-pass traversal steps per loop iteration */
 #endif
 
-/* Cooperative closest-hit query: the 4 lanes of a group (lanes 4g..4g+3 of a wave) advance ONE
-   query together — at a node each lane tests one child box, at a leaf (or a candidate-list
-   block) each lane tests one triangle — so a step's work is a quarter of the per-lane step's
-   and a leaf of up to 4 triangles takes one memory round trip instead of one per triangle.  The
-   group's stack lives in LDS (RT_COOP_STACK entries per group).  The result is the reference's
-   closest hit (minimum t, ties to the highest original index: an order-free rule). */
-/* quad (4-lane group) exchanges through DPP quad_perm: a VALU modifier, not an LDS round trip
+/* Cooperative queries of the long chains' seed pass (coop_round below): the 4 lanes of a group
+   (lanes 4g..4g+3 of a wave) advance ONE query together, its stack in LDS (RT_COOP_STACK entries
+   per group).  Quad (4-lane group) exchanges through DPP quad_perm: a VALU modifier, not an LDS round trip
    like ds_bpermute (__shfl), whose latency a lone chain's wave cannot hide */
 template <int CTRL>
 __device__ __forceinline__ int quad_dpp(int v)
@@ -736,134 +689,8 @@ __device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
     q.sp = 0;
 }
 
-/* one step; true when the query is complete */
-__device__ __forceinline__ bool coop_step(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
-                                          CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
-                                          uint32_t n_nodes, uint32_t n_recs)
-{
-    const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
-    const int node = q.node;
-    const bool leaf = node < 0;
-    const uint32_t enc = (uint32_t)(~node);
-    const uint32_t first = enc >> 3, cnt = (enc & 7u) + 1u;
-    /* every record index is checked (a defect ends the query instead of reading outside the tree) */
-    if (leaf ? first + cnt > n_recs : (uint32_t)node >= n_nodes) return true;
-    const bool tri_ok = leaf && (uint32_t)sub < cnt;
-    const uint4 *rec = leaf ? reinterpret_cast<const uint4 *>(tris) + 3 * (first + (tri_ok ? (uint32_t)sub : 0u))
-                            : reinterpret_cast<const uint4 *>(nodes) + 4 * node;
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    const v4u *vrec = reinterpret_cast<const v4u *>(rec);
-    v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2];
-    v4u w3 = {0u, 0u, 0u, 0u};
-    if (!leaf) w3 = vrec[3];
-    asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
-    if (leaf) {
-        const float4 ta = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z),
-                                      __uint_as_float(w0.w));
-        const float4 tb = make_float4(__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z), 0.0f);
-        const float4 tc = make_float4(__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z), 0.0f);
-        float t = 0.0f;
-        const bool h = mt_test(o, d, ta, tb, tc, t);
-        const int orig = __float_as_int(ta.w);
-        bool ok = tri_ok && h && !(t < tmin) && (t < q.best_t || (t == q.best_t && orig > q.best_orig));
-        float ct = ok ? t : kInf;
-        int co = ok ? orig : -1, cs = ok ? (int)(first + (uint32_t)sub) : -1;
-        /* the group's best candidate: minimum t, ties to the highest original index */
-        {
-            const float ot = quad_xorf1(ct);
-            const int oo = quad_xor<1>(co), os = quad_xor<1>(cs);
-            const bool take = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
-            ct = take ? ot : ct;
-            co = take ? oo : co;
-            cs = take ? os : cs;
-        }
-        {
-            const float ot = quad_xorf2(ct);
-            const int oo = quad_xor<2>(co), os = quad_xor<2>(cs);
-            const bool take = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
-            ct = take ? ot : ct;
-            co = take ? oo : co;
-            cs = take ? os : cs;
-        }
-        if (cs >= 0) {
-            q.best = cs;
-            q.best_t = ct;
-            q.best_orig = co;
-        }
-        /* a sorted candidate list's early end: the last tested record's next-candidate bound */
-        const uint32_t last = (cnt < 4u ? cnt : 4u) - 1u;
-        const float bound = __int_as_float(quad_bcast((int)w1.w, (int)last));
-        if (q.best_t < bound) return true;
-        if (cnt > 4u) {
-            q.node = ~(int)(((first + 4u) << 3) | (cnt - 5u));
-            return false;
-        }
-    } else {
-        const float tmin_c = -1e-3f, tmax_c = t_slack(q.best_t);
-        const V3 inv = q.inv, oi = q.oi;
-        const uint32_t w = w0.w;
-        const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
-        const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
-        const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
-        const float bx = __builtin_fmaf(__uint_as_float(w0.x), inv.x, -oi.x);
-        const float by = __builtin_fmaf(__uint_as_float(w0.y), inv.y, -oi.y);
-        const float bz = __builtin_fmaf(__uint_as_float(w0.z), inv.z, -oi.z);
-        const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-        const uint32_t sh = 8u * (uint32_t)sub;
-        const float nx = (float)(((px ? w1.x : w1.y) >> sh) & 0xffu), fx = (float)(((px ? w1.y : w1.x) >> sh) & 0xffu);
-        const float ny = (float)(((py ? w1.z : w1.w) >> sh) & 0xffu), fy = (float)(((py ? w1.w : w1.z) >> sh) & 0xffu);
-        const float nz = (float)(((pz ? w2.x : w2.y) >> sh) & 0xffu), fz = (float)(((pz ? w2.y : w2.x) >> sh) & 0xffu);
-        const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nx, sx, bx), __builtin_fmaf(ny, sy, by)),
-                                         __builtin_fmaxf(__builtin_fmaf(nz, sz, bz), tmin_c));
-        const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaf(fx, sx, bx), __builtin_fmaf(fy, sy, by)),
-                                         __builtin_fminf(__builtin_fmaf(fz, sz, bz), tmax_c));
-        bool hit = tn <= tf; /* an unused slot's inverted box never passes */
-        { /* determinant cull (rt_quant.h), as trav_step_q */
-            const uint32_t nlo = w2.z, nhi = w2.w;
-            const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
-            const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
-            const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
-            const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
-            const float bias = 128.0f * (d.x + d.y + d.z);
-            const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
-                                             __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu),
-                                                            __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
-            const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
-                                             __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu),
-                                                            __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
-            const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
-            const float bnd = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
-            if (bnd < 1e-4f) hit = false;
-        }
-        const int link = (int)(sub == 0 ? w3.x : sub == 1 ? w3.y : sub == 2 ? w3.z : w3.w);
-        const uint32_t gm = (uint32_t)(__ballot(hit) >> gbase) & 15u;
-        if (gm) {
-            /* rank among the group's hit children: nearest first, ties to the lower slot */
-            const float t1 = quad_xorf1(tn), t2 = quad_xorf2(tn), t3 = quad_xorf3(tn);
-            const int j1 = sub ^ 1, j2 = sub ^ 2, j3 = sub ^ 3;
-            const int rank = (((gm >> j1) & 1u) && (t1 < tn || (t1 == tn && j1 < sub)) ? 1 : 0) +
-                             (((gm >> j2) & 1u) && (t2 < tn || (t2 == tn && j2 < sub)) ? 1 : 0) +
-                             (((gm >> j3) & 1u) && (t3 < tn || (t3 == tn && j3 < sub)) ? 1 : 0);
-            const int nhit = __popc(gm);
-            const uint32_t r0 = (uint32_t)(__ballot(hit && rank == 0) >> gbase) & 15u;
-            const int next = quad_bcast(link, __ffs((int)r0) - 1);
-            if (hit && rank > 0) gst[q.sp + nhit - 1 - rank] = link; /* the nearest of them on top */
-            q.sp += nhit - 1;
-            q.node = next;
-            return false;
-        }
-    }
-    if (q.sp == 0) return true;
-    q.node = gst[--q.sp];
-    return false;
-}
-
-#ifndef RT_SEED_PAIR
-#define RT_SEED_PAIR 0 /* the one-lane seed pass tests two triangles of a leaf or list block per step */
-#endif
-
-#ifndef RT_COOP_MULTI
-#define RT_COOP_MULTI 1 /* the seed pass's 4-lane groups take one stack item per lane (coop_round) */
+#ifndef RT_SEED_EXISTS
+#define RT_SEED_EXISTS 1 /* seed-pass queries end at the first accepted triangle */
 #endif
 
 /* Cooperative closest-hit query, one stack ITEM per lane: each round the 4 lanes of a group take
@@ -1001,7 +828,7 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
    sample of every chunk and after the last one.  The queries are resumable: the wave steps
    every running query and a lane whose query completed advances at once, so no chain waits for
    its neighbours'. */
-template <int G> /* lanes per query: 1 (trav_step_q) or 4 (coop_step) */
+template <int G> /* lanes per query: 1 (trav_step_q) or 4 (coop_round) */
 __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
 {
     constexpr bool COOP = G > 1;
@@ -1139,7 +966,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                     }
                 }
                 /* coop_round: the query's first entry (the root, or the list's first block) on top */
-                if (COOP && RT_COOP_MULTI && running) {
+                if (COOP && running) {
                     if (lane == gbase) gst[cq.sp] = cq.node;
                     ++cq.sp;
                 }
@@ -1155,18 +982,18 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 ++q_steps;
                 bool done;
                 if constexpr (G == 4) {
-                    if (RT_COOP_MULTI)
-                        done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs,
-                                          a.coop_multi_sp);
-                    else
-                        done = coop_step(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs);
+                    done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, a.coop_multi_sp);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
-                    done = trav_step_q<false, RT_SEED_PAIR != 0>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
+                    done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
                 }
+                /* The seed needs only WHETHER a segment hits the mesh (a hit ends the sample
+                   after the light samples' draws, wherever it is): the query ends at its first
+                   accepted triangle (the closest-hit rule's acceptance, t >= tmin) */
+                const bool exists = RT_SEED_EXISTS && (COOP ? cq.best : ts.best) >= 0;
                 /* a query never takes 2^14 rounds (a ray meets far fewer nodes than that):
                    a bound every wave reaches, whatever a defect would do to a stack */
-                if (done || q_steps > (1u << 14)) {
+                if (done || exists || q_steps > (1u << 14)) {
                     running = false;
                     fin = true;
                 }
@@ -1205,10 +1032,8 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         sample_done = false;
                         if (COOP) {
                             coop_begin(cq, qo, qd, kInf);
-                            if (RT_COOP_MULTI) { /* the root on the group's stack */
-                                if (lane == gbase) gst[0] = 0;
-                                cq.sp = 1;
-                            }
+                            if (lane == gbase) gst[0] = 0; /* the root on the group's stack */
+                            cq.sp = 1;
                         } else {
                             trav_begin(ts, stk, qo, qd, kInf);
                         }

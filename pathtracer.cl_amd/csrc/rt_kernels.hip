@@ -629,6 +629,10 @@ __device__ __forceinline__ uint32_t list_pack(const RtTriLaunch &a, uint32_t x, 
     return ((first >> 3) << RT_LIST_BITS) | (code & (RT_LIST_MAX - 1u));
 }
 
+#ifndef RT_DIAG_SKIP
+#define RT_DIAG_SKIP 0 /* diagnostics builds: k_tris skips the box pixels (1) or the mesh pixels (2) */
+#endif
+
 #ifndef RT_SEED_UNROLL
 #define RT_SEED_UNROLL 4 /* seed-pass traversal steps per loop iteration */
 #endif
@@ -1422,7 +1426,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         sample = 0;
                         /* some of the probe's rays missed the mesh: box paths, long chains */
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
-                        if (spp > 0) {
+                        if (RT_DIAG_SKIP && (RT_DIAG_SKIP == 1 ? pclass != -1 : pclass == -1)) {
+                            mode = M_IDLE; /* diagnostics builds: the mesh / box pixels alone (wrong frames) */
+                            pclass = -1;
+                        } else if (spp > 0) {
                             mode = M_NEWSAMPLE;
                         } else { /* no samples: 0/0 pixels, seeds untouched (raytracer.cl:234-242) */
                             const float n = 0.0f;

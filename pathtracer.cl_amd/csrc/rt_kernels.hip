@@ -1083,6 +1083,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     /* the pixel sum and the path throughput, touched once per sample / segment, live in LDS
        (6 floats per lane) instead of six registers across the stepping loop */
     __shared__ float s_state[6 * RT_BLOCK];
+    /* the lane's pixel's candidate list (list_pack), read when it takes the pixel instead of before
+       every camera ray (LDS budget: 5 blocks per CU with the 23-entry stack, RT_STACK_DEPTH) */
+    __shared__ uint32_t s_list[RT_BLOCK];
     float *const st_acc = s_state + threadIdx.x, *const st_prop = s_state + 3 * RT_BLOCK + threadIdx.x;
 #define ACC_GET(k) st_acc[(k) * RT_BLOCK]
 #define ACC_SET(k, v) (st_acc[(k) * RT_BLOCK] = (v))
@@ -1399,6 +1402,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         const uint32_t in0 = (dy & 7u) * 8u + (dx & 7u);
                         take = take && (x >> 3) == (dx >> 3) && (yl >> 3) == (dy >> 3) && ((in - in0) & 63u) < a.diag_k;
                     }
+                    if (take) s_list[threadIdx.x] = list_pack(a, x, yl, tiles_x);
                     if (SPLIT && take) { /* the chunk's first seed, from the seed pass */
                         const uint2 sd = reinterpret_cast<const uint2 *>(
                             a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + chunk * a.split_chunk / a.split_fine];
@@ -1491,22 +1495,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 } else {
                     trav_begin(ts, stk, qo, qd, qt);
                     running = true;
-                    if (!shadow && depth == 0 && a.list_code) { /* a camera ray: the pixel's candidate list */
-                        /* (read per sample: kept per pixel in LDS, list_pack, it measured 98.2 -> 101.7 ms) */
-                        const uint32_t code = a.list_code[yl * a.W + x];
-                        const uint32_t block = a.list_tile[(yl >> 3) * tiles_x + (x >> 3)];
-                        const uint32_t pc = (code & (RT_LIST_MAX - 1u)) + 1u, first = block + ((code >> RT_LIST_BITS) << 3);
-                        if (code == RT_LIST_EMPTY) { /* no triangle can be accepted by any of the pixel's camera rays */
+                    if (!shadow && depth == 0) { /* a camera ray: the pixel's candidate list */
+                        const uint32_t lpack = s_list[threadIdx.x];
+                        const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
+                        if (lpack == RT_LPACK_EMPTY) {
                             running = false;
                             ts.best = -1;
                             fin = true;
-                        } else if (code != RT_LIST_NONE) {
-                            /* the candidates as virtual leaves of up to 8: the first is stepped
-                               now, the others wait on the (empty) stack, pushed last block
-                               first so that they pop in list order (the sorted list's early
-                               end relies on it).  (The first record apart in a dense array in
-                               tile order, neighbouring lanes reading neighbouring records:
-                               106.1 vs 103.3 ms.) */
+                        } else if (lpack != RT_LPACK_NONE) {
                             for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
                                 const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
                                 stk.push(~(int)(((first + 8u * b) << 3) | (k - 1u)));

@@ -716,35 +716,31 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
     if (q.sp <= 0) return true;
     const int L = q.sp <= multi_sp ? 4 : 1; /* lanes taking items this round */
-    int e[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) e[j] = gst[q.sp - 1 - j]; /* read past the bottom: slot 0, unused */
-    /* entry j (from the top) takes one lane if a node, one per triangle if a leaf; a leaf only
-       partly taken stays on the stack with its first triangles removed */
-    int item = 0, off = 0, nfull = 0, cum = 0, part = 0;
-    bool act = false, partial = false;
+    int e[4], cu[5];
+    cu[0] = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        if (j < q.sp && cum < L) {
-            const int ej = e[j];
-            const uint32_t en = ~(uint32_t)ej;
-            const int dm = ej >= 0 ? 1 : (int)(en & 7u) + 1;
-            if (sub >= cum && sub < cum + dm && sub < L) {
-                item = ej;
-                off = sub - cum;
-                act = true;
-            }
-            if (cum + dm <= L) {
-                ++nfull;
-            } else {
-                const uint32_t used = (uint32_t)(L - cum);
-                part = ~(int)((((en >> 3) + used) << 3) | ((en & 7u) - used));
-                partial = true;
-            }
-            cum += dm;
-        }
+        e[j] = gst[q.sp - 1 - j]; /* read past the bottom: slot 0, unused */
+        /* entry j (from the top) takes one lane if a node, one per triangle if a leaf */
+        const int dm = j >= q.sp ? 0 : e[j] >= 0 ? 1 : (int)(~(uint32_t)e[j] & 7u) + 1;
+        cu[j + 1] = cu[j] + dm;
     }
-    const int n_act = cum < L ? cum : L; /* lanes 0 .. n_act - 1 hold an item */
+    /* branch-free, alike in the 4 lanes: lane `sub` takes entry j with cu[j] <= sub < cu[j+1]; the
+       entries with cu[j+1] <= L are taken whole, and a leaf only partly taken stays on the stack
+       with its first triangles removed */
+    const int n_act = cu[4] < L ? cu[4] : L; /* lanes 0 .. n_act - 1 hold an item */
+    const bool act = sub < n_act;
+    const int j = (sub >= cu[1] ? 1 : 0) + (sub >= cu[2] ? 1 : 0) + (sub >= cu[3] ? 1 : 0);
+    const int item = j == 0 ? e[0] : j == 1 ? e[1] : j == 2 ? e[2] : e[3];
+    const int off = sub - (j == 0 ? 0 : j == 1 ? cu[1] : j == 2 ? cu[2] : cu[3]);
+    const int top = q.sp < 4 ? q.sp : 4;
+    int nfull = (cu[1] <= L ? 1 : 0) + (cu[2] <= L ? 1 : 0) + (cu[3] <= L ? 1 : 0) + (cu[4] <= L ? 1 : 0);
+    nfull = nfull < top ? nfull : top;
+    const int cp = nfull == 0 ? 0 : nfull == 1 ? cu[1] : nfull == 2 ? cu[2] : cu[3];
+    const bool partial = nfull < top && cp < L;
+    const int ep = nfull == 0 ? e[0] : nfull == 1 ? e[1] : nfull == 2 ? e[2] : e[3];
+    const uint32_t used = (uint32_t)(L - cp), enp = ~(uint32_t)ep;
+    const int part = ~(int)((((enp >> 3) + used) << 3) | ((enp & 7u) - used));
     const bool leaf = item < 0;
     const uint32_t slot = (~(uint32_t)item >> 3) + (uint32_t)off;
     /* every record index is checked (a defect ends the query instead of reading outside the tree) */

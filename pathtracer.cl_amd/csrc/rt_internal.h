@@ -13,12 +13,13 @@
 
 #include "rt_types.h"
 
-/* Traversal stack entries per lane kept in LDS (23 x 256 lanes x 4 B = 23 KB per
-   block, which with k_tris's other LDS (31,232 B per block) keeps 5 blocks per CU; 24 entries
-   plus the per-pixel list word measured 1.5 % slower: profiles/r03z); deeper entries go to a
-   per-lane global spill tail sized from the tree (rt_host.cpp spill_cap). */
+/* Traversal stack entries per lane kept in LDS (20 x 256 lanes x 4 B = 20 KB per block, which
+   with k_tris's other per-lane LDS — pixel sum and throughput, list word, hit normal: 31,232 B
+   per block in all — keeps 5 blocks per CU; one block more of LDS measured 3.5 % slower:
+   profiles/r03z, r03zb); deeper entries go to a per-lane global spill tail sized from the tree
+   (rt_host.cpp spill_cap). */
 #ifndef RT_STACK_DEPTH
-#define RT_STACK_DEPTH 23
+#define RT_STACK_DEPTH 20
 #endif
 /* Inner depth bound of the binary tree (median splits below it). */
 #define RT_BVH_MAX_DEPTH 33

@@ -136,9 +136,11 @@ __device__ __forceinline__ bool leaf_tests(const float4 *__restrict__ tris, int 
    would occupy the vector-memory address path for every LDS pop. */
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef __attribute__((address_space(3))) int lds_int;
+typedef __attribute__((address_space(3))) float lds_float;
 typedef __attribute__((address_space(1))) int32_t glob_int;
 #else
 typedef int lds_int;
+typedef float lds_float;
 typedef int32_t glob_int;
 #endif
 
@@ -311,7 +313,7 @@ __device__ __forceinline__ int node_children(uint4 q0, uint4 q1, uint4 q2, uint4
 template <bool COUNT>
 __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                             TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
-                                            TravCounts &cnt, bool longest = false)
+                                            TravCounts &cnt, bool longest = false, lds_float *hn_out = nullptr)
 {
     const V3 inv = s.inv, oi = s.oi;
     const int node = s.node;
@@ -366,6 +368,12 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
                 if (acc) {
                     s.best = slot;
                     s.best_t = t;
+                    if (hn_out) { /* the hit's unnormalised normal for the shading (rtcommon.h:389) */
+                        const V3 n = cross3(v3(c.x, c.y, c.z), v3(b.x, b.y, b.z));
+                        hn_out[0] = n.x;
+                        hn_out[RT_BLOCK] = n.y;
+                        hn_out[2 * RT_BLOCK] = n.z;
+                    }
                 }
             }
         }
@@ -416,9 +424,10 @@ __device__ __forceinline__ bool trav_step_q(const float4 *__restrict__ nodes, co
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trav_step(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                           TravState &s, Stack &stk, V3 o, V3 d, float tmin, bool any_hit,
-                                          TravCounts &cnt, bool longest = false)
+                                          TravCounts &cnt, bool longest = false, lds_float *hn_out = nullptr)
 {
-    if (TRAV == RT_TRAV_BVH4Q) return trav_step_q<COUNT>(nodes, tris, s, stk, o, d, tmin, any_hit, cnt, longest);
+    if (TRAV == RT_TRAV_BVH4Q)
+        return trav_step_q<COUNT>(nodes, tris, s, stk, o, d, tmin, any_hit, cnt, longest, hn_out);
     const float tmin_c = -1e-3f;
     const V3 inv = s.inv, oi = s.oi;
     int node = s.node;
@@ -1082,6 +1091,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     /* the lane's pixel's candidate list (list_pack), read when it takes the pixel instead of before
        every camera ray (LDS budget: 5 blocks per CU with the 23-entry stack, RT_STACK_DEPTH) */
     __shared__ uint32_t s_list[RT_BLOCK];
+    /* the closest hit's unnormalised normal, formed at its accept from the record in registers
+       (trav_step_q), so the path advance needs no second fetch of the hit's edges */
+    __shared__ float s_hn[3 * RT_BLOCK];
+    lds_float *const st_hn = (lds_float *)(s_hn + threadIdx.x);
     float *const st_acc = s_state + threadIdx.x, *const st_prop = s_state + 3 * RT_BLOCK + threadIdx.x;
 #define ACC_GET(k) st_acc[(k) * RT_BLOCK]
 #define ACC_SET(k, v) (st_acc[(k) * RT_BLOCK] = (v))
@@ -1172,11 +1185,17 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 if (ts.best >= 0) {
                     const float qt = ts.best_t;
                     hp = v3(qo.x + qd.x * qt, qo.y + qd.y * qt, qo.z + qd.z * qt);
-                    /* (forming the normal at the accept instead, from the record in registers,
-                       measured 8 % slower: three more live registers in the traversal) */
-                    const float4 e1 = tris[3 * ts.best + 1];
-                    const float4 e2 = tris[3 * ts.best + 2];
-                    hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z)); /* unnormalised, rtcommon.h:389 */
+                    /* the unnormalised normal (rtcommon.h:389): written to LDS at the accept, the
+                       same float operations on the same record (kept in registers instead it
+                       measured 8 % slower, r01; a second fetch of the edges here is one more
+                       dependent round trip per mesh hit) */
+                    if (TRAV == RT_TRAV_BVH4Q) {
+                        hn = v3(st_hn[0], st_hn[RT_BLOCK], st_hn[2 * RT_BLOCK]);
+                    } else {
+                        const float4 e1 = tris[3 * ts.best + 1];
+                        const float4 e2 = tris[3 * ts.best + 2];
+                        hn = cross3(v3(e2.x, e2.y, e2.z), v3(e1.x, e1.y, e1.z)); /* unnormalised, rtcommon.h:389 */
+                    }
                     tri_hit = true;
                 } else {
                     /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
@@ -1532,7 +1551,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         const bool shadow = (mode == M_SHADOW);
                         TravCounts tc = {0u, 0u, 0u};
                         if (trav_step<TRAV, COUNT>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, shadow, tc,
-                                                   shadow && tri_hit)) {
+                                                   shadow && tri_hit, st_hn)) {
                             running = false;
                             fin = true;
                         }

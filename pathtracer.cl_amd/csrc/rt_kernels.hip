@@ -750,6 +750,9 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     const int ep = nfull == 0 ? e[0] : nfull == 1 ? e[1] : nfull == 2 ? e[2] : e[3];
     const uint32_t used = (uint32_t)(L - cp), enp = ~(uint32_t)ep;
     const int part = ~(int)((((enp >> 3) + used) << 3) | ((enp & 7u) - used));
+    /* the partly taken leaf's rest goes back now, in place (below every push of this round), so
+       that nothing of the assignment stays live across the round but nfull */
+    if (partial && sub == 0) gst[q.sp - 1 - nfull] = part;
     const bool leaf = item < 0;
     const uint32_t slot = (~(uint32_t)item >> 3) + (uint32_t)off;
     /* every record index is checked (a defect ends the query instead of reading outside the tree) */
@@ -818,7 +821,6 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     const int total = quad_dpp<0x00>(nh) + h1 + h2 + h3;
     const int above = (sub < 1 ? h1 : 0) + (sub < 2 ? h2 : 0) + (sub < 3 ? h3 : 0);
     const int sp = q.sp - nfull;
-    if (partial && sub == 0) gst[sp - 1] = part;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
         if (i < nh) gst[sp + above + nh - 1 - i] = c[i];

@@ -76,7 +76,10 @@ constexpr uint32_t kProbeN = 2;
 /* a 1-spp frame traces fewer rays than a 2x2 probe would: one probe ray per pixel there (bunny
    class 1024^2 at 1 spp: a camera move cost 2.2 ms against a 1.0 ms frame with the 2x2 probe) */
 uint32_t probe_n(uint32_t sample_rate) { return sample_rate >= 2 ? kProbeN : 1u; }
-constexpr uint32_t kFetchK = 24;
+#ifndef RT_FETCH_K
+#define RT_FETCH_K 24
+#endif
+constexpr uint32_t kFetchK = RT_FETCH_K;
 constexpr uint32_t kFetchFrac = 24;
 
 } // namespace

@@ -49,6 +49,7 @@ NODE_BYTES = {"bvh": 64, "bvh4f": 112, "linear": 0}  # bytes read per node visit
 # bytes read per triangle test: the whole 48-B record (one-record steps of the compressed traversal), else
 # v0+orig (16), e1 (12), e2 (12); csrc/rt_internal.h
 TRI_BYTES = {"bvh": 48, "bvh4f": 40, "linear": 40}
+TRI_BYTES_8D = 36  # the reference's triangle_t per test
 PIXEL_BYTES = 16 + 8 + 8  # RGBA32F store + seed read + seed write per pixel
 
 
@@ -83,9 +84,75 @@ def parse():
     return ap.parse_args()
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start N fresh child processes of this script
+    (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set; nothing here has touched the GPU:
+    counting devices does not initialise it on this image), relay their output (rank 0 prints the
+    line) and return non-zero if any rank fails — then the others, which would wait in a collective
+    for it, are stopped.  With RCCL (the default) the node must have N devices; the gloo rehearsal
+    (BENCH_DIST_BACKEND=gloo) may share one."""
+    import signal
+    import subprocess
+
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py --gpus {n}: this node has {have} GPU(s); one rank per GPU needs {n} "
+                  "(BENCH_DIST_BACKEND=gloo rehearses the N > 1 path on fewer)", file=sys.stderr)
+            return 2
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.2)
+            if rc:
+                deadline = time.time() + 20
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -341,6 +408,10 @@ def main():
         # the same frames counting only the queries that ran a traversal (rank 0's counting
         # launch share; DESIGN.md §5: shadow rays answered without one are still rays)
         "mrays_traversed_per_sec": round(mrays * (rays_cnt - cnt.get("rays_skipped", 0)) / max(rays_cnt, 1), 2),
+        "value_traversed": round(mrays * (rays_cnt - cnt.get("rays_skipped", 0)) / max(rays_cnt, 1), 2),
+        "value_rule": ("value counts the reference's queries (closest-hit + shadow, equal to the oracle's counts); "
+                       "value_traversed leaves out the shadow rays answered without a traversal (tmax <= tmin, or "
+                       "cos(wi) <= 0, whose term rtcommon.h:93-95 drops after the visibility test)"),
         "higher_is_better": True,
         "scaling": "weak" if frames_per_rank else "strong",
         "vs_baseline": None,
@@ -373,6 +444,9 @@ def main():
         line["comm_note"] = comm_note
     if sharded is not None:
         line.update(sharded)
+        if sharded["ranks"] != world:
+            print(f"bench.py: {world} ranks launched but the communicator has {sharded['ranks']}", file=sys.stderr)
+            sys.exit(3)
     if cpu is not None and "gpu_vs_reference_bit_exact" in cpu:
         line["gpu_vs_reference_bit_exact"] = cpu["gpu_vs_reference_bit_exact"]
         line["gpu_vs_reference_pixels"] = cpu["gpu_vs_reference_pixels"]
@@ -497,21 +571,30 @@ def critical_chain(rt, pt, W, H, Wp, Hp, seeds0, kernel):
 
 def roofline_block(pt, kernel, cnt, traversal, pix, k_ms, workload, n_ranks, chain, rays_cnt, frame_ms=None,
                    pre_ms=0.0):
-    """Fractions of the resources the dominant kernel could be bound by, each <= 1:
-      hbm            PMC HBM bytes per launch (profiles/pmc_roofline.json, FETCH_SIZE x 2 + WRITE_SIZE)
-                     / live kernel time, vs 8 TB/s;
-      valu_issue     PMC VALU wave-instructions per launch, 2 cycles each on 1024 SIMD-32s at the
-                     profiled clock;
-      salu_issue     PMC SALU instructions on 256 scalar units;
-      vmem_address   PMC TA busy cycles / kernel cycles (the gather address path);
-      record_gather  node + triangle records per second (device counters) vs the best random
-                     64-B record rate measured on a table of the scene's size (profiles/gather_ceiling.json);
-      critical_path  the longest pixel chain rendered alone / the frame time.
-    bound = the largest.  Algorithmic bytes (every record counted as fetched) are reported too."""
+    """The dominant kernel against the HBM roofline, SURVEY.md §8(d): algorithmic bytes per launch =
+    nodes visited x 64 B (the compressed node) + triangle tests x 36 B (the reference's triangle_t)
+    + 32 B of pixel I/O per pixel, from the device counters of a counting launch of the same frame,
+    over the live (HIP-event) kernel time, against 8 TB/s.  `traffic` = the PMC HBM bytes per launch
+    (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) of the committed profile of this workload.
+
+    `fractions` adds every resource the kernel could be bound by, each <= 1, each recomputable from
+    the committed profile alone (its own kernel time and clock, profiles/pmc_roofline.json <-
+    profiles/<run>/pmc_summary.json):
+      hbm_pmc        PMC HBM bytes / the profiled launch time, vs 8 TB/s;
+      valu_issue     SQ_INSTS_VALU wave-instructions, 2 cycles each on 1024 SIMD-32s, over the
+                     profiled kernel cycles (GRBM_GUI_ACTIVE / 8 XCDs);
+      salu_issue     SQ_INSTS_SALU on 256 scalar units over those cycles;
+      vmem_address   TA busy cycles / those cycles (the gather address path);
+    and, measured live: record_gather (node + triangle records per second vs the best random 64-B
+    record rate measured on a table of the scene's size, profiles/gather_ceiling.json) and
+    critical_path (the frame's longest pixel chain rendered alone / the frame time).
+    `limiter` = the largest of them."""
     is_tris = kernel == pt.RayTracer.KERNEL_TRIS
     records = (cnt["nodes_visited"] + cnt["tris_tested"]) if is_tris else 0
-    alg_bytes = (cnt["nodes_visited"] * NODE_BYTES[traversal] + cnt["tris_tested"] * TRI_BYTES[traversal]
+    alg_bytes = (cnt["nodes_visited"] * NODE_BYTES[traversal] + cnt["tris_tested"] * TRI_BYTES_8D
                  if is_tris else 0) + pix * PIXEL_BYTES
+    fetched = (cnt["nodes_visited"] * NODE_BYTES[traversal] + cnt["tris_tested"] * TRI_BYTES[traversal]
+               if is_tris else 0) + pix * PIXEL_BYTES
     sec = k_ms * 1e-3
     fr = {}
     pm = None
@@ -519,45 +602,48 @@ def roofline_block(pt, kernel, cnt, traversal, pix, k_ms, workload, n_ranks, cha
     if tp.exists() and n_ranks == 1:
         pm = json.loads(tp.read_text()).get(workload)
     if pm:
+        sec_p = pm["avg_kernel_ms_rocprof"] * 1e-3
         f_ghz = pm["effective_clock_ghz"]
-        fr["hbm"] = {"achieved": pm["hbm_bytes_per_launch"] / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
-        fr["valu_issue"] = {"achieved": pm["sq_insts_valu"] / sec / 1e9, "peak": N_SIMD * f_ghz / 2,
-                            "unit": "G wave-instr/s"}
-        if pm.get("sq_insts_salu"):
-            fr["salu_issue"] = {"achieved": pm["sq_insts_salu"] / sec / 1e9, "peak": N_CU * f_ghz,
-                                "unit": "G instr/s"}
-        if pm.get("ta_busy_avr"):
-            fr["vmem_address"] = {"achieved": pm["ta_busy_avr"] / sec / 1e9, "peak": f_ghz,
-                                  "unit": "G busy cycles/s per TA"}
+        fr["hbm_pmc"] = {"achieved": pm["hbm_bytes_per_launch"] / sec_p / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+        fr["valu_issue"] = {"achieved": pm["valu_issue_frac"] * N_SIMD * f_ghz / 2, "peak": N_SIMD * f_ghz / 2,
+                            "unit": "G wave-instr/s", "frac_exact": pm["valu_issue_frac"]}
+        if pm.get("salu_issue_frac"):
+            fr["salu_issue"] = {"achieved": pm["salu_issue_frac"] * N_CU * f_ghz, "peak": N_CU * f_ghz,
+                                "unit": "G instr/s", "frac_exact": pm["salu_issue_frac"]}
+        if pm.get("ta_busy_frac"):
+            fr["vmem_address"] = {"achieved": pm["ta_busy_frac"] * f_ghz, "peak": f_ghz,
+                                  "unit": "G busy cycles/s per TA", "frac_exact": pm["ta_busy_frac"]}
+        for v in fr.values():
+            v["time_base"] = f"profiled launch {pm['avg_kernel_ms_rocprof']:.3f} ms at {f_ghz:.3f} GHz ({pm['source']})"
     gp = ROOT / "profiles" / "gather_ceiling.json"
     if is_tris and gp.exists() and traversal != "linear":
         g = json.loads(gp.read_text())
         fr["record_gather"] = {"achieved": records / sec / 1e9, "peak": g["best_grec_per_s"], "unit": "G records/s",
-                               "ceiling": g["source"]}
+                               "ceiling": g["source"], "time_base": "live kernel time"}
     if chain:
         fr["critical_path"] = {"achieved": chain["alone_ms"], "peak": round(frame_ms or k_ms, 3),
-                               "unit": "ms (chain alone / frame)",
-                               **chain}
+                               "unit": "ms (chain alone / frame)", "time_base": "live", **chain}
     for v in fr.values():
-        v["frac"] = round(v["achieved"] / v["peak"], 4)
+        v["frac"] = round(v.pop("frac_exact", v["achieved"] / v["peak"]), 4)
         v["achieved"] = round(v["achieved"], 3)
         v["peak"] = round(v["peak"], 3)
-    bound = max(fr, key=lambda k: fr[k]["frac"]) if fr else "hbm"
-    top = fr.get(bound) or {"achieved": alg_bytes / sec / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s (algorithmic)"}
-    over = sorted(k for k, v in fr.items() if v["frac"] > 1.0)
-    out = {"bound": bound, "achieved": top["achieved"], "peak": top["peak"], "unit": top["unit"],
-           "frac": top.get("frac", round(top["achieved"] / top["peak"], 4)),
+    limiter = max(fr, key=lambda k: fr[k]["frac"]) if fr else None
+    alg_gbps = alg_bytes / sec / 1e9
+    out = {"bound": "hbm", "achieved": round(alg_gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(alg_gbps / HBM_PEAK_GBS, 4),
            "traffic": pm["hbm_bytes_per_launch"] if pm else None,
            "traffic_unit": "HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE, PMC)" if pm else None,
            "traffic_source": pm["source"] if pm else None,
+           "achieved_def": "SURVEY 8(d) algorithmic bytes per launch (nodes x 64 B + triangle tests x 36 B + pixels x "
+                           "32 B, device counters) / live HIP-event kernel time",
+           "algorithmic_bytes_per_launch": int(alg_bytes),
+           "fetched_record_bytes_per_launch": int(fetched),
+           "limiter": limiter,
            "fractions": fr,
-           "fractions_over_1": over,
            "kernel": (f"k_tris<{traversal.upper()}>" if is_tris else "k_spheres"),
            "kernel_ms": round(k_ms, 3),
            "prepass_ms": round(pre_ms, 3),
-           "frame_kernels_ms": round(frame_ms or k_ms, 3),
-           "algorithmic_bytes_per_launch": int(alg_bytes),
-           "algorithmic_gbps": round(alg_bytes / sec / 1e9, 1)}
+           "frame_kernels_ms": round(frame_ms or k_ms, 3)}
     if is_tris:
         out["nodes_per_ray"] = round(cnt["nodes_visited"] / max(rays_cnt, 1), 2)
         out["tris_per_ray"] = round(cnt["tris_tested"] / max(rays_cnt, 1), 2)

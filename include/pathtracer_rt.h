@@ -214,8 +214,16 @@ typedef struct rt_render_info {
     double schedule_host_ms;   /* host time spent enqueueing / sizing the schedule this render */
     uint32_t split_chunks;     /* sample-split render (a tile with few pixels per lane): chunks per
                                   pixel, each an independent task seeded by the seed pass; 0: whole pixels */
+    uint32_t split_coop;       /* lanes per query of the long chains' seed pass (4: coop_round; 0: one) */
+    uint32_t split_guard;      /* read after completion: a defect guard of the long chains' seed pass
+                                  fired (record index out of range, group stack overflow, query round
+                                  bound); rt_synchronize then fails with RT_ERR_STATE */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
+/* The long chains of the last sample-split render (pixels_long of them: tile-local y * W + x, the
+   order of their slots), the pixels whose seed pass ran on the second stream with split_coop lanes
+   per query.  Copies min(cap, *n) entries; *n = pixels_long.  Diagnostics and parity tests. */
+int rt_last_long_chains(rt_ctx *ctx, uint32_t *out, uint32_t cap, uint32_t *n);
 
 /* ---- ray queries for hit-index parity (rtcommon.h:39-52 / :59-68 semantics).
    Host arrays; any_hit=0: out_idx = closest triangle (-1 none), out_t = its t;

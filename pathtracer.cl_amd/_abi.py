@@ -123,6 +123,8 @@ class RtRenderInfo(ctypes.Structure):
         ("lists_rebuilt", ctypes.c_uint32),
         ("schedule_host_ms", ctypes.c_double),
         ("split_chunks", ctypes.c_uint32),
+        ("split_coop", ctypes.c_uint32),
+        ("split_guard", ctypes.c_uint32),
     ]
 
 
@@ -162,6 +164,7 @@ SIGNATURES = {
     "rt_last_kernel_ms": (_i32, [_vp, ctypes.POINTER(_f32)]),
     "rt_last_kernel_split_ms": (_i32, [_vp, ctypes.POINTER(_f32), ctypes.POINTER(_f32)]),
     "rt_last_render_info": (_i32, [_vp, ctypes.POINTER(RtRenderInfo)]),
+    "rt_last_long_chains": (_i32, [_vp, _vp, _u32, ctypes.POINTER(_u32)]),
     "rt_trace_rays": (_i32, [_vp, _vp, _u32, _i32, _vp, _vp]),
     "rt_mesh_vertex_count": (_u32, [_u32]),
     "rt_make_mesh": (_i32, [_u32, _f32, _f32, _f32, _f32, _vp, _vp]),

@@ -110,6 +110,8 @@ struct rt_ctx {
                              costs about a traversal per pixel: a 1-spp frame does not repay it) */
     size_t list_mb = 4096; /* RT_LIST_MB: device memory of the list area (pixels beyond it take the tree) */
     std::vector<uint32_t> list_key; /* what the lists in the list area were built for (empty: none) */
+    uint64_t list_used_last = 0, list_cap_last = 0, list_npx_last = 0; /* the last list build: records taken /
+                                                                          given, its pixels */
     std::vector<uint32_t> last_view; /* the previous triangle render's view (camera, mesh, frame, tile) */
     uint32_t n_tris = 0;
     int32_t *d_spill = nullptr; /* per-lane stack overflow for the 4-wide traversal */
@@ -355,13 +357,18 @@ const float *trav_nodes(const rt_ctx *c)
 }
 
 /* Grow the triangle buffer to `records` 48-B records, keeping the first `keep` (the mesh's). */
-int ensure_tris_capacity(rt_ctx *c, size_t records, size_t keep, hipStream_t st)
+int ensure_tris_capacity(rt_ctx *c, size_t records, size_t keep, hipStream_t st, bool shrink = false)
 {
-    if (records <= c->tris_cap) return RT_OK;
+    /* grows to `records`; with `shrink`, also gives back an area more than twice the need */
+    if (records <= c->tris_cap && !(shrink && c->tris_cap > keep + 2 * (records - keep) + (1u << 20))) return RT_OK;
     float *nt = nullptr;
     HIPCHK(c, hipMalloc(&nt, records * 48));
-    HIPCHK(c, hipMemcpyAsync(nt, c->d_tris, keep * 48, hipMemcpyDeviceToDevice, st));
-    HIPCHK(c, hipStreamSynchronize(st));
+    hipError_t e = hipMemcpyAsync(nt, c->d_tris, keep * 48, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        (void)hipFree(nt);
+        return hip_fail(c, e, "triangle buffer copy");
+    }
     free_dev(c->d_tris);
     c->d_tris = nt;
     c->tris_cap = records;
@@ -611,7 +618,7 @@ int rt_create(int device, rt_ctx **out)
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evm) != hipSuccess ||
-        hipMalloc(&c->d_work, 64 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&c->d_counters, RT_N_COUNTERS * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_work, 64 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&c->d_counters, RT_COUNTER_WORDS * sizeof(unsigned long long)) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_HIP;
     }
@@ -961,7 +968,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         dout = c->d_stage;
         if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
     }
-    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT_N_COUNTERS * sizeof(unsigned long long), st));
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), st));
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;
     int e = 0;
@@ -1118,12 +1125,27 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         }
         const bool same_view = view == c->last_view;
         c->last_view = view;
+        /* The list area: after a build that did not fill its area, a new view's build gets twice
+           what the last one took per pixel plus 8 records per pixel (dragon 1080p: 24.9M records
+           used of the 89.5M the RT_LIST_MB cap allows), and the buffer gives back the rest; a build
+           that filled its area gets the whole cap again (pixels whose list does not fit take the
+           tree: the same bits).  The same view keeps the area its lists were built in. */
+        bool list_shrink = false;
+        if (c->list_cap_last && c->list_used_last < c->list_cap_last && c->list_npx_last) {
+            if (same_view) {
+                list_cap = std::min<uint64_t>(list_cap, c->list_cap_last);
+            } else {
+                const uint64_t est = (2 * c->list_used_last * npx + c->list_npx_last - 1) / c->list_npx_last + 8 * npx;
+                list_cap = std::min<uint64_t>(list_cap, est);
+                list_shrink = true;
+            }
+        }
         /* Lists pay for their pre-pass (about one traversal per pixel) within one frame from
            sampleRate 4 on; below, from the second frame of a view on, since they are then reused
            (bunny class 1024^2 at 1 spp: a 2.4-ms pre-pass against a 1.0-ms frame) */
         bool lists = (c->pixel_lists == 1 || (c->pixel_lists < 0 && (c->sample_rate >= 4 || same_view))) && bvh4 &&
                      list_cap > 0;
-        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), c->n_tris, st) != RT_OK) {
+        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), c->n_tris, st, list_shrink) != RT_OK) {
             (void)hipGetLastError(); /* out of device memory: no lists this render */
             lists = false;
         }
@@ -1199,6 +1221,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info_list_px = lists ? (size_t)npx : 0u;
         c->info.pixels_long = c->last_long;
         c->info.split_chunks = a.split_chunks;
+        c->info.split_coop = a.split_chunks && a.split_n_box ? a.split_coop : 0u;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
         c->info_list_pending = lists;
@@ -1252,8 +1275,15 @@ int rt_synchronize(rt_ctx *c)
     if (!c) return RT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    unsigned long long h[RT_N_COUNTERS];
+    unsigned long long h[RT_COUNTER_WORDS];
     HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+    if (c->info.lists_rebuilt) { /* the list area the new lists took: sizes the next build's area */
+        uint32_t used = 0;
+        HIPCHK(c, hipMemcpy(&used, c->d_list_alloc, sizeof(used), hipMemcpyDeviceToHost));
+        c->list_used_last = used;
+        c->list_cap_last = c->info.list_capacity;
+        c->list_npx_last = c->info_list_px;
+    }
     c->last.rays_closest = h[0];
     c->last.rays_shadow = h[1];
     c->last.nodes_visited = h[2];
@@ -1268,6 +1298,15 @@ int rt_synchronize(rt_ctx *c)
     c->last.pixel_rays_max = h[11];
     c->last.pixel_steps_max = h[12];
     c->last.pixels_long = c->last_long;
+    if (h[RT_CNT_GUARD]) { /* a defect guard of the long chains' seed pass: the frame is not the reference's */
+        c->info.split_guard = (uint32_t)h[RT_CNT_GUARD];
+        char msg[160];
+        snprintf(msg, sizeof(msg),
+                 "sample-split seed pass: a defect guard fired (flags 0x%x: 1 record index, 2 group stack, 4 round "
+                 "bound); the frame is invalid (RT_SPLIT=0 renders whole pixels)",
+                 (unsigned)h[RT_CNT_GUARD]);
+        return fail(c, RT_ERR_STATE, msg);
+    }
     return RT_OK;
 }
 
@@ -1359,6 +1398,18 @@ int rt_last_render_info(rt_ctx *c, rt_render_info *out)
     return RT_OK;
 }
 
+int rt_last_long_chains(rt_ctx *c, uint32_t *out, uint32_t cap, uint32_t *n)
+{
+    if (!c || !n || (cap && !out)) return RT_ERR_ARG;
+    *n = c->last_long;
+    const uint32_t k = std::min(cap, c->last_long);
+    if (!k) return RT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->d_split_box, (size_t)k * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 int rt_get_counters(const rt_ctx *c, rt_counters *out)
 {
     if (!c || !out) return RT_ERR_ARG;
@@ -1431,7 +1482,7 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
                     break;
                 }
             }
-        if (c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_N_COUNTERS * sizeof(unsigned long long), c->stream);
+        if (c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), c->stream);
         if (e == hipSuccess) {
             const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,
                                                 cap, d_idx, d_t, c->counting ? c->d_counters : nullptr, c->stream);

@@ -54,6 +54,11 @@
 #define RT_N_COUNTERS 13
 #define RT_CNT_SKIPPED 8
 #define RT_CNT_SHADE 9
+/* one word past the counters: the long chains' seed-pass defect guards (atomicOr of RT_GUARD_*);
+   the device counter buffer holds RT_COUNTER_WORDS words */
+#define RT_CNT_GUARD RT_N_COUNTERS
+#define RT_COUNTER_WORDS (RT_N_COUNTERS + 1)
+enum { RT_GUARD_INDEX = 1, RT_GUARD_STACK = 2, RT_GUARD_ROUNDS = 4 };
 
 /* One BVH node = 4 x float4 = 64 B (both children's boxes in the parent):
      n0 = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
@@ -127,7 +132,7 @@ struct RtTriLaunch {
     uint32_t sample_rate, max_depth, progressive;
     uint32_t stripe, n_ranks, rank;
     uint32_t *work_counter;
-    unsigned long long *counters; /* [RT_N_COUNTERS] */
+    unsigned long long *counters; /* [RT_COUNTER_WORDS]: the counters, then the guard word (RT_CNT_GUARD) */
     int32_t *spill;      /* per-lane stack overflow (4-wide traversal), spill_cap entries per lane */
     uint32_t spill_cap;
     const uint32_t *tile_order; /* queue position -> 8x8 tile index (NULL: row-major) */

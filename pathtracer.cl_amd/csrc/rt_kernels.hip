@@ -720,7 +720,7 @@ __device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
    stack stays inside the group's RT_COOP_STACK words. */
 __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                            CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
-                                           uint32_t n_nodes, uint32_t n_recs, int multi_sp)
+                                           uint32_t n_nodes, uint32_t n_recs, int multi_sp, uint32_t &defect)
 {
     const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
     if (q.sp <= 0) return true;
@@ -755,9 +755,13 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     if (partial && sub == 0) gst[q.sp - 1 - nfull] = part;
     const bool leaf = item < 0;
     const uint32_t slot = (~(uint32_t)item >> 3) + (uint32_t)off;
-    /* every record index is checked (a defect ends the query instead of reading outside the tree) */
+    /* every record index is checked: a defect ends the query instead of reading outside the tree,
+       and is reported (the render then fails: rt_synchronize) */
     const bool bad = act && (leaf ? slot >= n_recs : (uint32_t)item >= n_nodes);
-    if ((__ballot(bad) >> gbase) & 15ull) return true;
+    if ((__ballot(bad) >> gbase) & 15ull) {
+        defect |= RT_GUARD_INDEX;
+        return true;
+    }
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     v4u w0 = {0u, 0u, 0u, 0u}, w1 = w0, w2 = w0, w3 = w0;
     if (act) {
@@ -821,6 +825,10 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     const int total = quad_dpp<0x00>(nh) + h1 + h2 + h3;
     const int above = (sub < 1 ? h1 : 0) + (sub < 2 ? h2 : 0) + (sub < 3 ? h3 : 0);
     const int sp = q.sp - nfull;
+    if (sp + total > CoopStack::kCap) { /* cannot happen (multi_sp bound, rt_host.cpp): reported, not clamped */
+        defect |= RT_GUARD_STACK;
+        return true;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
         if (i < nh) gst[sp + above + nh - 1 - i] = c[i];
@@ -877,6 +885,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     coop_begin(cq, qo, qd, kInf);
     uint32_t st_steps = 0, st_box = 0, st_t0 = 0; /* diagnostics (RT_PIXEL_STATS): per pixel */
     uint32_t q_steps = 0;                          /* rounds of the current query */
+    uint32_t defect = 0;                           /* RT_GUARD_* that fired in this lane's queries */
     for (;;) {
         /* lanes (COOP: groups) without a pixel take the next ones of the queue */
         /* takers: the first split_gpw lanes (COOP: 4-lane groups) of the wave */
@@ -921,7 +930,12 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
             }
         }
         if (!__any(have)) {
-            if (drained) break;
+            if (drained) {
+                /* a guard that fired anywhere in the wave is reported once (rt_synchronize fails the render) */
+                const unsigned long long bad = __ballot(defect != 0);
+                if (bad && lane == __ffsll((long long)bad) - 1) atomicOr(&a.counters[RT_CNT_GUARD], (unsigned long long)defect);
+                break;
+            }
             continue;
         }
         /* a new sample: the chunk's first seed, then the camera ray and its query */
@@ -993,7 +1007,8 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 ++q_steps;
                 bool done;
                 if constexpr (G == 4) {
-                    done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, a.coop_multi_sp);
+                    done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, a.coop_multi_sp,
+                                      defect);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
                     done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
@@ -1003,7 +1018,8 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                    accepted triangle (the closest-hit rule's acceptance, t >= tmin) */
                 const bool exists = RT_SEED_EXISTS && (COOP ? cq.best : ts.best) >= 0;
                 /* a query never takes 2^14 rounds (a ray meets far fewer nodes than that):
-                   a bound every wave reaches, whatever a defect would do to a stack */
+                   a bound every wave reaches, whatever a defect would do to a stack (reported) */
+                if (q_steps > (1u << 14)) defect |= RT_GUARD_ROUNDS;
                 if (done || exists || q_steps > (1u << 14)) {
                     running = false;
                     fin = true;
@@ -1091,7 +1107,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
        (6 floats per lane) instead of six registers across the stepping loop */
     __shared__ float s_state[6 * RT_BLOCK];
     /* the lane's pixel's candidate list (list_pack), read when it takes the pixel instead of before
-       every camera ray (LDS budget: 5 blocks per CU with the 23-entry stack, RT_STACK_DEPTH) */
+       every camera ray (LDS budget: 5 blocks per CU beside the RT_STACK_DEPTH = 20-entry stack and
+       the hit normal: 31,232 B per block) */
     __shared__ uint32_t s_list[RT_BLOCK];
     /* the closest hit's unnormalised normal, formed at its accept from the record in registers
        (trav_step_q), so the path advance needs no second fetch of the hit's edges */
@@ -1307,7 +1324,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 dst[2] = col_z;
                 ++sample;
                 mode = (sample >= spp || sample % a.split_chunk == 0u) ? M_IDLE : M_NEWSAMPLE;
-                if (mode == M_IDLE) pclass = -1;
+                if (mode == M_IDLE) {
+                    pclass = -1;
+                    if (COUNT && a.pixel_stats) { /* diagnostics: the pixel's queries and steps over its chunks */
+                        uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
+                        atomicAdd(ps + 5, (uint32_t)pix_q);
+                        atomicAdd(ps + 6, (uint32_t)pix_steps);
+                    }
+                }
             } else if (sample_done) {
                 ACC_SET(0, ACC_GET(0) + col_x);
                 ACC_SET(1, ACC_GET(1) + col_y);
@@ -1428,6 +1452,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         sample = chunk * a.split_chunk;
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
                         mode = M_NEWSAMPLE;
+                        if (COUNT) pix_q = pix_steps = 0;
                     } else if (take) {
                         const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                         /* raytracer.cl:207-209: unshifted seed slot */

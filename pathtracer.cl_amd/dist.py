@@ -239,12 +239,43 @@ class NativeComm:
 
     @classmethod
     def from_torch(cls, device: int, group=None):
-        """Collective over a torch.distributed group: rank 0 makes the id, a broadcast carries it."""
+        """Collective over a torch.distributed group: rank 0 makes the id, a broadcast carries it.
+
+        Every rank takes the same collective steps whatever fails where: each checks that the library
+        and its rt_comm_* entry points load; rank 0 ALWAYS joins the broadcast, sending None (the
+        error marker) when it could not make the id; then one all_reduce (MIN) agrees on the
+        outcome, and only if every rank is ready does any rank enter ncclCommInitRank
+        (rt_comm_create).  Otherwise every rank raises, none of them waiting in a collective the
+        others never reach."""
+        import torch
         import torch.distributed as dist
 
-        obj = [cls.unique_id() if dist.get_rank(group) == 0 else None]
+        from . import _abi
+
+        rank = dist.get_rank(group)
+        err = None
+        try:
+            lib = _abi.load()
+            for sym in ("rt_comm_get_unique_id", "rt_comm_create", "rt_comm_render", "rt_comm_destroy"):
+                getattr(lib, sym)
+        except Exception as e:  # noqa: BLE001 - agreed on below
+            err = f"{type(e).__name__}: {e}"
+        uid = None
+        if rank == 0 and err is None:
+            try:
+                uid = cls.unique_id()
+            except Exception as e:  # noqa: BLE001
+                err = f"{type(e).__name__}: {e}"
+        obj = [uid if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
-        return cls(dist.get_world_size(group), dist.get_rank(group), device, obj[0])
+        if obj[0] is None and err is None:
+            err = "rank 0 could not make the communicator id"
+        dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        ready = torch.tensor([0 if err else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(ready, op=dist.ReduceOp.MIN, group=group)
+        if not int(ready.item()):
+            raise RuntimeError(f"native communicator not created on any rank ({err or 'a peer was not ready'})")
+        return cls(dist.get_world_size(group), rank, device, obj[0])
 
     def _check(self, st: int, what: str):
         if st != self._abi.RT_OK:

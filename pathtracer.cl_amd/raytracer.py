@@ -265,6 +265,17 @@ class RayTracer:
         self._check(fn(self._h, ctypes.byref(i)), "rt_last_render_info")
         return {f: getattr(i, f) for f, _ in _abi.RtRenderInfo._fields_}
 
+    def longChains(self) -> np.ndarray:
+        """rt_last_long_chains: the last sample-split render's long chains (tile-local y * W + x),
+        the pixels whose seed pass ran on the second stream (cooperative queries)."""
+        n = ctypes.c_uint32(0)
+        self._check(self._lib.rt_last_long_chains(self._h, None, 0, ctypes.byref(n)), "rt_last_long_chains")
+        out = np.empty(n.value, np.uint32)
+        if n.value:
+            self._check(self._lib.rt_last_long_chains(self._h, _abi.ptr(out), n.value, ctypes.byref(n)),
+                        "rt_last_long_chains")
+        return out
+
     def traceRays(self, rays: np.ndarray, any_hit: bool = False) -> tuple[np.ndarray, np.ndarray]:
         r = np.ascontiguousarray(rays, _abi.RAY_DTYPE)
         idx = np.empty(r.size, np.int32)

@@ -4,10 +4,14 @@ frame for N = 1, 2, 4, 8 ranks (rank 0 and the slowest rank) against 1/N of the 
     python profiles/tile_scaling.py [--config dragon] [--stripe 8]
 """
 import argparse
+import ctypes
 import json
+import os
 import sys
-import time
+import tempfile
 from pathlib import Path
+
+import numpy as np
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
@@ -36,27 +40,42 @@ def main():
     res = {}
     for n in (1, 2, 4, 8):
         times = []
-        for r in range(n):
+        for r in range(n):  # every rank's tile: the slowest sets the N-GPU frame time
             tile = (args.stripe, n, r) if n > 1 else None
             best = 1e9
             for _ in range(args.reps):
                 rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
                 best = min(best, rt.lastKernelMs())
             times.append(best)
-            if n > 1 and r >= 1 and n == 8 and r >= 3:
-                break  # a few ranks suffice to see the spread
-        res[n] = {"max_ms": max(times), "min_ms": min(times), "ranks_timed": len(times)}
-    # the costliest pixel (counting launch): clocks, queries, traversal steps
+        res[n] = {"max_ms": max(times), "min_ms": min(times), "ranks_timed": len(times),
+                  "rank_ms": [round(t, 3) for t in times], "split_chunks": rt.renderInfo().get("split_chunks", 0)}
+    # the costliest pixel (counting launch with per-pixel stats, RT_PIXEL_STATS): queries and traversal
+    # steps; in a sample-split tile a pixel's samples run as chunk tasks, whose counts add up per pixel
+    # (the seed pass's rounds are reported apart)
+    path = os.path.join(tempfile.gettempdir(), f"tile_stats_{os.getpid()}.bin")
     for n, r in ((1, 0), (8, 0), (8, 1)):
+        tile = (args.stripe, n, r) if n > 1 else None
+        os.environ["RT_PIXEL_STATS"] = path
         rt.setCounting(True)
-        rt.rayTrace(out, W, H, 0, kernel=2, tile=(args.stripe, n, r) if n > 1 else None)
+        rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
         c = rt.counters()
+        info = rt.renderInfo()
         rt.setCounting(False)
-        px = W * (H if n == 1 else len(range(0, H)) // n)
-        res.setdefault("pixel", {})[f"{n}:{r}"] = {
-            "kernel_ms": rt.lastKernelMs(), "max_pixel_ms_at_2.4GHz": c["pixel_clocks_max"] / 2.4e6,
-            "max_pixel_rays": c["pixel_rays_max"], "max_pixel_steps": c["pixel_steps_max"],
-            "mean_pixel_rays": (c["rays_closest"] + c["rays_shadow"]) / px}
+        os.environ.pop("RT_PIXEL_STATS")
+        rows = rt._lib.rt_tile_rows(H, ctypes.byref(pt._abi.RtTile(*tile)) if tile else None)
+        st = np.fromfile(path, np.uint32).reshape(rows * W, 8).astype(np.int64)
+        os.remove(path)
+        split = info.get("split_chunks", 0) > 0
+        q, steps = (st[:, 5], st[:, 6]) if split else (st[:, 2], st[:, 3])
+        px = rows * W
+        e = {"kernel_ms": rt.lastKernelMs(), "split": split, "max_pixel_rays": int(q.max()),
+             "max_pixel_steps": int(steps.max()), "mean_pixel_rays": (c["rays_closest"] + c["rays_shadow"]) / px}
+        if split:
+            e["max_seed_pass_rounds"] = int(st[:, 2].max())
+            e["long_chains"] = int(info.get("pixels_long", 0))
+        else:
+            e["max_pixel_ms_at_2.4GHz"] = c["pixel_clocks_max"] / 2.4e6
+        res.setdefault("pixel", {})[f"{n}:{r}"] = e
     full = res[1]["max_ms"]
     for n in (2, 4, 8):
         res[n]["ideal_ms"] = full / n

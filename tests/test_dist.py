@@ -265,3 +265,47 @@ def test_native_comm_render_block_plan_replay(pt, n, H, hpad, stripe):
         halo.commit(shift)
         np.testing.assert_array_equal(writer, halo.writer)
     assert moved > 0
+
+
+# ---- NativeComm.from_torch: the ranks agree before ncclCommInitRank ------------
+
+def _from_torch_worker(rank, world, port, mode, result_path):
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import ptload
+
+    pdist = ptload.submodule("dist")
+    made = []
+
+    def fake_init(self, n_ranks, r, device, uid):  # stands in for rt_comm_create (RCCL needs GPUs)
+        made.append((n_ranks, r, device, len(uid)))
+
+    pdist.NativeComm.__init__ = fake_init
+    if mode == "ok":
+        pdist.NativeComm.unique_id = staticmethod(lambda: bytes(range(128)))
+    else:  # rank 0 cannot make the id: every rank must raise, none may wait in a collective
+        def boom():
+            raise RuntimeError("no id")
+        pdist.NativeComm.unique_id = staticmethod(boom)
+    try:
+        pdist.NativeComm.from_torch(0)
+        res = "made" if made == [(world, rank, 0, 128)] else f"bad {made}"
+    except RuntimeError as e:
+        res = "raised" if not made and "not created on any rank" in str(e) else f"bad {e}"
+    dist.barrier()  # every rank got here: nobody is stuck in a collective
+    with open(f"{result_path}.{rank}", "w") as f:
+        f.write(res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,want", [("ok", "made"), ("fail", "raised")])
+def test_native_comm_from_torch_agrees_before_init(mode, want, tmp_path, pt):
+    world = 3
+    rp = tmp_path / "res"
+    mp.spawn(_from_torch_worker, args=(world, _free_port(), mode, str(rp)), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"res.{r}").read_text() == want

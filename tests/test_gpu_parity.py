@@ -640,7 +640,26 @@ def test_dragon_headline_config_vs_oracle(tracer, pt, oracle):
     assert out.reshape(-1, 4)[pix, :3].max() > 0
 
 
-def test_lucy_class_28m_tris(tracer, pt, oracle):
+@pytest.fixture(scope="module")
+def lucy_mesh(pt):
+    """BASELINE config 5's mesh (Lucy class, 28,055,742 triangles), made once per module."""
+    return pt.scenes.make_mesh(pt.scenes.MESH_CONFIGS["lucy"])
+
+
+@pytest.fixture(scope="module")
+def lucy_culled(pt, tracer, lucy_mesh):
+    """A context with the Lucy-class mesh on the default (host SAH) builder's tree."""
+    verts, idx = lucy_mesh
+    rt = pt.RayTracer(0)
+    rt.setSpheres(pt.scenes.ply_scene())
+    rt.setMaxPathDepth(6)
+    rt.setBuilder("host")
+    rt.setMesh(verts, idx)
+    yield rt
+    rt.close()
+
+
+def test_lucy_class_28m_tris(tracer, pt, oracle, lucy_mesh, lucy_culled):
     """BASELINE config 5's mesh (Lucy class, 28,055,742 triangles) at reduced resolution.
     Under the reference's absolute |det| < 1e-4 rule (geometryFuncs.h:167) no unit ray can
     accept any of its triangles, so the host build's tree holds almost none of them
@@ -648,29 +667,26 @@ def test_lucy_class_28m_tris(tracer, pt, oracle):
     a pixel subset equals the oracle's linear loop over all 28M triangles; and on the full
     28M tree, rays long enough to pass the det rule hit real triangles with BVH == linear."""
     sc = pt.scenes
+    verts, idx = lucy_mesh
     n = sc.MESH_CONFIGS["lucy"]
-    verts, idx = sc.make_mesh(n)
     S = sc.ply_scene()
     W, H = 192, 144
     Wp, Hp = sc.padded_dims(W, H)
     cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
     seeds = sc.default_seeds(Wp, Hp, skip=11)
 
-    def make(builder):
-        rt = pt.RayTracer(0)
-        rt.setSpheres(S)
-        rt.setCamera(cam)
-        rt.setMaxPathDepth(6)
-        rt.setBuilder(builder)
-        rt.setMesh(verts, idx)
-        return rt
-
-    culled, full = make("host"), make("gpu")
+    culled = lucy_culled
+    full = pt.RayTracer(0)
+    full.setSpheres(S)
+    full.setMaxPathDepth(6)
+    full.setBuilder("gpu")
+    full.setMesh(verts, idx)
     try:
         assert culled.meshInfo()["n_tris_tree"] < 16
         assert full.meshInfo()["n_tris_tree"] == n
         frames = []
         for rt in (culled, full):
+            rt.setCamera(cam)
             rt.setSampleRate(4)
             rt.setSeeds(Wp, Hp, seeds)
             f = np.zeros(W * H * 4, np.float32)
@@ -716,8 +732,71 @@ def test_lucy_class_28m_tris(tracer, pt, oracle):
         np.testing.assert_array_equal(oh[0], exp_h[0][:64])
         np.testing.assert_array_equal(bits(oh[1]), bits(exp_h[1][:64]))
     finally:
-        culled.close()
         full.close()
+
+
+def test_lucy_config5_at_size_eight_tiles(tracer, pt, oracle, lucy_mesh, lucy_culled):
+    """BASELINE config 5 at its own size: the Lucy-class mesh (28,055,742 triangles), 4096x4096,
+    sampleRate 4, as the 8 row-stripe tiles of an 8-GPU run (stripe 8; RayTracerCL.cpp:217-307 over
+    raytracer.cl:184-243, sharded).  The whole frame is finite, alpha 0 and advances every seed;
+    the 8 tiles, each rendered from the same seeds into a device tile and scattered by the root's
+    device assembly (rt_assemble_tiles, the last step of rt_comm_gather_frame), equal the whole
+    frame bit for bit, and so do the seed planes after them; a strided pixel subset rendered at
+    sampleRate 1 equals the oracle's linear loop over all 28M triangles, frames and seeds."""
+    import torch
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    sc = pt.scenes
+    verts, idx = lucy_mesh
+    S = sc.ply_scene()
+    W = H = 4096
+    n_ranks, stripe = 8, 8
+    Wp, Hp = sc.padded_dims(W, H)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=13)
+    rt = lucy_culled
+    rt.setCamera(cam)
+    rt.setSampleRate(4)
+    rt.setSeeds(Wp, Hp, seeds)
+    dev = torch.device("cuda", 0)
+    whole = torch.zeros(W * H * 4, dtype=torch.float32, device=dev)
+    rt.rayTrace(whole, W, H, 0, kernel=2)
+    s_whole = rt.getSeeds()
+    img = whole.cpu().numpy()
+    f = img.reshape(H, W, 4)
+    assert np.isfinite(f).all() and (f[..., 3] == 0).all() and f[..., :3].max() > 0
+    changed = (s_whole.reshape(2, Hp, Wp)[:, :H, :W] != seeds.reshape(2, Hp, Wp)[:, :H, :W]).any(0)
+    assert changed.all()
+    del f
+    # the 8 ranks' tiles on one GPU: tiles own disjoint rows and read / write only their own seed
+    # slots (raytrace_tris: unshifted y * Wpad + x), so rendering them in turn from the same
+    # starting planes is what 8 GPUs with replicated seeds do
+    rt.setSeeds(Wp, Hp, seeds)
+    rows_max = dist.max_tile_rows(H, stripe, n_ranks)
+    tiles = []
+    for r in range(n_ranks):
+        t = torch.zeros(rows_max * W * 4, dtype=torch.float32, device=dev)
+        rt.rayTrace(t, W, H, 0, kernel=2, tile=(stripe, n_ranks, r))
+        tiles.append(t)
+    s_tiles = rt.getSeeds()
+    frame = torch.full((W * H * 4,), -1.0, dtype=torch.float32, device=dev)
+    dist.assemble_native(tiles, H, W, stripe, frame, device=0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(bits(frame.cpu().numpy()), bits(img))
+    np.testing.assert_array_equal(s_tiles, s_whole)
+    del tiles, frame, whole, img
+    # oracle subset at sampleRate 1 (the oracle walks all 28M triangles per ray)
+    rt.setSampleRate(1)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    rt.rayTrace(got, W, H, 0, kernel=2, tile=None)
+    pix = np.arange(1_234, W * H, W * H // 24, dtype=np.uint32)
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, 1, 6, 0, sd, verts, idx, pixels=pix)
+    np.testing.assert_array_equal(bits(got.reshape(-1, 4)[pix]), bits(exp.reshape(-1, 4)[pix]))
+    np.testing.assert_array_equal(_pixel_seeds(rt.getSeeds(), pix, Wp, Hp, W), _pixel_seeds(sd, pix, Wp, Hp, W))
 
 
 @pytest.mark.parametrize("kernel", [0, 2])
@@ -1046,7 +1125,11 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
     sd = seeds.copy()
     for p in range(2):
         rt.rayTrace(got, W, H, p, kernel=2)
-        assert rt.renderInfo()["split_chunks"] == (spp + csz - 1) // csz
+        info = rt.renderInfo()
+        assert info["split_chunks"] == (spp + csz - 1) // csz
+        # the long chains ran on their own stream with the 4-lane cooperative seed pass (coop_round)
+        assert info["pixels_long"] > 0 and info["split_coop"] == 4 and info["split_guard"] == 0, info
+        assert len(rt.longChains()) == info["pixels_long"]
         oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, p, sd, verts, idx)
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
         np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg=f"seeds after frame {p}")
@@ -1058,7 +1141,8 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
     rt.setSeeds(Wp, Hp, seeds)
     got = np.zeros(len(rows) * W * 4, np.float32)
     rt.rayTrace(got, W, H, 0, kernel=2, tile=tile)
-    assert rt.renderInfo()["split_chunks"] > 0
+    info = rt.renderInfo()
+    assert info["split_chunks"] > 0 and info["pixels_long"] > 0 and info["split_coop"] == 4, info
     np.testing.assert_array_equal(bits(got), bits(exp.reshape(H, W, 4)[rows].reshape(-1)), err_msg="tile")
     np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg="tile seeds")
     rt.close()
@@ -1350,3 +1434,44 @@ def test_sample_split_at_full_size(tracer, pt, monkeypatch):
         rt.close()
     np.testing.assert_array_equal(res["1"][0], res["0"][0])
     np.testing.assert_array_equal(res["1"][1], res["0"][1])
+
+
+def test_long_chains_of_the_8way_dragon_tile_vs_oracle(tracer, pt, oracle):
+    """The 8-way row-stripe tile of the headline frame (dragon class, 1920x1080, sampleRate 16 =
+    256 spp, maxDepth 6; tile (8, 8, 3): 1 of the 8 ranks of BASELINE's 8-GPU case): a
+    sample-split render whose long chains (box pixels and costly mesh pixels) take the 4-lane
+    cooperative seed pass (coop_round, existence queries) on the second stream.  16 of those
+    pixels, spread over the list, equal the oracle's linear loop bit for bit — radiance and both
+    seed words (raytracer.cl:205-242, rtcommon.h:371-470) — so the pass that bounds N = 8 is
+    pinned against the reference's algorithm at the configuration it serves."""
+    sc = pt.scenes
+    W, H, sr = 1920, 1080, 16
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    seeds = sc.default_seeds(Wp, Hp, skip=9)
+    stripe, n_ranks, rank = 8, 8, 3
+    rows = np.arange(H)[(np.arange(H) // stripe) % n_ranks == rank]
+    rt = tracer
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(len(rows) * W * 4, np.float32)
+    rt.rayTrace(got, W, H, 0, kernel=2, tile=(stripe, n_ranks, rank))
+    info = rt.renderInfo()
+    assert info["split_chunks"] == 16 and info["split_coop"] == 4 and info["split_guard"] == 0, info
+    long_px = rt.longChains()
+    assert len(long_px) == info["pixels_long"] and len(long_px) >= 1000, len(long_px)
+    pick = long_px[np.linspace(0, len(long_px) - 1, 16).astype(np.int64)]
+    yl, x = pick // W, pick % W
+    gpix = (rows[yl] * W + x).astype(np.uint32)  # the tile's local rows -> frame rows
+    exp = np.zeros(W * H * 4, np.float32)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=gpix)
+    np.testing.assert_array_equal(bits(got.reshape(-1, 4)[pick]), bits(exp.reshape(-1, 4)[gpix]))
+    np.testing.assert_array_equal(_pixel_seeds(rt.getSeeds(), gpix, Wp, Hp, W), _pixel_seeds(sd, gpix, Wp, Hp, W))
+    assert got.reshape(-1, 4)[pick, :3].max() > 0

@@ -720,7 +720,7 @@ __device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
    stack stays inside the group's RT_COOP_STACK words. */
 __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
                                            CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
-                                           uint32_t n_nodes, uint32_t n_recs, int multi_sp, uint32_t &defect)
+                                           uint32_t n_nodes, uint32_t n_recs, int multi_sp, unsigned long long *guard)
 {
     const int lane = (int)(threadIdx.x & 63), sub = lane & 3, gbase = lane & ~3;
     if (q.sp <= 0) return true;
@@ -759,7 +759,7 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
        and is reported (the render then fails: rt_synchronize) */
     const bool bad = act && (leaf ? slot >= n_recs : (uint32_t)item >= n_nodes);
     if ((__ballot(bad) >> gbase) & 15ull) {
-        defect |= RT_GUARD_INDEX;
+        if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_INDEX); /* rare path: no register carried */
         return true;
     }
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -826,7 +826,7 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     const int above = (sub < 1 ? h1 : 0) + (sub < 2 ? h2 : 0) + (sub < 3 ? h3 : 0);
     const int sp = q.sp - nfull;
     if (sp + total > CoopStack::kCap) { /* cannot happen (multi_sp bound, rt_host.cpp): reported, not clamped */
-        defect |= RT_GUARD_STACK;
+        if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_STACK);
         return true;
     }
 #pragma unroll
@@ -885,7 +885,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     coop_begin(cq, qo, qd, kInf);
     uint32_t st_steps = 0, st_box = 0, st_t0 = 0; /* diagnostics (RT_PIXEL_STATS): per pixel */
     uint32_t q_steps = 0;                          /* rounds of the current query */
-    uint32_t defect = 0;                           /* RT_GUARD_* that fired in this lane's queries */
+    unsigned long long *const guard = a.counters + RT_CNT_GUARD; /* RT_GUARD_* flags (rt_synchronize) */
     for (;;) {
         /* lanes (COOP: groups) without a pixel take the next ones of the queue */
         /* takers: the first split_gpw lanes (COOP: 4-lane groups) of the wave */
@@ -930,12 +930,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
             }
         }
         if (!__any(have)) {
-            if (drained) {
-                /* a guard that fired anywhere in the wave is reported once (rt_synchronize fails the render) */
-                const unsigned long long bad = __ballot(defect != 0);
-                if (bad && lane == __ffsll((long long)bad) - 1) atomicOr(&a.counters[RT_CNT_GUARD], (unsigned long long)defect);
-                break;
-            }
+            if (drained) break;
             continue;
         }
         /* a new sample: the chunk's first seed, then the camera ray and its query */
@@ -1008,7 +1003,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 bool done;
                 if constexpr (G == 4) {
                     done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, a.coop_multi_sp,
-                                      defect);
+                                      guard);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
                     done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
@@ -1019,7 +1014,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 const bool exists = RT_SEED_EXISTS && (COOP ? cq.best : ts.best) >= 0;
                 /* a query never takes 2^14 rounds (a ray meets far fewer nodes than that):
                    a bound every wave reaches, whatever a defect would do to a stack (reported) */
-                if (q_steps > (1u << 14)) defect |= RT_GUARD_ROUNDS;
+                if (q_steps > (1u << 14)) atomicOr(guard, (unsigned long long)RT_GUARD_ROUNDS);
                 if (done || exists || q_steps > (1u << 14)) {
                     running = false;
                     fin = true;

@@ -836,6 +836,41 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     return q.sp == 0;
 }
 
+#ifndef RT_SEED_ROOT
+#define RT_SEED_ROOT 1 /* cooperative seed-pass queries start from the root's child boxes, tested in registers */
+#endif
+#ifndef RT_SEED_REC
+#define RT_SEED_REC 1 /* one-lane seed pass: a camera ray tests its list's first record in the path advance */
+#endif
+#ifndef RT_SEED_IMM
+#define RT_SEED_IMM 3 /* path-advance passes per seed-pass iteration (queries answered at once chain) */
+#endif
+
+/* A cooperative query of the tree starts at the root's children: the root node (uniform, loaded
+   once per wave into registers) is tested in the path advance instead of in a stepping round of
+   its own, and the hit children go on the group's stack, nearest on top.  Returns false when no
+   child box is hit (or the determinant cull rules the tree out): no mesh hit, without a round.
+   Culling only: the same children coop_round would push from the root. */
+__device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3, CoopQuery &q, const CoopStack &gst, V3 d,
+                                          bool writer)
+{
+    if (!RT_SEED_ROOT) {
+        if (writer) gst[0] = 0;
+        q.sp = 1;
+        return true;
+    }
+    float t[4];
+    int c[4];
+    const int nh = node_children(r0, r1, r2, r3, q.inv, q.oi, d, q.best_t, false, false, t, c);
+    if (writer) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (i < nh) gst[nh - 1 - i] = c[i];
+    }
+    q.sp = nh;
+    return nh > 0;
+}
+
 /* Sample-split tiles, step 1: the seed pass.  A pixel's random numbers depend only on its
    closest hits (trace_path_tri, rtcommon.h:371-468): per surface hit two draws per light
    whatever its shadow ray finds (:88-92), two more for the Lambert bounce off the box (:459);
@@ -860,6 +895,10 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
         for (int k = 0; k < RT_STACK_DEPTH; ++k) s_stack[k * RT_BLOCK + threadIdx.x] = 0;
     const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
+    /* the root node (coop_root): a uniform address, so scalar loads */
+    const uint4 *__restrict__ rootp = reinterpret_cast<const uint4 *>(a.nodes);
+    const uint4 rq0 = COOP ? rootp[0] : uint4{}, rq1 = COOP ? rootp[1] : uint4{}, rq2 = COOP ? rootp[2] : uint4{},
+                rq3 = COOP ? rootp[3] : uint4{};
     const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
@@ -933,64 +972,154 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
             if (drained) break;
             continue;
         }
-        /* a new sample: the chunk's first seed, then the camera ray and its query */
-        if (next) {
-            next = false;
-            if ((sample == spp || sample % fine == 0u) && lane == gbase) {
-                const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
-                reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
-            }
-            if (sample == spp) {
-                have = false;
-                if (a.pixel_stats && lane == gbase) {
-                    uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
-                    ps[0] = st_t0;
-                    ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                    ps[2] = st_steps;
-                    ps[3] = st_box;
-                    ps[4] = 1u + (uint32_t)a.split_which;
+        /* The path advance, over as many segments and samples as it takes before the next stepping
+           round: a new sample's camera ray, and every query answered without a round — an empty
+           candidate list, a mesh pixel's camera ray accepted by the first record of its list (loaded
+           before the ray is formed: RT_SEED_REC), a box bounce whose ray misses the root's child boxes (tested from
+           registers: RT_SEED_ROOT) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly leave the mesh's box
+           alone, so a long chain's samples are mostly resolved here, without a memory round trip. */
+        for (int pass = 0;; ++pass) {
+            /* a new sample: the chunk's first seed, then the camera ray and its query */
+            if (next) {
+                next = false;
+                if ((sample == spp || sample % fine == 0u) && lane == gbase) {
+                    const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
                 }
-            } else {
-                const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
-                const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
-                const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
-                const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
-                qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
-                qd = camera_dir(a.cam, fa - hw, fb - hh);
-                depth = 0;
-                if (COOP) coop_begin(cq, qo, qd, kInf);
-                else trav_begin(ts, stk, qo, qd, kInf);
-                q_steps = 0;
-                running = true;
-                { /* the pixel's candidate list, as k_tris takes it */
-                    const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
-                    if (lpack == RT_LPACK_EMPTY) {
-                        running = false;
-                        ts.best = -1;
-                        cq.best = -1;
-                        fin = true;
-                    } else if (lpack != RT_LPACK_NONE) {
-                        for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
-                            const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
-                            const int v = ~(int)(((first + 8u * b) << 3) | (k - 1u));
-                            if (COOP) {
-                                if (lane == gbase) gst[cq.sp] = v;
-                                ++cq.sp;
-                            } else {
-                                stk.push(v);
+                if (sample == spp) {
+                    have = false;
+                    if (a.pixel_stats && lane == gbase) {
+                        uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
+                        ps[0] = st_t0;
+                        ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        ps[2] = st_steps;
+                        ps[3] = st_box;
+                        ps[4] = 1u + (uint32_t)a.split_which;
+                    }
+                } else {
+                    /* the list's first record (the earliest possible accept t), loaded before the
+                       camera ray is formed so that its latency hides behind that arithmetic */
+                    float4 ra = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rb = ra, rc = ra;
+                    const bool has_list = lpack < RT_LPACK_EMPTY;
+                    if (!COOP && RT_SEED_REC && has_list) {
+                        const uint32_t f0 = (lpack >> RT_LIST_BITS) << 3;
+                        ra = tris[3 * f0];
+                        rb = tris[3 * f0 + 1];
+                        rc = tris[3 * f0 + 2];
+                    }
+                    const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
+                    const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
+                    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                    const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
+                    qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+                    qd = camera_dir(a.cam, fa - hw, fb - hh);
+                    depth = 0;
+                    if (COOP) coop_begin(cq, qo, qd, kInf);
+                    else trav_begin(ts, stk, qo, qd, kInf);
+                    q_steps = 0;
+                    running = true;
+                    { /* the pixel's candidate list, as k_tris takes it */
+                        const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
+                        if (lpack == RT_LPACK_EMPTY) {
+                            running = false;
+                            ts.best = -1;
+                            cq.best = -1;
+                            fin = true;
+                        } else if (lpack != RT_LPACK_NONE) {
+                            bool accepted = false;
+                            if (!COOP && RT_SEED_REC) {
+                                /* accepted by the first record (mt_test, t >= tmin): the camera ray hits
+                                   the mesh — all the seed needs */
+                                float t0 = 0.0f;
+                                accepted = mt_test(qo, qd, ra, rb, rc, t0) && !(t0 < RT_SMALL_F);
+                                if (accepted) {
+                                    running = false;
+                                    ts.best = (int)first;
+                                    fin = true;
+                                }
+                            }
+                            if (!accepted) {
+                                for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
+                                    const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
+                                    const int v = ~(int)(((first + 8u * b) << 3) | (k - 1u));
+                                    if (COOP) {
+                                        if (lane == gbase) gst[cq.sp] = v;
+                                        ++cq.sp;
+                                    } else {
+                                        stk.push(v);
+                                    }
+                                }
+                                const int n0 = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
+                                if (COOP) {
+                                    /* coop_round: the list's first block on top */
+                                    if (lane == gbase) gst[cq.sp] = n0;
+                                    ++cq.sp;
+                                } else {
+                                    ts.node = n0;
+                                }
+                            }
+                        } else if (COOP) { /* no list: the tree, from the root's children */
+                            if (!coop_root(rq0, rq1, rq2, rq3, cq, gst, qd, lane == gbase)) {
+                                running = false;
+                                fin = true;
                             }
                         }
-                        const int n0 = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
-                        if (COOP) cq.node = n0;
-                        else ts.node = n0;
                     }
                 }
-                /* coop_round: the query's first entry (the root, or the list's first block) on top */
-                if (COOP && running) {
-                    if (lane == gbase) gst[cq.sp] = cq.node;
-                    ++cq.sp;
+            }
+            /* lanes whose query completed: the segment's draws, then the bounce or the next sample */
+            if (fin) {
+                fin = false;
+                bool sample_done = true;
+                if ((COOP ? cq.best : ts.best) >= 0) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
+                    for (uint32_t l = 0; l < nl; ++l) {
+                        (void)frand(seed);
+                        (void)frand(seed);
+                    }
+                } else { /* the enclosing box (rtcommon.h:425-466) */
+                    const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
+                    if (depth == 0) ++st_box;
+                    if (hd > RT_SMALL_F && hd < kInf) {
+                        const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
+                        const V3 hn = box_normal(hp, bw, bh, bw);
+                        for (uint32_t l = 0; l < nl; ++l) {
+                            (void)frand(seed);
+                            (void)frand(seed);
+                        }
+                        const float r1 = frand(seed);
+                        const float r2 = frand(seed);
+                        const float ct = rt_sqrtf(1.0f - r1);
+                        const float st = rt_sqrtf(1.0f - ct * ct);
+                        const float phi = RT_M_2PI_F * r2;
+                        float sphi, cphi;
+                        rt_sincosf(phi, &sphi, &cphi);
+                        qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
+                        qo = hp;
+                        ++depth;
+                        if (depth <= a.max_depth) {
+                            sample_done = false;
+                            q_steps = 0;
+                            running = true;
+                            if (COOP) {
+                                coop_begin(cq, qo, qd, kInf);
+                                if (!coop_root(rq0, rq1, rq2, rq3, cq, gst, qd, lane == gbase)) {
+                                    running = false; /* misses the mesh's box: no mesh hit, at once */
+                                    fin = true;
+                                }
+                            } else {
+                                trav_begin(ts, stk, qo, qd, kInf);
+                            }
+                        }
+                    }
+                }
+                if (sample_done) {
+                    ++sample;
+                    next = true;
                 }
             }
+            /* at most RT_SEED_IMM passes before the next stepping round: the lanes whose queries
+               need a traversal must not wait long for those whose answers come at once */
+            if (pass + 1 >= RT_SEED_IMM || !__any(next || fin)) break;
         }
         /* step the running queries (the box pixels' chains at top priority: they run beside the
            chunk tasks and set when the box pixels' chunks can start) */
@@ -1019,54 +1148,6 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                     running = false;
                     fin = true;
                 }
-            }
-        }
-        /* lanes whose query completed: the segment's draws, then the bounce or the next sample */
-        if (fin) {
-            fin = false;
-            bool sample_done = true;
-            if ((COOP ? cq.best : ts.best) >= 0) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
-                for (uint32_t l = 0; l < nl; ++l) {
-                    (void)frand(seed);
-                    (void)frand(seed);
-                }
-            } else { /* the enclosing box (rtcommon.h:425-466) */
-                const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
-                if (depth == 0) ++st_box;
-                if (hd > RT_SMALL_F && hd < kInf) {
-                    const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
-                    const V3 hn = box_normal(hp, bw, bh, bw);
-                    for (uint32_t l = 0; l < nl; ++l) {
-                        (void)frand(seed);
-                        (void)frand(seed);
-                    }
-                    const float r1 = frand(seed);
-                    const float r2 = frand(seed);
-                    const float ct = rt_sqrtf(1.0f - r1);
-                    const float st = rt_sqrtf(1.0f - ct * ct);
-                    const float phi = RT_M_2PI_F * r2;
-                    float sphi, cphi;
-                    rt_sincosf(phi, &sphi, &cphi);
-                    qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
-                    qo = hp;
-                    ++depth;
-                    if (depth <= a.max_depth) {
-                        sample_done = false;
-                        if (COOP) {
-                            coop_begin(cq, qo, qd, kInf);
-                            if (lane == gbase) gst[0] = 0; /* the root on the group's stack */
-                            cq.sp = 1;
-                        } else {
-                            trav_begin(ts, stk, qo, qd, kInf);
-                        }
-                        q_steps = 0;
-                        running = true;
-                    }
-                }
-            }
-            if (sample_done) {
-                ++sample;
-                next = true;
             }
         }
     }

@@ -4,7 +4,7 @@ Every library gets its own RayTracer context (same mesh, camera, seeds); launche
 alternate between the libraries round after round, so clock and neighbour drift
 hit all variants alike.  Prints per-variant median / min kernel ms.
 
-    python profiles/ab_inproc.py LABEL=path.so LABEL=path.so ... [--rounds 8] [--config dragon]
+    python profiles/ab_inproc.py LABEL=path.so LABEL=path.so ... [--rounds 8] [--config dragon] [--tile 8,8,0]
     (LABEL= with an empty path: the in-tree build)
 """
 from __future__ import annotations
@@ -23,7 +23,9 @@ def main():
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--config", default="dragon", choices=["dragon", "bunny", "lucy"])
+    ap.add_argument("--tile", default=None, help="stripe,n_ranks,rank: time one rank's row-stripe tile")
     args = ap.parse_args()
+    tile = tuple(int(v) for v in args.tile.replace(":", ",").split(",")) if args.tile else None
     import numpy as np
     import torch
     import ptload
@@ -53,7 +55,7 @@ def main():
         k = r % len(variants)  # rotate the order every round (no variant always first)
         for label, rt, ms in variants[k:] + variants[:k]:
             rt.setSeeds(Wp, Hp, seeds)
-            rt.rayTrace(out, W, H, 0, kernel=pt.RayTracer.KERNEL_TRIS)
+            rt.rayTrace(out, W, H, 0, kernel=pt.RayTracer.KERNEL_TRIS, tile=tile)
             torch.cuda.synchronize()
             if r == 0:  # warmup round; every variant's frame must be the same bits
                 img = out.cpu().numpy().view(np.uint32).copy()
@@ -65,7 +67,7 @@ def main():
                 # the main kernel alone (k_tris + deferred-shadow kernels): builds that reuse the
                 # candidate lists of an unchanged view skip the pre-pass, older builds do not
                 try:
-                    ms.append(rt.lastKernelSplitMs()[1])
+                    ms.append(rt.lastKernelSplitMs()[1] if tile is None else rt.lastKernelMs())
                 except Exception:
                     ms.append(rt.lastKernelMs())
         if r > 0:

@@ -31,7 +31,7 @@ def main():
     rt.setSampleRate(sr)
     rt.setMaxPathDepth(6)
     rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS[args.config]))
-    tile = tuple(int(v) for v in args.tile.split(",")) if args.tile else None
+    tile = tuple(int(v) for v in args.tile.replace(":", ",").split(",")) if args.tile else None
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     for _ in range(args.reps):
         rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)

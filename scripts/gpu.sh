@@ -14,6 +14,8 @@
 #   tiles[=<args>]             profiles/tile_scaling.py <args>               -> tiles[_<n>].json / .log
 #   ab=<args>                  profiles/ab_inproc.py <args> (in-process A/B of library builds) -> ab[_<n>].txt
 #   py=<script>[,<args>]       python <script> <args>                        -> py_<n>.log
+#   trace=<args>               rocprofv3 kernel trace of profiles/render_tile.py <args> -> trace_<n>/ + trace_<n>.txt
+#                              (profiles/tile_trace.py: per-kernel spans of the last render)
 # Example: bash scripts/gpu.sh r04a tests smoke bench bench=--config,bunny tiles=--config,dragon
 set -o pipefail
 TAG=${1:?usage: scripts/gpu.sh <tag> <step>...}
@@ -51,6 +53,10 @@ for step in "$@"; do
         timeout -k 10 900 python -u profiles/ab_inproc.py $args > "$OUT/ab_$n.txt" 2>&1 ;;
     py)
         timeout -k 10 600 python -u $args > "$OUT/py_$n.log" 2>&1 ;;
+    trace)
+        timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_$n" -o run -- \
+            python3 profiles/render_tile.py $args > "$OUT/trace_$n.log" 2>&1 &&
+            python3 profiles/tile_trace.py "$OUT/trace_$n" > "$OUT/trace_$n.txt" ;;
     *)
         echo "[gpu.sh] unknown step '$step'" >&2
         exit 2 ;;

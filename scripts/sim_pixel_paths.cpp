@@ -36,6 +36,7 @@ static long g_node_steps, g_tri_steps; /* of all queries */
 static long g_near[2], g_far[2];         /* shadow-query steps entered within / beyond t = 0.05 (node, tri) */
 static bool g_track;
 static bool g_from_mesh; /* the shadow query leaves a mesh hit */
+static bool g_backface; /* ... a back face (the closest-hit ray met the triangle from behind) */
 static float g_tmin_shadow = -1e-3f; /* experiment: node-cull tmin of shadow rays leaving the mesh */
 static double g_occ[2], g_occ_steps[2]; /* camera-hit shadow queries: unoccluded / occluded, and their steps */
 static int g_order = 0; /* 0 sorted push, 1 nearest first only, 2 sorted with any-hit origin boxes last, 3 and those by segment length, 5 = 3 for shadow rays leaving the mesh else 2 (k_tris) */
@@ -171,9 +172,19 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
             if (g_order >= 2 && any) { /* any-hit: children holding the origin visited last */
                 It key[4];
                 for (int j = 0; j < k; ++j) {
-                    const bool longest = g_order == 3 || (g_order == 5 && g_from_mesh);
+                    const bool longest = g_order == 3 || (g_order == 5 && g_from_mesh) ||
+                                         (g_order == 8 && g_from_mesh && !g_backface);
                     float kk = longest ? -(bt[j] - buf[j].tn) : g_order == 4 ? -buf[j].tn : buf[j].tn;
-                    key[j] = {buf[j].c, buf[j].tn <= -1e-3f ? kk + 1e4f : kk};
+                    /* 6: far exit first, 7: far entry first (shadow rays leaving the mesh); 8: far exit
+                       first for those leaving a back face (the origin inside the closed surface) */
+                    if (g_from_mesh && (g_order == 6 || (g_order == 8 && g_backface))) kk = -bt[j];
+                    if (g_from_mesh && g_order == 7) kk = -buf[j].tn;
+                    bool origin_last = buf[j].tn <= -1e-3f;
+                    /* 9: nearest entry first for rays leaving the mesh, origin boxes not postponed;
+                       10: nearest exit first for them */
+                    if (g_from_mesh && g_order == 9) kk = buf[j].tn, origin_last = false;
+                    if (g_from_mesh && g_order == 10) kk = bt[j], origin_last = false;
+                    key[j] = {buf[j].c, origin_last ? kk + 1e4f : kk};
                 }
                 std::sort(key, key + k, [](const It &a, const It &b) { return a.tn > b.tn; });
                 for (int j = 0; j < k; ++j) buf[j] = {key[j].c, 0.0f};
@@ -201,6 +212,7 @@ static long query(V o, V d, float tmax, bool any, float &t_hit, int &hit)
                     if (any) {
                         if (t > 1e-4f && t < tmax) {
                             hit = first + j;
+                            t_hit = t;
                             return steps;
                         }
                     } else if (!(t < 1e-4f) && t < best) {

@@ -79,6 +79,9 @@ uint32_t probe_n(uint32_t sample_rate) { return sample_rate >= 2 ? kProbeN : 1u;
 #ifndef RT_FETCH_K
 #define RT_FETCH_K 24
 #endif
+#ifndef RT_SEED_GRID_ITEMS
+#define RT_SEED_GRID_ITEMS 1
+#endif
 constexpr uint32_t kFetchK = RT_FETCH_K;
 constexpr uint32_t kFetchFrac = 24;
 
@@ -1014,7 +1017,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
            its own part of the area) */
         a.spill_cap = spill_cap(c);
         if (a.spill_cap) {
-            const int rs = ensure_spill(c, (size_t)std::max(blocks, blocks_split) * 2 * RT_BLOCK * a.spill_cap);
+            const int rs = ensure_spill(c, (size_t)std::max<uint64_t>(std::max(blocks, blocks_split), item_blocks) * 2 *
+                                               RT_BLOCK * a.spill_cap);
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
@@ -1081,7 +1085,10 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                    the mesh pixels' kernels, whose grids leave room for it */
                 const int box_blocks = c->n_split_box ? split_box_blocks(c, std::max(1u, a.split_coop), blocks) : 0;
                 c->split_box_grid = box_blocks;
+                /* the mesh pixels' seed pass: at least one lane per queue item (RT_SEED_GRID_ITEMS), so no lane
+                   walks two pixels' chains in turn (the blocks beyond residency start as others end) */
                 a.split_seed_blocks = (uint32_t)std::max(1, blocks - box_blocks);
+                if (RT_SEED_GRID_ITEMS) a.split_seed_blocks = (uint32_t)std::max<uint64_t>(a.split_seed_blocks, item_blocks);
                 blocks = std::max(1, std::min((int)std::min<uint64_t>((uint64_t)blocks_split, item_blocks * nch),
                                               blocks_split - box_blocks));
             }

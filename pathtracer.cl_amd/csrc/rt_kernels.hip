@@ -836,14 +836,24 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     return q.sp == 0;
 }
 
+#ifndef RT_COOP_SPLIT
+#define RT_COOP_SPLIT 1 /* cooperative seed-pass rounds: one stack item shared by the 4 lanes (coop_round2) */
+#endif
+
 #ifndef RT_SEED_ROOT
 #define RT_SEED_ROOT 1 /* cooperative seed-pass queries start from the root's child boxes, tested in registers */
 #endif
 #ifndef RT_SEED_REC
 #define RT_SEED_REC 1 /* one-lane seed pass: a camera ray tests its list's first record in the path advance */
 #endif
+#ifndef RT_SEED_STATS
+#define RT_SEED_STATS 0 /* diagnostics builds: per-pixel query / immediate-answer / iteration counts (RT_PIXEL_STATS) */
+#endif
+#ifndef RT_SEED_FAST
+#define RT_SEED_FAST 8 /* one-lane seed pass: samples finished in a row in the new-sample step (first list record) */
+#endif
 #ifndef RT_SEED_IMM
-#define RT_SEED_IMM 3 /* path-advance passes per seed-pass iteration (queries answered at once chain) */
+#define RT_SEED_IMM 2 /* path-advance passes per seed-pass iteration (queries answered at once chain) */
 #endif
 
 /* A cooperative query of the tree starts at the root's children: the root node (uniform, loaded
@@ -855,6 +865,11 @@ __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
                                           bool writer)
 {
     if (!RT_SEED_ROOT) {
+        if (RT_COOP_SPLIT) {
+            q.node = 0;
+            q.sp = 0;
+            return true;
+        }
         if (writer) gst[0] = 0;
         q.sp = 1;
         return true;
@@ -862,6 +877,16 @@ __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
     float t[4];
     int c[4];
     const int nh = node_children(r0, r1, r2, r3, q.inv, q.oi, d, q.best_t, false, false, t, c);
+    if (RT_COOP_SPLIT) { /* coop_round2: the nearest is the current item, the others on the stack */
+        if (writer) {
+#pragma unroll
+            for (int i = 1; i < 4; ++i)
+                if (i < nh) gst[nh - 1 - i] = c[i];
+        }
+        q.node = c[0];
+        q.sp = nh > 0 ? nh - 1 : 0;
+        return nh > 0;
+    }
     if (writer) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -869,6 +894,182 @@ __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
     }
     q.sp = nh;
     return nh > 0;
+}
+
+/* The same for a one-lane query (trav_step_q's state): the root's hit children go on the lane's
+   stack, the nearest becomes the next node.  Returns false when none is hit. */
+__device__ __forceinline__ bool lane_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3, TravState &s, Stack &stk, V3 d)
+{
+    if (!RT_SEED_ROOT) return true; /* s.node = 0: the root, in a round */
+    float t[4];
+    int c[4];
+    const int nh = node_children(r0, r1, r2, r3, s.inv, s.oi, d, s.best_t, false, false, t, c);
+    if (nh >= 4) stk.push(c[3]);
+    if (nh >= 3) stk.push(c[2]);
+    if (nh >= 2) stk.push(c[1]);
+    s.node = c[0];
+    return nh > 0;
+}
+
+/* Child `k` (per lane) of a compressed node against the ray: node_children's arithmetic for one
+   child (fma(byte, scale, base): the same bits as its f16-subnormal form), its entry t and whether
+   it is hit.  Culling only. */
+__device__ __forceinline__ bool node_child_k(uint4 q0, uint4 q1, uint4 q2, int k, V3 inv, V3 oi, float best_t, float &tn)
+{
+    const float tmin_c = -1e-3f;
+    const float tmax_c = t_slack(best_t);
+    const uint32_t w = q0.w;
+    const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
+    const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
+    const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
+    const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
+    const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
+    const float bz = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
+    const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+    const uint32_t nxw = px ? q1.x : q1.y, fxw = px ? q1.y : q1.x;
+    const uint32_t nyw = py ? q1.z : q1.w, fyw = py ? q1.w : q1.z;
+    const uint32_t nzw = pz ? q2.x : q2.y, fzw = pz ? q2.y : q2.x;
+    const uint32_t sh = 8u * (uint32_t)k;
+    const float nx = __builtin_fmaf((float)((nxw >> sh) & 0xffu), sx, bx), fx = __builtin_fmaf((float)((fxw >> sh) & 0xffu), sx, bx);
+    const float ny = __builtin_fmaf((float)((nyw >> sh) & 0xffu), sy, by), fy = __builtin_fmaf((float)((fyw >> sh) & 0xffu), sy, by);
+    const float nz = __builtin_fmaf((float)((nzw >> sh) & 0xffu), sz, bz), fz = __builtin_fmaf((float)((fzw >> sh) & 0xffu), sz, bz);
+    tn = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, tmin_c));
+    const float tf = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tmax_c));
+    return tn <= tf; /* an unused slot's inverted box never passes */
+}
+
+/* The node's determinant cull (node_children): false when no triangle below can pass |det| >= 1e-4. */
+__device__ __forceinline__ bool node_det_possible(uint4 q2, V3 d)
+{
+    const bool px = d.x >= 0.0f, py = d.y >= 0.0f, pz = d.z >= 0.0f;
+    const uint32_t nlo = q2.z, nhi = q2.w;
+    const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
+    const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
+    const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
+    const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
+    const float bias = 128.0f * (d.x + d.y + d.z);
+    const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
+                                     __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu), __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
+    const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
+                                     __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu), __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
+    const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
+    const float bound = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
+    return !(bound < 1e-4f);
+}
+
+/* Cooperative closest-hit round, one stack ITEM per round shared by the group's 4 lanes: a node's
+   4 child boxes one per lane (ranked by DPP exchanges, the hits pushed farthest first, the nearest
+   taken next), or up to 4 triangles of a leaf or candidate-list block one per lane (the rest of a
+   longer one stays the next item).  The same tests and accept rule as trav_step_q, depth first and
+   nearest first; about a quarter of coop_round's instructions per round for about a third more
+   rounds per query, and a long chain is its rounds' dependent latency.  q.node is the item. */
+__device__ __forceinline__ bool coop_round2(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                            CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
+                                            uint32_t n_nodes, uint32_t n_recs, unsigned long long *guard)
+{
+    const int sub = (int)(threadIdx.x & 3);
+    const int item = q.node;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    if (item < 0) {
+        const uint32_t enc = ~(uint32_t)item, first = enc >> 3, cnt = (enc & 7u) + 1u;
+        const uint32_t take = cnt < 4u ? cnt : 4u;
+        const bool act = (uint32_t)sub < take;
+        const uint32_t slot = first + (uint32_t)sub;
+        if (first + take > n_recs) { /* every record index is checked: a defect ends the query, reported */
+            if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_INDEX);
+            return true;
+        }
+        v4u w0 = {0u, 0u, 0u, 0u}, w1 = w0, w2 = w0;
+        if (act) {
+            const v4u *vrec = reinterpret_cast<const v4u *>(reinterpret_cast<const uint4 *>(tris) + 3 * slot);
+            w0 = vrec[0];
+            w1 = vrec[1];
+            w2 = vrec[2];
+        }
+        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2));
+        float ct = kInf;
+        int co = -1, cs = -1;
+        if (act) {
+            const float4 ta = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z),
+                                          __uint_as_float(w0.w));
+            const float4 tb = make_float4(__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z), 0.0f);
+            const float4 tc = make_float4(__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z), 0.0f);
+            float tt = 0.0f;
+            const bool h = mt_test(o, d, ta, tb, tc, tt);
+            const int orig = __float_as_int(ta.w);
+            if (h && !(tt < tmin) && (tt < q.best_t || (tt == q.best_t && orig > q.best_orig))) {
+                ct = tt;
+                co = orig;
+                cs = (int)slot;
+            }
+        }
+        /* the group's best candidate: minimum t, ties to the highest original index */
+        {
+            const float ot = quad_xorf1(ct);
+            const int oo = quad_xor<1>(co), os = quad_xor<1>(cs);
+            const bool tk = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
+            ct = tk ? ot : ct;
+            co = tk ? oo : co;
+            cs = tk ? os : cs;
+        }
+        {
+            const float ot = quad_xorf2(ct);
+            const int oo = quad_xor<2>(co), os = quad_xor<2>(cs);
+            const bool tk = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
+            ct = tk ? ot : ct;
+            co = tk ? oo : co;
+            cs = tk ? os : cs;
+        }
+        if (cs >= 0) {
+            q.best = cs;
+            q.best_t = ct;
+            q.best_orig = co;
+        }
+        /* a sorted candidate list's early end: the bound of the last record tested (tree leaves: 0) */
+        const float lb = __int_as_float(quad_bcast((int)w1.w, (int)take - 1));
+        if (q.best_t < lb) return true;
+        if (cnt > 4u) { /* the rest of a longer leaf is the next item */
+            q.node = ~(int)(((first + 4u) << 3) | (cnt - 5u));
+            return false;
+        }
+    } else {
+        if ((uint32_t)item >= n_nodes) {
+            if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_INDEX);
+            return true;
+        }
+        const v4u *vrec = reinterpret_cast<const v4u *>(reinterpret_cast<const uint4 *>(nodes) + 4 * item);
+        v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2], w3 = vrec[3];
+        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+        const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
+        const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);
+        float tn = kInf;
+        bool h = node_child_k(q0, q1, q2, sub, q.inv, q.oi, q.best_t, tn) && node_det_possible(q2, d);
+        const int child = (int)(sub == 0 ? w3.x : sub == 1 ? w3.y : sub == 2 ? w3.z : w3.w);
+        /* rank among the group's hits: nearest first, ties to the lower slot */
+        const int hi = h ? 1 : 0;
+        const float t1 = quad_xorf1(tn), t2 = quad_xorf2(tn), t3 = quad_xorf3(tn);
+        const int h1 = quad_xor<1>(hi), h2 = quad_xor<2>(hi), h3 = quad_xor<3>(hi);
+        const int rank = (h1 && (t1 < tn || (t1 == tn && (sub ^ 1) < sub)) ? 1 : 0) +
+                         (h2 && (t2 < tn || (t2 == tn && (sub ^ 2) < sub)) ? 1 : 0) +
+                         (h3 && (t3 < tn || (t3 == tn && (sub ^ 3) < sub)) ? 1 : 0);
+        const int nhit = hi + h1 + h2 + h3;
+        if (nhit > 0) {
+            if (q.sp + nhit - 1 > CoopStack::kCap) { /* cannot happen: reported, not clamped */
+                if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_STACK);
+                return true;
+            }
+            if (h && rank > 0) gst[q.sp + nhit - 1 - rank] = child; /* farthest deepest */
+            int nxt = (h && rank == 0) ? child : 0;
+            nxt |= quad_xor<1>(nxt);
+            nxt |= quad_xor<2>(nxt);
+            q.node = nxt;
+            q.sp += nhit - 1;
+            return false;
+        }
+    }
+    if (q.sp <= 0) return true;
+    q.node = gst[--q.sp];
+    return false;
 }
 
 /* Sample-split tiles, step 1: the seed pass.  A pixel's random numbers depend only on its
@@ -897,8 +1098,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
     /* the root node (coop_root): a uniform address, so scalar loads */
     const uint4 *__restrict__ rootp = reinterpret_cast<const uint4 *>(a.nodes);
-    const uint4 rq0 = COOP ? rootp[0] : uint4{}, rq1 = COOP ? rootp[1] : uint4{}, rq2 = COOP ? rootp[2] : uint4{},
-                rq3 = COOP ? rootp[3] : uint4{};
+    const uint4 rq0 = rootp[0], rq1 = rootp[1], rq2 = rootp[2], rq3 = rootp[3];
     const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
@@ -924,6 +1124,9 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     coop_begin(cq, qo, qd, kInf);
     uint32_t st_steps = 0, st_box = 0, st_t0 = 0; /* diagnostics (RT_PIXEL_STATS): per pixel */
     uint32_t q_steps = 0;                          /* rounds of the current query */
+    /* diagnostics builds (RT_SEED_STATS): per pixel the queries that took rounds, the queries
+       answered in the path advance, and the loop iterations */
+    uint32_t st_q = 0, st_imm = 0, st_it = 0;
     unsigned long long *const guard = a.counters + RT_CNT_GUARD; /* RT_GUARD_* flags (rt_synchronize) */
     for (;;) {
         /* lanes (COOP: groups) without a pixel take the next ones of the queue */
@@ -962,6 +1165,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         next = true;
                         if (a.pixel_stats) {
                             st_steps = st_box = 0;
+                            if (RT_SEED_STATS) st_q = st_imm = st_it = 0;
                             st_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         }
                     }
@@ -979,34 +1183,31 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
            registers: RT_SEED_ROOT) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly leave the mesh's box
            alone, so a long chain's samples are mostly resolved here, without a memory round trip. */
         for (int pass = 0;; ++pass) {
-            /* a new sample: the chunk's first seed, then the camera ray and its query */
+            /* a new sample: the chunk's first seed, then the camera ray and its query.  One-lane pass:
+               up to RT_SEED_FAST samples in a row whose camera ray the list's first record accepts are
+               finished right here (a mesh hit ends the sample after the light draws: rtcommon.h:411-421),
+               without the general advance below or a stepping round */
             if (next) {
                 next = false;
-                if ((sample == spp || sample % fine == 0u) && lane == gbase) {
-                    const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
-                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
-                }
-                if (sample == spp) {
-                    have = false;
-                    if (a.pixel_stats && lane == gbase) {
-                        uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
-                        ps[0] = st_t0;
-                        ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                        ps[2] = st_steps;
-                        ps[3] = st_box;
-                        ps[4] = 1u + (uint32_t)a.split_which;
+                for (int f = 0;; ++f) {
+                    if ((sample == spp || sample % fine == 0u) && lane == gbase) {
+                        const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
+                        reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
                     }
-                } else {
-                    /* the list's first record (the earliest possible accept t), loaded before the
-                       camera ray is formed so that its latency hides behind that arithmetic */
-                    float4 ra = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rb = ra, rc = ra;
+                    if (sample == spp) {
+                        have = false;
+                        if (a.pixel_stats && lane == gbase) {
+                            uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
+                            ps[0] = st_t0;
+                            ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                            ps[2] = st_steps;
+                            ps[3] = st_box;
+                            ps[4] = 1u + (uint32_t)a.split_which | (RT_SEED_STATS ? st_it << 4 : 0u);
+                            if (RT_SEED_STATS) ps[7] = st_q << 16 | (st_imm & 0xffffu);
+                        }
+                        break;
+                    }
                     const bool has_list = lpack < RT_LPACK_EMPTY;
-                    if (!COOP && RT_SEED_REC && has_list) {
-                        const uint32_t f0 = (lpack >> RT_LIST_BITS) << 3;
-                        ra = tris[3 * f0];
-                        rb = tris[3 * f0 + 1];
-                        rc = tris[3 * f0 + 2];
-                    }
                     const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
                     const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
                     const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
@@ -1014,6 +1215,23 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                     qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
                     qd = camera_dir(a.cam, fa - hw, fb - hh);
                     depth = 0;
+                    /* accepted by the list's first record (the earliest possible accept t; mt_test,
+                       t >= tmin): the camera ray hits the mesh — all the seed needs */
+                    bool accepted = false;
+                    if (!COOP && RT_SEED_REC && has_list) {
+                        const uint32_t f0 = (lpack >> RT_LIST_BITS) << 3;
+                        float t0 = 0.0f;
+                        accepted = mt_test(qo, qd, tris[3 * f0], tris[3 * f0 + 1], tris[3 * f0 + 2], t0) && !(t0 < RT_SMALL_F);
+                    }
+                    if (accepted && f + 1 < RT_SEED_FAST) {
+                        for (uint32_t l = 0; l < nl; ++l) {
+                            (void)frand(seed);
+                            (void)frand(seed);
+                        }
+                        if (RT_SEED_STATS) ++st_imm;
+                        ++sample;
+                        continue;
+                    }
                     if (COOP) coop_begin(cq, qo, qd, kInf);
                     else trav_begin(ts, stk, qo, qd, kInf);
                     q_steps = 0;
@@ -1025,51 +1243,48 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                             ts.best = -1;
                             cq.best = -1;
                             fin = true;
+                        } else if (accepted) {
+                            running = false;
+                            ts.best = (int)first;
+                            fin = true;
                         } else if (lpack != RT_LPACK_NONE) {
-                            bool accepted = false;
-                            if (!COOP && RT_SEED_REC) {
-                                /* accepted by the first record (mt_test, t >= tmin): the camera ray hits
-                                   the mesh — all the seed needs */
-                                float t0 = 0.0f;
-                                accepted = mt_test(qo, qd, ra, rb, rc, t0) && !(t0 < RT_SMALL_F);
-                                if (accepted) {
-                                    running = false;
-                                    ts.best = (int)first;
-                                    fin = true;
-                                }
-                            }
-                            if (!accepted) {
-                                for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
-                                    const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
-                                    const int v = ~(int)(((first + 8u * b) << 3) | (k - 1u));
-                                    if (COOP) {
-                                        if (lane == gbase) gst[cq.sp] = v;
-                                        ++cq.sp;
-                                    } else {
-                                        stk.push(v);
-                                    }
-                                }
-                                const int n0 = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
+                            for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
+                                const uint32_t k = pc - 8u * b < 8u ? pc - 8u * b : 8u;
+                                const int v = ~(int)(((first + 8u * b) << 3) | (k - 1u));
                                 if (COOP) {
-                                    /* coop_round: the list's first block on top */
-                                    if (lane == gbase) gst[cq.sp] = n0;
+                                    if (lane == gbase) gst[cq.sp] = v;
                                     ++cq.sp;
                                 } else {
-                                    ts.node = n0;
+                                    stk.push(v);
                                 }
+                            }
+                            const int n0 = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
+                            if (COOP && !RT_COOP_SPLIT) {
+                                /* coop_round: the list's first block on top */
+                                if (lane == gbase) gst[cq.sp] = n0;
+                                ++cq.sp;
+                            } else if (COOP) {
+                                cq.node = n0; /* coop_round2: the current item */
+                            } else {
+                                ts.node = n0;
                             }
                         } else if (COOP) { /* no list: the tree, from the root's children */
                             if (!coop_root(rq0, rq1, rq2, rq3, cq, gst, qd, lane == gbase)) {
                                 running = false;
                                 fin = true;
                             }
+                        } else if (!lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
+                            running = false;
+                            fin = true;
                         }
                     }
+                    break;
                 }
             }
             /* lanes whose query completed: the segment's draws, then the bounce or the next sample */
             if (fin) {
                 fin = false;
+                if (RT_SEED_STATS && q_steps == 0) ++st_imm; /* answered without a round */
                 bool sample_done = true;
                 if ((COOP ? cq.best : ts.best) >= 0) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
                     for (uint32_t l = 0; l < nl; ++l) {
@@ -1108,6 +1323,10 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                                 }
                             } else {
                                 trav_begin(ts, stk, qo, qd, kInf);
+                                if (!lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
+                                    running = false;
+                                    fin = true;
+                                }
                             }
                         }
                     }
@@ -1121,6 +1340,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                need a traversal must not wait long for those whose answers come at once */
             if (pass + 1 >= RT_SEED_IMM || !__any(next || fin)) break;
         }
+        if (RT_SEED_STATS) ++st_it;
         /* step the running queries (the box pixels' chains at top priority: they run beside the
            chunk tasks and set when the box pixels' chunks can start) */
         if (a.split_which == RT_SPLIT_BOX) __builtin_amdgcn_s_setprio(3);
@@ -1131,8 +1351,10 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 ++q_steps;
                 bool done;
                 if constexpr (G == 4) {
-                    done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, a.coop_multi_sp,
-                                      guard);
+                    done = RT_COOP_SPLIT
+                               ? coop_round2(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, guard)
+                               : coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs,
+                                            a.coop_multi_sp, guard);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
                     done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
@@ -1147,6 +1369,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 if (done || exists || q_steps > (1u << 14)) {
                     running = false;
                     fin = true;
+                    if (RT_SEED_STATS) ++st_q;
                 }
             }
         }

@@ -79,6 +79,10 @@ uint32_t probe_n(uint32_t sample_rate) { return sample_rate >= 2 ? kProbeN : 1u;
 #ifndef RT_FETCH_K
 #define RT_FETCH_K 24
 #endif
+constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
+#ifndef RT_BOX_GRID_DIV
+#define RT_BOX_GRID_DIV 4 /* the long chains' seed pass takes at most 1/RT_BOX_GRID_DIV of the persistent grid */
+#endif
 #ifndef RT_SEED_GRID_ITEMS
 #define RT_SEED_GRID_ITEMS 1
 #endif
@@ -182,8 +186,10 @@ struct rt_ctx {
     uint32_t *d_seeds = nullptr;
 
     /* scratch */
-    uint32_t *d_work = nullptr;
-    unsigned long long *d_counters = nullptr;
+    uint32_t *d_work = nullptr;                 /* queue cursors: inside the d_counters allocation, after the counters */
+    unsigned long long *d_counters = nullptr;   /* RT_COUNTER_WORDS counters + guard, then the 64 cursor words */
+    unsigned long long *h_counters = nullptr;   /* pinned: the counters (+ the list area's fill) copied back on the render's stream */
+    hipStream_t sync_stream = nullptr;          /* the stream of the last render (rt_synchronize waits on it) */
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
     rt_counters last = {};
@@ -449,7 +455,7 @@ int split_box_blocks(const rt_ctx *c, uint32_t width, int full_grid)
 {
     const uint32_t per_wave = c->split_gpw ? c->split_gpw : 64u / std::max(1u, width);
     int n = (int)((c->n_split_box + per_wave * 4u - 1u) / (per_wave * 4u));
-    if (full_grid > 0) n = std::min(n, std::max(1, full_grid / 4));
+    if (full_grid > 0) n = std::min(n, std::max(1, full_grid / RT_BOX_GRID_DIV));
     return n;
 }
 
@@ -621,10 +627,12 @@ int rt_create(int device, rt_ctx **out)
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evm) != hipSuccess ||
-        hipMalloc(&c->d_work, 64 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&c->d_counters, RT_COUNTER_WORDS * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_counters, kCounterBytes + 64 * sizeof(uint32_t)) != hipSuccess ||
+        hipHostMalloc(&c->h_counters, kCounterBytes + sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_HIP;
     }
+    c->d_work = reinterpret_cast<uint32_t *>(c->d_counters + RT_COUNTER_WORDS);
     *out = c;
     return RT_OK;
 }
@@ -657,8 +665,8 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_list_alloc);
     rt_sched_free(c->sched);
     free_dev(c->d_seeds);
-    free_dev(c->d_work);
-    free_dev(c->d_counters);
+    free_dev(c->d_counters); /* d_work lives in it */
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
     free_dev(c->d_stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -971,7 +979,8 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         dout = c->d_stage;
         if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
     }
-    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), st));
+    /* the counters, the guard word and the queue cursors: one memset */
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + 64 * sizeof(uint32_t), st));
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;
     int e = 0;
@@ -1094,7 +1103,6 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             }
         }
         const double sched_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
-        HIPCHK(c, hipMemsetAsync(c->d_work, 0, sizeof(uint32_t), st));
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
             fprintf(stderr,
                     "[rtmi %p] k_tris trav %d count %d grid %d x %d, spill_cap %u, order %p, split %u x %u, long %u\n",
@@ -1270,6 +1278,13 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info_list_pending = false;
     }
     if (e) return hip_fail(c, (hipError_t)e, "kernel launch");
+    /* the counters (and a new list build's fill) come back on the render's stream, so that
+       rt_synchronize is one stream wait (no blocking copy after it) */
+    HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, st));
+    if (c->info.lists_rebuilt)
+        HIPCHK(c, hipMemcpyAsync(c->h_counters + RT_COUNTER_WORDS, c->d_list_alloc, sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, st));
+    c->sync_stream = st;
     c->have_timing = true;
     c->last_out = dout;
     c->last_bytes = out_bytes;
@@ -1282,11 +1297,10 @@ int rt_synchronize(rt_ctx *c)
     if (!c) return RT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    unsigned long long h[RT_COUNTER_WORDS];
-    HIPCHK(c, hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+    if (c->sync_stream && c->sync_stream != c->stream) HIPCHK(c, hipStreamSynchronize(c->sync_stream));
+    const unsigned long long *h = c->h_counters;
     if (c->info.lists_rebuilt) { /* the list area the new lists took: sizes the next build's area */
-        uint32_t used = 0;
-        HIPCHK(c, hipMemcpy(&used, c->d_list_alloc, sizeof(used), hipMemcpyDeviceToHost));
+        const uint32_t used = (uint32_t)(h[RT_COUNTER_WORDS] & 0xffffffffu);
         c->list_used_last = used;
         c->list_cap_last = c->info.list_capacity;
         c->list_npx_last = c->info_list_px;

@@ -849,6 +849,9 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
 #ifndef RT_SEED_STATS
 #define RT_SEED_STATS 0 /* diagnostics builds: per-pixel query / immediate-answer / iteration counts (RT_PIXEL_STATS) */
 #endif
+#ifndef RT_SEED_RECN
+#define RT_SEED_RECN 1 /* ... that many of its first records */
+#endif
 #ifndef RT_SEED_FAST
 #define RT_SEED_FAST 8 /* one-lane seed pass: samples finished in a row in the new-sample step (first list record) */
 #endif
@@ -1127,6 +1130,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     /* diagnostics builds (RT_SEED_STATS): per pixel the queries that took rounds, the queries
        answered in the path advance, and the loop iterations */
     uint32_t st_q = 0, st_imm = 0, st_it = 0;
+    unsigned long long st_adv = 0, st_rnd = 0; /* clocks in the path advance / in stepping rounds */
     unsigned long long *const guard = a.counters + RT_CNT_GUARD; /* RT_GUARD_* flags (rt_synchronize) */
     for (;;) {
         /* lanes (COOP: groups) without a pixel take the next ones of the queue */
@@ -1165,7 +1169,10 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         next = true;
                         if (a.pixel_stats) {
                             st_steps = st_box = 0;
-                            if (RT_SEED_STATS) st_q = st_imm = st_it = 0;
+                            if (RT_SEED_STATS) {
+                                st_q = st_imm = st_it = 0;
+                                st_adv = st_rnd = 0;
+                            }
                             st_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         }
                     }
@@ -1182,6 +1189,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
            before the ray is formed: RT_SEED_REC), a box bounce whose ray misses the root's child boxes (tested from
            registers: RT_SEED_ROOT) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly leave the mesh's box
            alone, so a long chain's samples are mostly resolved here, without a memory round trip. */
+        const unsigned long long t_adv0 = RT_SEED_STATS ? wave_clock() : 0ull;
         for (int pass = 0;; ++pass) {
             /* a new sample: the chunk's first seed, then the camera ray and its query.  One-lane pass:
                up to RT_SEED_FAST samples in a row whose camera ray the list's first record accepts are
@@ -1203,7 +1211,11 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                             ps[2] = st_steps;
                             ps[3] = st_box;
                             ps[4] = 1u + (uint32_t)a.split_which | (RT_SEED_STATS ? st_it << 4 : 0u);
-                            if (RT_SEED_STATS) ps[7] = st_q << 16 | (st_imm & 0xffffu);
+                            if (RT_SEED_STATS) {
+                                ps[7] = st_q << 16 | (st_imm & 0xffffu);
+                                ps[5] = (uint32_t)(st_adv >> 6);
+                                ps[6] = (uint32_t)(st_rnd >> 6);
+                            }
                         }
                         break;
                     }
@@ -1219,9 +1231,16 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                        t >= tmin): the camera ray hits the mesh — all the seed needs */
                     bool accepted = false;
                     if (!COOP && RT_SEED_REC && has_list) {
-                        const uint32_t f0 = (lpack >> RT_LIST_BITS) << 3;
-                        float t0 = 0.0f;
-                        accepted = mt_test(qo, qd, tris[3 * f0], tris[3 * f0 + 1], tris[3 * f0 + 2], t0) && !(t0 < RT_SMALL_F);
+                        /* any accept answers an existence query, so the first RT_SEED_RECN records
+                           are tried in list order (a pixel whose nearest candidate the determinant
+                           test rejects is mostly accepted by its second or third) */
+                        const uint32_t f0 = (lpack >> RT_LIST_BITS) << 3, pc0 = (lpack & (RT_LIST_MAX - 1u)) + 1u;
+                        const uint32_t kn = pc0 < (uint32_t)RT_SEED_RECN ? pc0 : (uint32_t)RT_SEED_RECN;
+                        for (uint32_t k = 0; k < kn && !accepted; ++k) {
+                            float t0 = 0.0f;
+                            const uint32_t s = f0 + k;
+                            accepted = mt_test(qo, qd, tris[3 * s], tris[3 * s + 1], tris[3 * s + 2], t0) && !(t0 < RT_SMALL_F);
+                        }
                     }
                     if (accepted && f + 1 < RT_SEED_FAST) {
                         for (uint32_t l = 0; l < nl; ++l) {
@@ -1340,7 +1359,12 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                need a traversal must not wait long for those whose answers come at once */
             if (pass + 1 >= RT_SEED_IMM || !__any(next || fin)) break;
         }
-        if (RT_SEED_STATS) ++st_it;
+        unsigned long long t_rnd0 = 0;
+        if (RT_SEED_STATS) {
+            ++st_it;
+            t_rnd0 = wave_clock();
+            st_adv += t_rnd0 - t_adv0;
+        }
         /* step the running queries (the box pixels' chains at top priority: they run beside the
            chunk tasks and set when the box pixels' chunks can start) */
         if (a.split_which == RT_SPLIT_BOX) __builtin_amdgcn_s_setprio(3);
@@ -1373,6 +1397,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 }
             }
         }
+        if (RT_SEED_STATS) st_rnd += wave_clock() - t_rnd0;
     }
 }
 
@@ -2200,7 +2225,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
 }
 
 template <int G>
-__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLaunch a)
+#ifndef RT_SEED_WAVES
+#define RT_SEED_WAVES RT_TRIS_WAVES /* blocks per CU the seed pass's register budget is cut for */
+#endif
+__global__ __launch_bounds__(RT_BLOCK, RT_SEED_WAVES) void k_split_seeds(RtTriLaunch a)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     seed_pass<G>(a, s_stack);

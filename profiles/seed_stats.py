@@ -71,6 +71,9 @@ def main():
             res[name]["iterations"] = {p: int(np.quantile(it, p / 100)) for p in (50, 90, 100)}
             res[name]["us_per_iteration_longest"] = [round(float(dur[i]) * 1e3 / max(1, int(it[i])), 2) for i in order[:4]]
             res[name]["longest_q_imm_it"] = [[int(q[i]), int(imm[i]), int(it[i])] for i in order[:6]]
+            adv, rnd = st[m, 5] * 64.0, st[m, 6] * 64.0  # shader clocks in the path advance / the rounds
+            res[name]["advance_share_longest"] = [round(float(adv[i] / max(1.0, adv[i] + rnd[i])), 3) for i in order[:6]]
+            res[name]["clocks_per_iteration_longest"] = [int((adv[i] + rnd[i]) / max(1, int(it[i]))) for i in order[:6]]
     print(json.dumps(res))
 
 

@@ -14,6 +14,7 @@
 #   tiles[=<args>]             profiles/tile_scaling.py <args>               -> tiles[_<n>].json / .log
 #   ab=<args>                  profiles/ab_inproc.py <args> (in-process A/B of library builds) -> ab[_<n>].txt
 #   py=<script>[,<args>]       python <script> <args>                        -> py_<n>.log
+#   benchgloo=<args>           BENCH_DIST_BACKEND=gloo python bench.py <args> (e.g. --gpus,2: N ranks rehearsed on one GPU)
 #   trace=<args>               rocprofv3 kernel trace of profiles/render_tile.py <args> -> trace_<n>/ + trace_<n>.txt
 #                              (profiles/tile_trace.py: per-kernel spans of the last render)
 # Example: bash scripts/gpu.sh r04a tests smoke bench bench=--config,bunny tiles=--config,dragon
@@ -53,6 +54,8 @@ for step in "$@"; do
         timeout -k 10 900 python -u profiles/ab_inproc.py $args > "$OUT/ab_$n.txt" 2>&1 ;;
     py)
         timeout -k 10 600 python -u $args > "$OUT/py_$n.log" 2>&1 ;;
+    benchgloo)
+        BENCH_DIST_BACKEND=gloo timeout -k 10 900 python -u bench.py $args > "$OUT/benchgloo_$n.json" 2> "$OUT/benchgloo_$n.err" ;;
     trace)
         timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/trace_$n" -o run -- \
             python3 profiles/render_tile.py $args > "$OUT/trace_$n.log" 2>&1 &&

@@ -55,6 +55,7 @@ int main(int argc, char **argv)
             }
         }
     }
+    double n_boxs = 0, n_boxs_only = 0;
     double n_back = 0, n_meshhit = 0, occ_t_hist[5] = {}, occ_t_steps[5] = {};
     int dbg_n = 0;
     double occ_steps = 0, occ_lb = 0, occ_n = 0, unocc_steps = 0, unocc_n = 0;
@@ -107,6 +108,7 @@ int main(int argc, char **argv)
         for (int s = 0; s < spp; ++s) {
             V d = norm(add(add(view, mul(right, px + U(rng) - W / 2.0f)), mul(up, py + U(rng) - H / 2.0f)));
             V o = pos;
+            bool box_sample = false, mesh_later = false;
             for (int depth = 0; depth <= 6; ++depth) {
                 float t;
                 int hit;
@@ -163,12 +165,20 @@ int main(int argc, char **argv)
                 } else {
                     nskip[ks] += 1;
                 }
+                if (depth == 0 && hit < 0) box_sample = true;
+                if (depth > 0 && hit >= 0) mesh_later = true;
                 if (hit >= 0) break;
                 o = p;
                 d = frame_dir(n, U(rng), U(rng));
             }
+            if (box_sample) {
+                n_boxs += 1;
+                n_boxs_only += !mesh_later;
+            }
         }
     }
+    printf("box samples (camera ray misses the mesh): %.0f, box-only paths (no bounce hits the mesh): %.1f%%\n", n_boxs,
+           100 * n_boxs_only / std::max(1.0, n_boxs));
     double tot = 0;
     for (int k = 0; k < NK; ++k) tot += ns[k];
     printf("%d pixels x %d samples: %.0f traversal steps\n", n_px, spp, tot);

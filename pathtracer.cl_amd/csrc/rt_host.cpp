@@ -87,6 +87,15 @@ constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
 #define RT_SEED_GRID_ITEMS 1
 #endif
 constexpr uint32_t kFetchK = RT_FETCH_K;
+/* an unsigned environment knob (tuning sweeps), `def` when unset or unparsable */
+uint32_t env_u32(const char *name, uint32_t def)
+{
+    const char *v = getenv(name);
+    if (!v || !*v) return def;
+    char *end = nullptr;
+    const unsigned long x = strtoul(v, &end, 10);
+    return (end && *end == 0) ? (uint32_t)x : def;
+}
 constexpr uint32_t kFetchFrac = 24;
 
 } // namespace
@@ -1017,6 +1026,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         int r = grid_blocks(c, trav, c->counting, RT_FORM_PLAIN, &blocks);
         if (r != RT_OK) return r;
         blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks, item_blocks));
+        if (const uint32_t gb = env_u32("RTMI_GRID_BLOCKS", 0)) blocks = std::min(blocks, (int)gb);
         if (trav == RT_TRAV_BVH4Q) {
             r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
             if (r != RT_OK) return r;
@@ -1031,9 +1041,9 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
-        a.fetch_k = kFetchK;
-        a.fetch_k_box = kFetchK;
-        a.fetch_frac = kFetchFrac;
+        a.fetch_k = env_u32("RTMI_FETCH_K", kFetchK); /* tuning knobs (profiles/bunny_sweep.py) */
+        a.fetch_k_box = a.fetch_k;
+        a.fetch_frac = env_u32("RTMI_FETCH_FRAC", kFetchFrac);
         a.box_exit = 0;
         a.probe_n = probe_n(c->sample_rate);
         a.diag_pixel = 0xffffffffu;

@@ -662,7 +662,6 @@ __device__ __forceinline__ int quad_xor(int v)
 }
 __device__ __forceinline__ float quad_xorf1(float v) { return __int_as_float(quad_xor<1>(__float_as_int(v))); }
 __device__ __forceinline__ float quad_xorf2(float v) { return __int_as_float(quad_xor<2>(__float_as_int(v))); }
-__device__ __forceinline__ float quad_xorf3(float v) { return __int_as_float(quad_xor<3>(__float_as_int(v))); }
 /* the value of quad lane k (k uniform within the quad) */
 __device__ __forceinline__ int quad_bcast(int v, int k)
 {
@@ -686,7 +685,7 @@ struct CoopStackG {
 typedef CoopStackG<4> CoopStack;
 
 struct CoopQuery {
-    int node, best, best_orig, sp;
+    int best, best_orig, sp;
     float best_t;
     V3 inv, oi;
 };
@@ -695,7 +694,6 @@ __device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
 {
     q.inv = v3(safe_rcp(d.x), safe_rcp(d.y), safe_rcp(d.z));
     q.oi = v3(o.x * q.inv.x, o.y * q.inv.y, o.z * q.inv.z);
-    q.node = 0;
     q.best = -1;
     q.best_orig = -1;
     q.best_t = tmax;
@@ -836,24 +834,11 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     return q.sp == 0;
 }
 
-#ifndef RT_COOP_SPLIT
-#define RT_COOP_SPLIT 1 /* cooperative seed-pass rounds: one stack item shared by the 4 lanes (coop_round2) */
-#endif
-
 #ifndef RT_SEED_ROOT
 #define RT_SEED_ROOT 1 /* cooperative seed-pass queries start from the root's child boxes, tested in registers */
 #endif
-#ifndef RT_SEED_REC
-#define RT_SEED_REC 1 /* one-lane seed pass: a camera ray tests its list's first record in the path advance */
-#endif
 #ifndef RT_SEED_STATS
 #define RT_SEED_STATS 0 /* diagnostics builds: per-pixel query / immediate-answer / iteration counts (RT_PIXEL_STATS) */
-#endif
-#ifndef RT_SEED_RECN
-#define RT_SEED_RECN 1 /* ... that many of its first records */
-#endif
-#ifndef RT_SEED_FAST
-#define RT_SEED_FAST 8 /* one-lane seed pass: samples finished in a row in the new-sample step (first list record) */
 #endif
 #ifndef RT_SEED_IMM
 #define RT_SEED_IMM 2 /* path-advance passes per seed-pass iteration (queries answered at once chain) */
@@ -868,11 +853,6 @@ __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
                                           bool writer)
 {
     if (!RT_SEED_ROOT) {
-        if (RT_COOP_SPLIT) {
-            q.node = 0;
-            q.sp = 0;
-            return true;
-        }
         if (writer) gst[0] = 0;
         q.sp = 1;
         return true;
@@ -880,16 +860,6 @@ __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
     float t[4];
     int c[4];
     const int nh = node_children(r0, r1, r2, r3, q.inv, q.oi, d, q.best_t, false, false, t, c);
-    if (RT_COOP_SPLIT) { /* coop_round2: the nearest is the current item, the others on the stack */
-        if (writer) {
-#pragma unroll
-            for (int i = 1; i < 4; ++i)
-                if (i < nh) gst[nh - 1 - i] = c[i];
-        }
-        q.node = c[0];
-        q.sp = nh > 0 ? nh - 1 : 0;
-        return nh > 0;
-    }
     if (writer) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -914,178 +884,6 @@ __device__ __forceinline__ bool lane_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
     return nh > 0;
 }
 
-/* Child `k` (per lane) of a compressed node against the ray: node_children's arithmetic for one
-   child (fma(byte, scale, base): the same bits as its f16-subnormal form), its entry t and whether
-   it is hit.  Culling only. */
-__device__ __forceinline__ bool node_child_k(uint4 q0, uint4 q1, uint4 q2, int k, V3 inv, V3 oi, float best_t, float &tn)
-{
-    const float tmin_c = -1e-3f;
-    const float tmax_c = t_slack(best_t);
-    const uint32_t w = q0.w;
-    const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
-    const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
-    const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
-    const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
-    const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
-    const float bz = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
-    const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
-    const uint32_t nxw = px ? q1.x : q1.y, fxw = px ? q1.y : q1.x;
-    const uint32_t nyw = py ? q1.z : q1.w, fyw = py ? q1.w : q1.z;
-    const uint32_t nzw = pz ? q2.x : q2.y, fzw = pz ? q2.y : q2.x;
-    const uint32_t sh = 8u * (uint32_t)k;
-    const float nx = __builtin_fmaf((float)((nxw >> sh) & 0xffu), sx, bx), fx = __builtin_fmaf((float)((fxw >> sh) & 0xffu), sx, bx);
-    const float ny = __builtin_fmaf((float)((nyw >> sh) & 0xffu), sy, by), fy = __builtin_fmaf((float)((fyw >> sh) & 0xffu), sy, by);
-    const float nz = __builtin_fmaf((float)((nzw >> sh) & 0xffu), sz, bz), fz = __builtin_fmaf((float)((fzw >> sh) & 0xffu), sz, bz);
-    tn = __builtin_fmaxf(__builtin_fmaxf(nx, ny), __builtin_fmaxf(nz, tmin_c));
-    const float tf = __builtin_fminf(__builtin_fminf(fx, fy), __builtin_fminf(fz, tmax_c));
-    return tn <= tf; /* an unused slot's inverted box never passes */
-}
-
-/* The node's determinant cull (node_children): false when no triangle below can pass |det| >= 1e-4. */
-__device__ __forceinline__ bool node_det_possible(uint4 q2, V3 d)
-{
-    const bool px = d.x >= 0.0f, py = d.y >= 0.0f, pz = d.z >= 0.0f;
-    const uint32_t nlo = q2.z, nhi = q2.w;
-    const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
-    const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
-    const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
-    const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
-    const float bias = 128.0f * (d.x + d.y + d.z);
-    const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
-                                     __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu), __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
-    const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
-                                     __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu), __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
-    const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
-    const float bound = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
-    return !(bound < 1e-4f);
-}
-
-/* Cooperative closest-hit round, one stack ITEM per round shared by the group's 4 lanes: a node's
-   4 child boxes one per lane (ranked by DPP exchanges, the hits pushed farthest first, the nearest
-   taken next), or up to 4 triangles of a leaf or candidate-list block one per lane (the rest of a
-   longer one stays the next item).  The same tests and accept rule as trav_step_q, depth first and
-   nearest first; about a quarter of coop_round's instructions per round for about a third more
-   rounds per query, and a long chain is its rounds' dependent latency.  q.node is the item. */
-__device__ __forceinline__ bool coop_round2(const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
-                                            CoopQuery &q, const CoopStack &gst, V3 o, V3 d, float tmin,
-                                            uint32_t n_nodes, uint32_t n_recs, unsigned long long *guard)
-{
-    const int sub = (int)(threadIdx.x & 3);
-    const int item = q.node;
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    if (item < 0) {
-        const uint32_t enc = ~(uint32_t)item, first = enc >> 3, cnt = (enc & 7u) + 1u;
-        const uint32_t take = cnt < 4u ? cnt : 4u;
-        const bool act = (uint32_t)sub < take;
-        const uint32_t slot = first + (uint32_t)sub;
-        if (first + take > n_recs) { /* every record index is checked: a defect ends the query, reported */
-            if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_INDEX);
-            return true;
-        }
-        v4u w0 = {0u, 0u, 0u, 0u}, w1 = w0, w2 = w0;
-        if (act) {
-            const v4u *vrec = reinterpret_cast<const v4u *>(reinterpret_cast<const uint4 *>(tris) + 3 * slot);
-            w0 = vrec[0];
-            w1 = vrec[1];
-            w2 = vrec[2];
-        }
-        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2));
-        float ct = kInf;
-        int co = -1, cs = -1;
-        if (act) {
-            const float4 ta = make_float4(__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z),
-                                          __uint_as_float(w0.w));
-            const float4 tb = make_float4(__uint_as_float(w1.x), __uint_as_float(w1.y), __uint_as_float(w1.z), 0.0f);
-            const float4 tc = make_float4(__uint_as_float(w2.x), __uint_as_float(w2.y), __uint_as_float(w2.z), 0.0f);
-            float tt = 0.0f;
-            const bool h = mt_test(o, d, ta, tb, tc, tt);
-            const int orig = __float_as_int(ta.w);
-            if (h && !(tt < tmin) && (tt < q.best_t || (tt == q.best_t && orig > q.best_orig))) {
-                ct = tt;
-                co = orig;
-                cs = (int)slot;
-            }
-        }
-        /* the group's best candidate: minimum t, ties to the highest original index */
-        {
-            const float ot = quad_xorf1(ct);
-            const int oo = quad_xor<1>(co), os = quad_xor<1>(cs);
-            const bool tk = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
-            ct = tk ? ot : ct;
-            co = tk ? oo : co;
-            cs = tk ? os : cs;
-        }
-        {
-            const float ot = quad_xorf2(ct);
-            const int oo = quad_xor<2>(co), os = quad_xor<2>(cs);
-            const bool tk = os >= 0 && (cs < 0 || ot < ct || (ot == ct && oo > co));
-            ct = tk ? ot : ct;
-            co = tk ? oo : co;
-            cs = tk ? os : cs;
-        }
-        if (cs >= 0) {
-            q.best = cs;
-            q.best_t = ct;
-            q.best_orig = co;
-        }
-        /* a sorted candidate list's early end: the bound of the last record tested (tree leaves: 0) */
-        const float lb = __int_as_float(quad_bcast((int)w1.w, (int)take - 1));
-        if (q.best_t < lb) return true;
-        if (cnt > 4u) { /* the rest of a longer leaf is the next item */
-            q.node = ~(int)(((first + 4u) << 3) | (cnt - 5u));
-            return false;
-        }
-    } else {
-        if ((uint32_t)item >= n_nodes) {
-            if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_INDEX);
-            return true;
-        }
-        const v4u *vrec = reinterpret_cast<const v4u *>(reinterpret_cast<const uint4 *>(nodes) + 4 * item);
-        v4u w0 = vrec[0], w1 = vrec[1], w2 = vrec[2], w3 = vrec[3];
-        asm volatile("" : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
-        const uint4 q0 = make_uint4(w0.x, w0.y, w0.z, w0.w), q1 = make_uint4(w1.x, w1.y, w1.z, w1.w);
-        const uint4 q2 = make_uint4(w2.x, w2.y, w2.z, w2.w);
-        float tn = kInf;
-        bool h = node_child_k(q0, q1, q2, sub, q.inv, q.oi, q.best_t, tn) && node_det_possible(q2, d);
-        const int child = (int)(sub == 0 ? w3.x : sub == 1 ? w3.y : sub == 2 ? w3.z : w3.w);
-        /* rank among the group's hits: nearest first, ties to the lower slot */
-        const int hi = h ? 1 : 0;
-        const float t1 = quad_xorf1(tn), t2 = quad_xorf2(tn), t3 = quad_xorf3(tn);
-        const int h1 = quad_xor<1>(hi), h2 = quad_xor<2>(hi), h3 = quad_xor<3>(hi);
-        const int rank = (h1 && (t1 < tn || (t1 == tn && (sub ^ 1) < sub)) ? 1 : 0) +
-                         (h2 && (t2 < tn || (t2 == tn && (sub ^ 2) < sub)) ? 1 : 0) +
-                         (h3 && (t3 < tn || (t3 == tn && (sub ^ 3) < sub)) ? 1 : 0);
-        const int nhit = hi + h1 + h2 + h3;
-        if (nhit > 0) {
-            if (q.sp + nhit - 1 > CoopStack::kCap) { /* cannot happen: reported, not clamped */
-                if (sub == 0) atomicOr(guard, (unsigned long long)RT_GUARD_STACK);
-                return true;
-            }
-            if (h && rank > 0) gst[q.sp + nhit - 1 - rank] = child; /* farthest deepest */
-            int nxt = (h && rank == 0) ? child : 0;
-            nxt |= quad_xor<1>(nxt);
-            nxt |= quad_xor<2>(nxt);
-            q.node = nxt;
-            q.sp += nhit - 1;
-            return false;
-        }
-    }
-    if (q.sp <= 0) return true;
-    q.node = gst[--q.sp];
-    return false;
-}
-
-/* Sample-split tiles, step 1: the seed pass.  A pixel's random numbers depend only on its
-   closest hits (trace_path_tri, rtcommon.h:371-468): per surface hit two draws per light
-   whatever its shadow ray finds (:88-92), two more for the Lambert bounce off the box (:459);
-   a mesh hit (:421) or a box miss (:463-466) ends the sample; each sample starts with the two
-   strat_rand draws of its camera ray (raytracer.cl:216-224).  So one lane (COOP: one 4-lane
-   group) per pixel walks the pixel's samples with the closest-hit queries alone (camera rays
-   through the pixel's candidate list, box bounces through the tree, directions in k_tris's
-   arithmetic), draws and drops the light samples' numbers, and stores the seed at the first
-   sample of every chunk and after the last one.  The queries are resumable: the wave steps
-   every running query and a lane whose query completed advances at once, so no chain waits for
-   its neighbours'. */
 template <int G> /* lanes per query: 1 (trav_step_q) or 4 (coop_round) */
 __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
 {
@@ -1185,41 +983,35 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
         }
         /* The path advance, over as many segments and samples as it takes before the next stepping
            round: a new sample's camera ray, and every query answered without a round — an empty
-           candidate list, a mesh pixel's camera ray accepted by the first record of its list (loaded
-           before the ray is formed: RT_SEED_REC), a box bounce whose ray misses the root's child boxes (tested from
-           registers: RT_SEED_ROOT) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly leave the mesh's box
-           alone, so a long chain's samples are mostly resolved here, without a memory round trip. */
+           candidate list, a box bounce whose ray misses the root's child boxes (tested from
+           registers: RT_SEED_ROOT) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly
+           leave the mesh's box alone, so a long chain's samples are mostly resolved here, without a
+           memory round trip. */
         const unsigned long long t_adv0 = RT_SEED_STATS ? wave_clock() : 0ull;
         for (int pass = 0;; ++pass) {
-            /* a new sample: the chunk's first seed, then the camera ray and its query.  One-lane pass:
-               up to RT_SEED_FAST samples in a row whose camera ray the list's first record accepts are
-               finished right here (a mesh hit ends the sample after the light draws: rtcommon.h:411-421),
-               without the general advance below or a stepping round */
+            /* a new sample: the chunk's first seed, then the camera ray and its query */
             if (next) {
                 next = false;
-                for (int f = 0;; ++f) {
-                    if ((sample == spp || sample % fine == 0u) && lane == gbase) {
-                        const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
-                        reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
-                    }
-                    if (sample == spp) {
-                        have = false;
-                        if (a.pixel_stats && lane == gbase) {
-                            uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
-                            ps[0] = st_t0;
-                            ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                            ps[2] = st_steps;
-                            ps[3] = st_box;
-                            ps[4] = 1u + (uint32_t)a.split_which | (RT_SEED_STATS ? st_it << 4 : 0u);
-                            if (RT_SEED_STATS) {
-                                ps[7] = st_q << 16 | (st_imm & 0xffffu);
-                                ps[5] = (uint32_t)(st_adv >> 6);
-                                ps[6] = (uint32_t)(st_rnd >> 6);
-                            }
+                if ((sample == spp || sample % fine == 0u) && lane == gbase) {
+                    const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
+                }
+                if (sample == spp) {
+                    have = false;
+                    if (a.pixel_stats && lane == gbase) {
+                        uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
+                        ps[0] = st_t0;
+                        ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        ps[2] = st_steps;
+                        ps[3] = st_box;
+                        ps[4] = 1u + (uint32_t)a.split_which | (RT_SEED_STATS ? st_it << 4 : 0u);
+                        if (RT_SEED_STATS) {
+                            ps[7] = st_q << 16 | (st_imm & 0xffffu);
+                            ps[5] = (uint32_t)(st_adv >> 6);
+                            ps[6] = (uint32_t)(st_rnd >> 6);
                         }
-                        break;
                     }
-                    const bool has_list = lpack < RT_LPACK_EMPTY;
+                } else {
                     const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
                     const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
                     const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
@@ -1227,30 +1019,6 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                     qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
                     qd = camera_dir(a.cam, fa - hw, fb - hh);
                     depth = 0;
-                    /* accepted by the list's first record (the earliest possible accept t; mt_test,
-                       t >= tmin): the camera ray hits the mesh — all the seed needs */
-                    bool accepted = false;
-                    if (!COOP && RT_SEED_REC && has_list) {
-                        /* any accept answers an existence query, so the first RT_SEED_RECN records
-                           are tried in list order (a pixel whose nearest candidate the determinant
-                           test rejects is mostly accepted by its second or third) */
-                        const uint32_t f0 = (lpack >> RT_LIST_BITS) << 3, pc0 = (lpack & (RT_LIST_MAX - 1u)) + 1u;
-                        const uint32_t kn = pc0 < (uint32_t)RT_SEED_RECN ? pc0 : (uint32_t)RT_SEED_RECN;
-                        for (uint32_t k = 0; k < kn && !accepted; ++k) {
-                            float t0 = 0.0f;
-                            const uint32_t s = f0 + k;
-                            accepted = mt_test(qo, qd, tris[3 * s], tris[3 * s + 1], tris[3 * s + 2], t0) && !(t0 < RT_SMALL_F);
-                        }
-                    }
-                    if (accepted && f + 1 < RT_SEED_FAST) {
-                        for (uint32_t l = 0; l < nl; ++l) {
-                            (void)frand(seed);
-                            (void)frand(seed);
-                        }
-                        if (RT_SEED_STATS) ++st_imm;
-                        ++sample;
-                        continue;
-                    }
                     if (COOP) coop_begin(cq, qo, qd, kInf);
                     else trav_begin(ts, stk, qo, qd, kInf);
                     q_steps = 0;
@@ -1261,10 +1029,6 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                             running = false;
                             ts.best = -1;
                             cq.best = -1;
-                            fin = true;
-                        } else if (accepted) {
-                            running = false;
-                            ts.best = (int)first;
                             fin = true;
                         } else if (lpack != RT_LPACK_NONE) {
                             for (uint32_t b = (pc - 1u) >> 3; b > 0u; --b) {
@@ -1278,12 +1042,9 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                                 }
                             }
                             const int n0 = ~(int)((first << 3) | ((pc < 8u ? pc : 8u) - 1u));
-                            if (COOP && !RT_COOP_SPLIT) {
-                                /* coop_round: the list's first block on top */
+                            if (COOP) { /* coop_round: the list's first block on top */
                                 if (lane == gbase) gst[cq.sp] = n0;
                                 ++cq.sp;
-                            } else if (COOP) {
-                                cq.node = n0; /* coop_round2: the current item */
                             } else {
                                 ts.node = n0;
                             }
@@ -1297,7 +1058,6 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                             fin = true;
                         }
                     }
-                    break;
                 }
             }
             /* lanes whose query completed: the segment's draws, then the bounce or the next sample */
@@ -1375,10 +1135,8 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 ++q_steps;
                 bool done;
                 if constexpr (G == 4) {
-                    done = RT_COOP_SPLIT
-                               ? coop_round2(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, guard)
-                               : coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs,
-                                            a.coop_multi_sp, guard);
+                    done = coop_round(nodes, tris, cq, gst, qo, qd, RT_SMALL_F, a.n_nodes4, a.n_recs, a.coop_multi_sp,
+                                      guard);
                 } else {
                     TravCounts tc = {0u, 0u, 0u};
                     done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
@@ -2225,10 +1983,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
 }
 
 template <int G>
-#ifndef RT_SEED_WAVES
-#define RT_SEED_WAVES RT_TRIS_WAVES /* blocks per CU the seed pass's register budget is cut for */
-#endif
-__global__ __launch_bounds__(RT_BLOCK, RT_SEED_WAVES) void k_split_seeds(RtTriLaunch a)
+__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLaunch a)
 {
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     seed_pass<G>(a, s_stack);

@@ -4,7 +4,7 @@ steps per pixel), then: the finish
 time distribution, the last pixels to finish and what they are (probe: box or mesh pixel),
 and how the frame's last milliseconds are spent.  GPU box.
 
-    python profiles/pixel_stats.py [out.json]
+    python profiles/pixel_stats.py [out.json] [--config dragon|bunny] [--lib build.so]
 
 The plain launch records clocks only in a diagnostics build of the library
 (`bash profiles/build_variant.sh ab/stats.so -DRT_PLAIN_PIXEL_STATS=1`, run with
@@ -27,16 +27,26 @@ def main():
 
     dump = "/tmp/rt_pixel_stats.bin"
     os.environ["RT_PIXEL_STATS"] = dump
+    argv = sys.argv[1:]
+    cfg = "dragon"
+    if "--config" in argv:
+        i = argv.index("--config")
+        cfg = argv[i + 1]
+        del argv[i:i + 2]
+    if "--lib" in argv:  # a diagnostics build (RT_PLAIN_PIXEL_STATS)
+        i = argv.index("--lib")
+        os.environ["RTMI_LIB"] = str(Path(argv[i + 1]).resolve())
+        del argv[i:i + 2]
     pt = ptload.load()
     sc = pt.scenes
-    W, H, sr = 1920, 1080, 16
+    W, H, sr = (1920, 1080, 16) if cfg == "dragon" else (1024, 1024, 1)
     rt = pt.RayTracer(0)
     rt.setSpheres(sc.ply_scene())
     c = sc.PLY_CAMERA
     rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
     rt.setSampleRate(sr)
     rt.setMaxPathDepth(6)
-    rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS["dragon"]))
+    rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS[cfg]))
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     rt.rayTrace(out, W, H, 0, kernel=2)  # probe + warm
     rt.rayTrace(out, W, H, 0, kernel=2)
@@ -62,9 +72,10 @@ def main():
            "dur_pct": {p: float(np.percentile(dur, p)) for p in (50, 90, 99, 99.9, 100)},
            "queries_pct": {p: float(np.percentile(q, p)) for p in (50, 90, 99, 100)},
            "pixels_running_at_pct_of_span": {}}
-    for f in (0.5, 0.7, 0.8, 0.9, 0.95, 0.99):
+    for f in (0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9, 0.95, 0.99):
         t = f * end
         res["pixels_running_at_pct_of_span"][f] = int(((start <= t) & (fin > t)).sum())
+    res["started_pct"] = {p: float(np.percentile(start, p)) for p in (50, 90, 99, 100)}
     # the 20 last finishers
     idx = np.argsort(fin.ravel())[-20:]
     res["last"] = [{"x": int(i % W), "y": int(i // W), "start": round(float(start.ravel()[i]), 2),
@@ -78,8 +89,8 @@ def main():
     res["light_dur_pct"] = {p: float(np.percentile(dur[~heavy], p)) for p in (10, 50, 90, 100)}
     txt = json.dumps(res, indent=1)
     print(txt)
-    if len(sys.argv) > 1:
-        Path(sys.argv[1]).write_text(txt + "\n")
+    if argv:
+        Path(argv[0]).write_text(txt + "\n")
 
 
 if __name__ == "__main__":

@@ -87,6 +87,8 @@ constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
 #define RT_SEED_GRID_ITEMS 1
 #endif
 constexpr uint32_t kFetchK = RT_FETCH_K;
+constexpr uint64_t kShortFrameSamplesPerLane = 8; /* below: a short frame (fewer blocks per CU) */
+constexpr int kShortFrameBlocksPerCU = 3;
 /* an unsigned environment knob (tuning sweeps), `def` when unset or unparsable */
 uint32_t env_u32(const char *name, uint32_t def)
 {
@@ -1026,6 +1028,12 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         int r = grid_blocks(c, trav, c->counting, RT_FORM_PLAIN, &blocks);
         if (r != RT_OK) return r;
         blocks = std::max(1, (int)std::min<uint64_t>((uint64_t)blocks, item_blocks));
+        /* a short frame — a few samples per resident lane (bunny class at 1 spp: 3.2) — runs on
+           3 of the 5 blocks per CU: its time is then its costliest pixels' serial paths, which step
+           faster on less crowded SIMDs (bunny class 0.54 -> 0.46 ms at 768 of 1280 blocks; the
+           dragon frame at 1024 blocks 96.7 -> 101.2 ms: profiles/r04l, r04m) */
+        if ((uint64_t)W * hl * c->sample_rate * c->sample_rate < kShortFrameSamplesPerLane * (uint64_t)blocks * RT_BLOCK)
+            blocks = std::max(1, blocks * kShortFrameBlocksPerCU / RT_TRIS_WAVES);
         if (const uint32_t gb = env_u32("RTMI_GRID_BLOCKS", 0)) blocks = std::min(blocks, (int)gb);
         if (trav == RT_TRAV_BVH4Q) {
             r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
@@ -1042,9 +1050,9 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         }
         a.spill = c->d_spill;
         a.fetch_k = env_u32("RTMI_FETCH_K", kFetchK); /* tuning knobs (profiles/bunny_sweep.py) */
-        a.fetch_k_box = a.fetch_k;
+        a.fetch_k_box = env_u32("RTMI_FETCH_K_BOX", a.fetch_k);
         a.fetch_frac = env_u32("RTMI_FETCH_FRAC", kFetchFrac);
-        a.box_exit = 0;
+        a.box_exit = env_u32("RTMI_BOX_EXIT", 0);
         a.probe_n = probe_n(c->sample_rate);
         a.diag_pixel = 0xffffffffu;
 #if RT_DIAG_ONE_PIXEL

@@ -873,7 +873,6 @@ __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3
    stack, the nearest becomes the next node.  Returns false when none is hit. */
 __device__ __forceinline__ bool lane_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3, TravState &s, Stack &stk, V3 d)
 {
-    if (!RT_SEED_ROOT) return true; /* s.node = 0: the root, in a round */
     float t[4];
     int c[4];
     const int nh = node_children(r0, r1, r2, r3, s.inv, s.oi, d, s.best_t, false, false, t, c);
@@ -1053,7 +1052,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                                 running = false;
                                 fin = true;
                             }
-                        } else if (!lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
+                        } else if (RT_SEED_ROOT && !lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
                             running = false;
                             fin = true;
                         }
@@ -1102,7 +1101,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                                 }
                             } else {
                                 trav_begin(ts, stk, qo, qd, kInf);
-                                if (!lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
+                                if (RT_SEED_ROOT && !lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
                                     running = false;
                                     fin = true;
                                 }

@@ -1,9 +1,10 @@
 """Sweep k_tris's stepping knobs on one context (GPU box): for each setting the frame's kernel
-time (median of --reps renders) with RTMI_FETCH_K / RTMI_FETCH_FRAC / RTMI_GRID_BLOCKS set
+time (median of --reps renders) with RTMI_FETCH_K / RTMI_FETCH_FRAC / RTMI_GRID_BLOCKS /
+RTMI_BOX_EXIT / RTMI_FETCH_K_BOX set
 (rt_host.cpp reads them at every render).  Settings alternate round after round.
 
-    python profiles/bunny_sweep.py [--config bunny] [--reps 5] [--rounds 3] 24:24:0 16:24:0 ...
-    (K:FRAC:GRID; GRID 0 = the occupancy grid)
+    python profiles/bunny_sweep.py [--config bunny] [--reps 5] [--rounds 3] [--lib build.so] 24:24:0 16:24:0 ...
+    (K:FRAC:GRID[:BOXEXIT[:KBOX]]; GRID 0 = the host's grid, KBOX 0 = K)
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ def main():
     ap.add_argument("--config", default="bunny", choices=["bunny", "dragon"])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="another build of librtmi.so")
     args = ap.parse_args()
     import torch
     import ptload
@@ -31,7 +33,7 @@ def main():
     pt = ptload.load()
     sc = pt.scenes
     W, H, sr = (1024, 1024, 1) if args.config == "bunny" else (1920, 1080, 16)
-    rt = pt.RayTracer(0)
+    rt = pt.RayTracer(0, lib_path=args.lib)
     rt.setSpheres(sc.ply_scene())
     c = sc.PLY_CAMERA
     rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
@@ -46,10 +48,12 @@ def main():
     wall = {s: [] for s in args.settings}
     for r in range(args.rounds):
         for s in args.settings:
-            k, f, g = (s.split(":") + ["0", "0"])[:3]
+            k, f, g, bx, kb = (s.split(":") + ["0"] * 4)[:5]
             os.environ["RTMI_FETCH_K"] = k
             os.environ["RTMI_FETCH_FRAC"] = f
             os.environ["RTMI_GRID_BLOCKS"] = g
+            os.environ["RTMI_BOX_EXIT"] = bx
+            os.environ["RTMI_FETCH_K_BOX"] = kb if kb != "0" else k
             rt.rayTrace(out, W, H, 0, kernel=pt.RayTracer.KERNEL_TRIS)  # settle
             for _ in range(args.reps):
                 t0 = time.perf_counter()

@@ -389,10 +389,18 @@ def main():
 
     cpu = gpu_linear = None
     if world == 1 and not args.no_cpu_baseline:
+        print("cpu baseline", file=sys.stderr, flush=True)
         cpu = cpu_baseline(pt, sc, W, H, sr, S, seeds0, Wp, Hp, kernel, args.cpu_seconds,
                            verts if n_tris else None, idx if n_tris else None, frame0, seeds_after0)
         if kernel == pt.RayTracer.KERNEL_TRIS and not args.linear and not args.no_linear_leg:
-            gpu_linear = gpu_linear_leg(rt, pt, W, H, Wp, Hp, seeds0, cpu)
+            # every query tests every triangle: ~3 queries per pixel at sampleRate 1, ~4e11 tests/s
+            # (r03: the dragon frame in 9.5 s); a leg past ~50 s (the Lucy class: ~1 h) is skipped
+            est_s = 3.0 * W * H * n_tris / 4e11
+            if est_s <= 50.0:
+                print(f"gpu linear leg (~{est_s:.0f} s)", file=sys.stderr, flush=True)
+                gpu_linear = gpu_linear_leg(rt, pt, W, H, Wp, Hp, seeds0, cpu)
+            else:
+                gpu_linear = {"skipped": f"~{est_s:.0f} s estimated for {W}x{H} x {n_tris} triangles per query"}
 
     line = {
         "metric": (METRIC_WEAK if frames_per_rank else METRIC) if cfg == "dragon" else CONFIG_METRIC.get(

@@ -1406,6 +1406,42 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
         np.testing.assert_array_equal(s, frames[0][1])
 
 
+def test_stepping_knobs_change_no_bits(tracer, pt, monkeypatch):
+    """k_tris's stepping-round exit rule and its grid are scheduling only: a short frame (1 spp,
+    so the short-frame grid of 3 blocks per CU) renders to the same bits and seeds with a grid of
+    7 blocks, with the round ending at every completed query, with it ending only when 64 have
+    completed (no live-lane rule), and with box-pixel waves leaving at their first completion
+    (RTMI_* knobs, read at every render)."""
+    sc = pt.scenes
+    W, H, sr = 256, 192, 1
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    seeds = sc.default_seeds(Wp, Hp, skip=3)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(sc.ply_scene())
+    c = sc.PLY_CAMERA
+    rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    knobs = ("RTMI_GRID_BLOCKS", "RTMI_FETCH_K", "RTMI_FETCH_FRAC", "RTMI_BOX_EXIT", "RTMI_FETCH_K_BOX")
+    frames = []
+    for env in ({}, {"RTMI_GRID_BLOCKS": "7"}, {"RTMI_FETCH_K": "1"}, {"RTMI_FETCH_K": "64", "RTMI_FETCH_FRAC": "0"},
+                {"RTMI_BOX_EXIT": "1", "RTMI_FETCH_K_BOX": "3"}):
+        for k in knobs:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        rt.setSeeds(Wp, Hp, seeds)
+        out = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        frames.append((bits(out).copy(), rt.getSeeds().copy()))
+    rt.close()
+    for f, s in frames[1:]:
+        np.testing.assert_array_equal(f, frames[0][0])
+        np.testing.assert_array_equal(s, frames[0][1])
+
+
 def test_sample_split_at_full_size(tracer, pt, monkeypatch):
     """Sample-split rendering on the dragon-class frame at full size, sampleRate 16 (16 chunks
     of 16 samples), as a row-stripe tile of 8 (259k pixels: fewer than the resident lanes):

@@ -218,6 +218,10 @@ typedef struct rt_render_info {
     uint32_t split_guard;      /* read after completion: a defect guard of the long chains' seed pass
                                   fired (record index out of range, group stack overflow, query round
                                   bound); rt_synchronize then fails with RT_ERR_STATE */
+    uint32_t split_spec;       /* 1: the mesh pixels' chunk seeds were jumped ahead from their frame
+                                  seeds (no seed pass for them; pixels near a silhouette run as long chains) */
+    uint32_t split_repaired;   /* read after completion: speculated pixels whose camera rays missed the
+                                  mesh after all, re-rendered by the repair pass (seed pass + chunks) */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
 /* The long chains of the last sample-split render (pixels_long of them: tile-local y * W + x, the

@@ -125,6 +125,8 @@ class RtRenderInfo(ctypes.Structure):
         ("split_chunks", ctypes.c_uint32),
         ("split_coop", ctypes.c_uint32),
         ("split_guard", ctypes.c_uint32),
+        ("split_spec", ctypes.c_uint32),
+        ("split_repaired", ctypes.c_uint32),
     ]
 
 

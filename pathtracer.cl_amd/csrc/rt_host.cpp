@@ -159,6 +159,14 @@ struct rt_ctx {
     uint32_t n_split_box = 0;
     int split_box_grid = 0;           /* the box pixels' seed-pass grid of the render being launched */
     hipStream_t stream2 = nullptr;    /* the box pixels' seed pass and chunks, beside the mesh pixels' */
+    /* speculated mesh pixels (RT_SPLIT_SPEC, default on): their chunk seeds jumped ahead from the
+       frame seeds; a per-pixel mark and the list of the pixels to repair */
+    int split_spec = 1;
+    uint32_t *d_split_dirty = nullptr, *d_split_repair = nullptr;
+    size_t split_dirty_px = 0;
+    uint32_t *d_spec_mul = nullptr;   /* per chunk: the two generators' jump multipliers */
+    std::vector<uint32_t> h_spec_mul; /* their host copy (the upload's source; re-uploaded on change) */
+    uint64_t spec_mul_key = ~0ull;
     hipEvent_t ev_split0 = nullptr, ev_box = nullptr;
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
@@ -470,6 +478,56 @@ int split_box_blocks(const rt_ctx *c, uint32_t width, int full_grid)
     return n;
 }
 
+/* Speculated mesh pixels: every mesh pixel's sample draws 2 + 2 x lights random
+   numbers, so chunk c starts c x chunk x D draws after the frame seed; per chunk the jump
+   multipliers A^(c chunk D) mod A 2^16 - 1 of the two MWC generators (rng.h:9-47), computed here
+   and uploaded when they change; the per-pixel marks are cleared for the render. */
+uint32_t powmod(uint64_t a, uint64_t e, uint64_t m)
+{
+    uint64_t r = 1 % m;
+    a %= m;
+    while (e) {
+        if (e & 1u) r = r * a % m;
+        a = a * a % m;
+        e >>= 1;
+    }
+    return (uint32_t)r;
+}
+
+int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
+{
+    const uint32_t draws = 2u + 2u * (uint32_t)c->lights.size();
+    const uint64_t key = (uint64_t)a.split_chunks << 40 | (uint64_t)a.split_chunk << 20 | draws;
+    if (!c->d_spec_mul) HIPCHK(c, hipMalloc(&c->d_spec_mul, 2 * 64 * sizeof(uint32_t)));
+    if (a.split_chunks > 64) return fail(c, RT_ERR_ARG, "speculated split: more than 64 chunks");
+    if (key != c->spec_mul_key) {
+        c->h_spec_mul.assign(2 * 64, 1u);
+        for (uint32_t ch = 0; ch < a.split_chunks; ++ch) {
+            const uint64_t k = (uint64_t)ch * a.split_chunk * draws;
+            c->h_spec_mul[2 * ch] = powmod(36969u, k, 36969ull * 65536u - 1u);
+            c->h_spec_mul[2 * ch + 1] = powmod(18000u, k, 18000ull * 65536u - 1u);
+        }
+        HIPCHK(c, hipMemcpy(c->d_spec_mul, c->h_spec_mul.data(), 2 * 64 * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->spec_mul_key = key;
+    }
+    if (c->split_dirty_px < npx) {
+        free_dev(c->d_split_dirty);
+        free_dev(c->d_split_repair);
+        c->d_split_dirty = c->d_split_repair = nullptr;
+        c->split_dirty_px = 0;
+        HIPCHK(c, hipMalloc(&c->d_split_dirty, npx * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc(&c->d_split_repair, npx * sizeof(uint32_t)));
+        c->split_dirty_px = npx;
+    }
+    HIPCHK(c, hipMemsetAsync(c->d_split_dirty, 0, npx * sizeof(uint32_t), st));
+    a.split_spec = 1;
+    a.split_spec_draws = draws;
+    a.split_spec_mul = c->d_spec_mul;
+    a.split_dirty = c->d_split_dirty;
+    a.split_repair = c->d_split_repair;
+    return RT_OK;
+}
+
 /* A sample-split render: the box pixels' seed pass and then their chunks on stream2, beside
    the mesh pixels' seed pass and chunks on the render stream (the box pixels' chains are the
    long ones: they overlap the rest of the frame instead of preceding it); then the in-order
@@ -497,9 +555,29 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     }
     RtTriLaunch m = a; /* the mesh pixels' seed pass: short chains, one lane each */
     m.split_coop = 0;
-    int e = rt_launch_split_seeds(m, st);
+    int e = a.split_spec ? 0 : rt_launch_split_seeds(m, st); /* speculated: no seed pass */
     if (!e) e = rt_launch_tris(m, RT_TRAV_BVH4Q, c->counting, blocks, st);
     if (e) return e;
+    if (a.split_spec) {
+        /* the repair pass: the speculated pixels a camera ray of which missed the mesh, as long
+           chains (seed pass, then every chunk), their count read on the device (usually none:
+           the grids find no item and end) */
+        RtTriLaunch r = a;
+        r.split_spec = 0;
+        r.split_which = RT_SPLIT_BOX;
+        r.split_box = a.split_repair;
+        r.split_n_box = 0;
+        r.split_n_dev = reinterpret_cast<const uint32_t *>(a.counters + RT_CNT_REPAIR);
+        r.split_counter = a.split_counter + 48;
+        r.work_counter = a.work_counter + 48;
+        r.split_gpw = c->split_gpw;
+        r.split_seed_blocks = 16;
+        r.split_chunk = a.split_fine;
+        r.split_chunks = (a.sample_rate * a.sample_rate + r.split_chunk - 1u) / r.split_chunk;
+        e = rt_launch_split_seeds(r, st);
+        if (!e) e = rt_launch_tris(r, RT_TRAV_BVH4Q, c->counting, 64, st);
+        if (e) return hip_fail(c, (hipError_t)e, "repair launches");
+    }
     if (n_box) HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0));
     return rt_launch_split_finish(a, st);
 }
@@ -526,7 +604,8 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     const uintptr_t np = reinterpret_cast<uintptr_t>(a.nodes);
     std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
                                  (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks,
-                                 c->sample_rate, (uint32_t)(c->split + 1), (uint32_t)trav_kind(c), (uint32_t)np,
+                                 c->sample_rate, (uint32_t)(c->split + 1) | (uint32_t)c->split_spec << 8,
+                                 (uint32_t)trav_kind(c), (uint32_t)np,
                                  (uint32_t)((uint64_t)np >> 32)};
     const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
@@ -574,7 +653,10 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
     e = rt_sched_order(c->sched, c->d_flags, W, hl, pn2, (uint32_t)c->lights.size(), c->max_depth, c->d_order, st);
     if (e) return hip_fail(c, (hipError_t)e, "tile order");
-    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? 96u * pn2 : 0u, st);
+    /* speculated mesh pixels: the silhouettes' neighbours run as long chains (RT_SPLIT_SPEC=2: every
+       probe-hit pixel speculated — a test knob that makes repairs happen) */
+    const uint32_t spec_row = split && c->split_spec == 1 ? W : 0u;
+    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? 96u * pn2 : 0u, spec_row, st);
     if (e) return hip_fail(c, (hipError_t)e, "box-pixel scan");
     uint32_t n_box = 0;
     if (split) { /* every long chain gets a slot: their seed pass and chunks run on a stream of their own */
@@ -633,6 +715,7 @@ int rt_create(int device, rt_ctx **out)
     if (const char *sch = getenv("RT_SCHEDULE")) c->schedule = std::string(sch) != "0";
     if (const char *v = getenv("RT_SPLIT_MB")) c->split_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
+    if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -664,6 +747,9 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_split_seed);
     free_dev(c->d_split_col);
     free_dev(c->d_split_counter);
+    free_dev(c->d_split_dirty);
+    free_dev(c->d_split_repair);
+    free_dev(c->d_spec_mul);
     free_dev(c->d_split_box);
     if (c->ev_split0) (void)hipEventDestroy(c->ev_split0);
     if (c->ev_box) (void)hipEventDestroy(c->ev_box);
@@ -1108,6 +1194,10 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 /* a round of 4 nodes adds at most 12 entries and a one-item depth-first walk at
                    most the tree's worst stack: rounds take 4 items up to this depth (coop_round) */
                 a.coop_multi_sp = std::max(0, (int)RT_COOP_STACK - 12 - (int)c->bvh.stack4);
+                if (c->split_spec && a.split_which == RT_SPLIT_MESH) {
+                    const int rs = spec_setup(c, a, npx_s, st);
+                    if (rs != RT_OK) return rs;
+                }
                 /* the box pixels' seed pass (one lane per pixel) keeps its blocks resident beside
                    the mesh pixels' kernels, whose grids leave room for it */
                 const int box_blocks = c->n_split_box ? split_box_blocks(c, std::max(1u, a.split_coop), blocks) : 0;
@@ -1255,6 +1345,7 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
         c->info.pixels_long = c->last_long;
         c->info.split_chunks = a.split_chunks;
         c->info.split_coop = a.split_chunks && a.split_n_box ? a.split_coop : 0u;
+        c->info.split_spec = a.split_chunks ? a.split_spec : 0u;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
         c->info_list_pending = lists;
@@ -1337,6 +1428,7 @@ int rt_synchronize(rt_ctx *c)
     c->last.pixel_rays_max = h[11];
     c->last.pixel_steps_max = h[12];
     c->last.pixels_long = c->last_long;
+    c->info.split_repaired = (uint32_t)h[RT_CNT_REPAIR];
     if (h[RT_CNT_GUARD]) { /* a defect guard of the long chains' seed pass: the frame is not the reference's */
         c->info.split_guard = (uint32_t)h[RT_CNT_GUARD];
         char msg[160];

@@ -54,10 +54,12 @@
 #define RT_N_COUNTERS 13
 #define RT_CNT_SKIPPED 8
 #define RT_CNT_SHADE 9
-/* one word past the counters: the long chains' seed-pass defect guards (atomicOr of RT_GUARD_*);
-   the device counter buffer holds RT_COUNTER_WORDS words */
+/* past the counters: the long chains' seed-pass defect guards (atomicOr of RT_GUARD_*), then the
+   count of speculated pixels to repair (sample-split renders, split_spec); the device counter
+   buffer holds RT_COUNTER_WORDS words */
 #define RT_CNT_GUARD RT_N_COUNTERS
-#define RT_COUNTER_WORDS (RT_N_COUNTERS + 1)
+#define RT_CNT_REPAIR (RT_N_COUNTERS + 1)
+#define RT_COUNTER_WORDS (RT_N_COUNTERS + 2)
 enum { RT_GUARD_INDEX = 1, RT_GUARD_STACK = 2, RT_GUARD_ROUNDS = 4 };
 
 /* One BVH node = 4 x float4 = 64 B (both children's boxes in the parent):
@@ -185,6 +187,19 @@ struct RtTriLaunch {
     uint32_t split_gpw;       /* seed pass: queries (chains) per wave, 0 = all lanes / groups */
     int32_t coop_multi_sp;    /* cooperative seed pass: rounds take 4 stack items while the group's stack holds
                                  at most this many entries, else one (coop_round) */
+    /* Speculated mesh pixels: a mesh pixel whose every camera ray hits the mesh
+       draws exactly split_spec_draws random numbers per sample (two for the camera ray, two per
+       light), so its chunks' first seeds follow from its frame seed by jumping each MWC
+       generator ahead (x_{n+k} = a^k x_n mod a 2^16 - 1) — no seed pass.  A chunk that meets a
+       camera ray missing the mesh marks the pixel (split_dirty) and lists it (split_repair,
+       counted in counters[RT_CNT_REPAIR]) for a repair pass: the long chains' seed pass and
+       chunks over that list, whose length they read from split_n_dev. */
+    uint32_t split_spec;          /* RT_SPLIT_MESH: the mesh pixels' chunk seeds by jump-ahead */
+    uint32_t split_spec_draws;    /* random numbers per sample of a speculated pixel */
+    const uint32_t *split_spec_mul; /* per chunk c: a_x^(c chunk D) mod m_x, a_y^(c chunk D) mod m_y */
+    uint32_t *split_dirty;        /* per pixel: 1 once a speculated chunk saw a camera ray miss */
+    uint32_t *split_repair;       /* the marked pixels (yl * W + x) */
+    const uint32_t *split_n_dev;  /* RT_SPLIT_BOX: the item count from device memory (NULL: split_n_box) */
 };
 enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
 #define RT_COOP_STACK (RT_STACK_DEPTH * 4) /* LDS stack entries of a 4-lane query group (k_split_seeds) */
@@ -251,8 +266,10 @@ struct RtSchedScratch {
 void rt_sched_free(RtSchedScratch &s);
 int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_t hl, uint32_t pn2, uint32_t n_lights,
                    uint32_t max_depth, uint32_t *order, void *stream);
+/* row > 0 (speculated mesh pixels): the tile's width; the neighbours of a pixel whose probe missed
+   the mesh are flagged too */
 int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, uint32_t step_max,
-                      void *stream);
+                      uint32_t row, void *stream);
 int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *slot_pixel,
                       void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed

@@ -902,7 +902,8 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
-    const uint32_t n_items = a.split_which == RT_SPLIT_BOX ? a.split_n_box : tiles_x * tiles_y * 64u;
+    const uint32_t n_items = a.split_which == RT_SPLIT_BOX ? (a.split_n_dev ? *a.split_n_dev : a.split_n_box)
+                                                           : tiles_x * tiles_y * 64u;
     const uint32_t nl = a.n_lights;
     const float hw = uniform_f(((float)a.W) / 2.0f);
     const float hh = uniform_f(((float)a.H) / 2.0f);
@@ -1158,6 +1159,29 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     }
 }
 
+/* One MWC generator of frand (rng.h:9-47: x = A (x & 0xffff) + (x >> 16)) advanced by k draws.
+   With M = A 2^16 - 1 the step is x -> A x mod M on the states below M (the step keeps them
+   there; a fresh seed at or above M gets there within 2 steps, M itself is a fixed point), so
+   k draws are one multiplication by A^k mod M (`mul`, from the host); a^-1 = 2^16 mod M undoes
+   the canonicalising steps.  Small k: the steps themselves. */
+template <uint32_t A>
+__device__ __forceinline__ uint32_t mwc_jump(uint32_t x, uint32_t k, uint32_t mul)
+{
+    constexpr uint32_t M = A * 65536u - 1u;
+    if (k <= 16u) {
+        for (uint32_t i = 0; i < k; ++i) x = A * (x & 65535u) + (x >> 16);
+        return x;
+    }
+    uint32_t k0 = 0;
+    while (x > M) { /* at most 2 steps (every 32-bit state checked) */
+        x = A * (x & 65535u) + (x >> 16);
+        ++k0;
+    }
+    if (x == M) return M;
+    for (uint32_t i = 0; i < k0; ++i) mul = (uint32_t)(((unsigned long long)mul * 65536u) % M);
+    return (uint32_t)(((unsigned long long)x * mul) % M);
+}
+
 /* ======================================================================== */
 /* Triangle kernel: raytrace_tris + trace_path_tri (rtcommon.h:371-470).     */
 
@@ -1228,7 +1252,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const uint32_t tiles_y = (a.Hl + 7u) >> 3;
     const uint32_t n_items = tiles_x * tiles_y * 64u;
     const uint32_t n_tasks =
-        SPLIT ? (a.split_which == RT_SPLIT_BOX ? a.split_n_box : n_items) * a.split_chunks : n_items;
+        SPLIT ? (a.split_which == RT_SPLIT_BOX ? (a.split_n_dev ? *a.split_n_dev : a.split_n_box) : n_items) * a.split_chunks
+              : n_items;
     /* launch-uniform values pinned to SGPRs (readfirstlane), so they neither occupy nor
        spill vector registers */
     const float hw = uniform_f(((float)a.W) / 2.0f);
@@ -1298,6 +1323,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                     tri_hit = true;
                 } else {
+                    if (SPLIT && depth == 0 && a.split_spec && a.split_which == RT_SPLIT_MESH &&
+                        sample / a.split_chunk + 1u < a.split_chunks) {
+                        /* a speculated pixel's camera ray missed the mesh: its later chunks started
+                           from wrong seeds — listed once for the repair pass (rare path) */
+                        const uint32_t p = yl * a.W + x;
+                        if (atomicExch(a.split_dirty + p, 1u) == 0u)
+                            a.split_repair[(uint32_t)atomicAdd(a.counters + RT_CNT_REPAIR, 1ull)] = p;
+                    }
                     /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
                     const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
                     if (hd > RT_SMALL_F && hd < kInf) {
@@ -1405,6 +1438,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 dst[2] = col_z;
                 ++sample;
                 mode = (sample >= spp || sample % a.split_chunk == 0u) ? M_IDLE : M_NEWSAMPLE;
+                if (sample >= spp) /* the pixel's final seed, from its last chunk's own draws */
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + a.split_nseed - 1u] =
+                        make_uint2(seed.x, seed.y);
                 if (mode == M_IDLE) {
                     pclass = -1;
                     if (COUNT && a.pixel_stats) { /* diagnostics: the pixel's queries and steps over its chunks */
@@ -1525,11 +1561,20 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         take = take && (x >> 3) == (dx >> 3) && (yl >> 3) == (dy >> 3) && ((in - in0) & 63u) < a.diag_k;
                     }
                     if (take) s_list[threadIdx.x] = list_pack(a, x, yl, tiles_x);
-                    if (SPLIT && take) { /* the chunk's first seed, from the seed pass */
+                    if (SPLIT && take && a.split_spec && a.split_which == RT_SPLIT_MESH) {
+                        /* a speculated mesh pixel: the chunk's first seed jumped ahead from the
+                           frame seed (split_spec_draws numbers per sample before it) */
+                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                        const uint32_t k = chunk * a.split_chunk * a.split_spec_draws;
+                        seed.x = mwc_jump<36969u>(a.seeds[slot], k, a.split_spec_mul[2 * chunk]);
+                        seed.y = mwc_jump<18000u>(a.seeds[plane + slot], k, a.split_spec_mul[2 * chunk + 1]);
+                    } else if (SPLIT && take) { /* the chunk's first seed, from the seed pass */
                         const uint2 sd = reinterpret_cast<const uint2 *>(
                             a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + chunk * a.split_chunk / a.split_fine];
                         seed.x = sd.x;
                         seed.y = sd.y;
+                    }
+                    if (SPLIT && take) {
                         sample = chunk * a.split_chunk;
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
                         mode = M_NEWSAMPLE;

@@ -93,12 +93,25 @@ __global__ __launch_bounds__(256) void k_tile_cost(const uint32_t *__restrict__ 
    than step_max steps in all (a long chain on the mesh: grazing camera rays without a candidate
    list); box[npx] = 0 (the scan's total) */
 __global__ __launch_bounds__(256) void k_box_flags(const uint32_t *__restrict__ flags, uint32_t npx, uint32_t pn2,
-                                                   uint32_t step_max, uint32_t *__restrict__ box)
+                                                   uint32_t step_max, uint32_t row, uint32_t *__restrict__ box)
 {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p < npx) {
         const uint32_t v = flags[p];
-        box[p] = (v >> RT_PROBE_HIT_SHIFT) < pn2 || (step_max && (v & RT_PROBE_STEP_MASK) > step_max) ? 1u : 0u;
+        bool b = (v >> RT_PROBE_HIT_SHIFT) < pn2 || (step_max && (v & RT_PROBE_STEP_MASK) > step_max);
+        if (row && !b) {
+            /* speculated mesh pixels (row = the tile's width): a pixel next to one whose probe
+               missed the mesh (a silhouette) runs as a long chain instead — its camera rays may
+               miss too, and a speculated pixel that does costs a repair */
+            const uint32_t x = p % row, y = p / row, rows = npx / row;
+            for (int dy = -1; dy <= 1 && !b; ++dy)
+                for (int dx = -1; dx <= 1 && !b; ++dx) {
+                    const int xx = (int)x + dx, yy = (int)y + dy;
+                    if (xx < 0 || yy < 0 || xx >= (int)row || yy >= (int)rows) continue;
+                    b = (flags[(uint32_t)yy * row + (uint32_t)xx] >> RT_PROBE_HIT_SHIFT) < pn2;
+                }
+        }
+        box[p] = b ? 1u : 0u;
     } else if (p == npx) {
         box[p] = 0u;
     }
@@ -197,10 +210,11 @@ int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_
 }
 
 int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, uint32_t step_max,
-                      void *stream)
+                      uint32_t row, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_box_flags, dim3((npx + 1u + 255u) / 256u), dim3(256), 0, st, flags, npx, pn2, step_max, s.box);
+    hipLaunchKernelGGL(k_box_flags, dim3((npx + 1u + 255u) / 256u), dim3(256), 0, st, flags, npx, pn2, step_max, row,
+                       s.box);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     size_t bytes = s.tmp_bytes;

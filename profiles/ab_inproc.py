@@ -5,11 +5,13 @@ alternate between the libraries round after round, so clock and neighbour drift
 hit all variants alike.  Prints per-variant median / min kernel ms.
 
     python profiles/ab_inproc.py LABEL=path.so LABEL=path.so ... [--rounds 8] [--config dragon] [--tile 8,8,0]
+                                 [--env NAME=VALUE ...]
     (LABEL= with an empty path: the in-tree build)
 """
 from __future__ import annotations
 
 import argparse
+import os
 import statistics
 import sys
 from pathlib import Path
@@ -24,7 +26,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--config", default="dragon", choices=["dragon", "bunny", "lucy"])
     ap.add_argument("--tile", default=None, help="stripe,n_ranks,rank: time one rank's row-stripe tile")
+    ap.add_argument("--env", action="append", default=[], help="NAME=VALUE set before the contexts are created")
     args = ap.parse_args()
+    for kv in args.env:
+        k, _, v = kv.partition("=")
+        os.environ[k] = v
     tile = tuple(int(v) for v in args.tile.replace(":", ",").split(",")) if args.tile else None
     import numpy as np
     import torch

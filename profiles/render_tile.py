@@ -4,6 +4,7 @@ kernel traces (rocprofv3 --kernel-trace --stats) of one launch form; RT_* knobs 
     python profiles/render_tile.py [--config dragon] [--tile 8,8,0] [--reps 3] [--lib build.so]
 """
 import argparse
+import os
 import sys
 from pathlib import Path
 
@@ -17,7 +18,11 @@ def main():
     ap.add_argument("--tile", default=None)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--lib", default=None, help="another build of librtmi.so (A/B)")
+    ap.add_argument("--env", action="append", default=[], help="NAME=VALUE set before the context is created")
     args = ap.parse_args()
+    for kv in args.env:
+        k, _, v = kv.partition("=")
+        os.environ[k] = v
     import torch
     import ptload
 

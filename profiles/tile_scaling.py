@@ -39,7 +39,7 @@ def main():
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     res = {}
     for n in (1, 2, 4, 8):
-        times = []
+        times, repaired, longc = [], [], []
         for r in range(n):  # every rank's tile: the slowest sets the N-GPU frame time
             tile = (args.stripe, n, r) if n > 1 else None
             best = 1e9
@@ -47,8 +47,13 @@ def main():
                 rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
                 best = min(best, rt.lastKernelMs())
             times.append(best)
+            info = rt.renderInfo()
+            repaired.append(int(info.get("split_repaired", 0)))
+            longc.append(int(info.get("pixels_long", 0)))
+        info = rt.renderInfo()
         res[n] = {"max_ms": max(times), "min_ms": min(times), "ranks_timed": len(times),
-                  "rank_ms": [round(t, 3) for t in times], "split_chunks": rt.renderInfo().get("split_chunks", 0)}
+                  "rank_ms": [round(t, 3) for t in times], "split_chunks": info.get("split_chunks", 0),
+                  "split_spec": info.get("split_spec", 0), "long_chains": longc, "repaired": repaired}
     # the costliest pixel (counting launch with per-pixel stats, RT_PIXEL_STATS): queries and traversal
     # steps; in a sample-split tile a pixel's samples run as chunk tasks, whose counts add up per pixel
     # (the seed pass's rounds are reported apart)

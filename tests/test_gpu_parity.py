@@ -612,8 +612,9 @@ def _pixel_seeds(seeds, pix, Wp, Hp, W):
 def test_dragon_headline_config_vs_oracle(tracer, pt, oracle):
     """The benchmark's own configuration (BASELINE config 4: 871k tris, 1920x1080,
     sampleRate 16 = 256 samples per pixel with strat_rand total = 16, maxDepth 6,
-    raytracer.cl:184-243): a strided subset of 24 pixels (mesh and box pixels) and their
-    seed slots are bit-exact against the oracle's linear loop."""
+    raytracer.cl:184-243): a strided subset of 64 pixels (mesh, silhouette and box pixels) and
+    their seed slots are bit-exact against the oracle's linear loop (16 oracle threads: about a
+    minute on the GPU box)."""
     sc = pt.scenes
     W, H, sr = 1920, 1080, 16
     Wp, Hp = sc.padded_dims(W, H)
@@ -631,7 +632,7 @@ def test_dragon_headline_config_vs_oracle(tracer, pt, oracle):
     out = np.zeros(W * H * 4, np.float32)
     rt.rayTrace(out, W, H, 0, kernel=2)
     s_gpu = rt.getSeeds()
-    pix = np.arange(4_321, W * H, 86_399, dtype=np.uint32)  # 24 pixels over the frame
+    pix = np.arange(4_321, W * H, 32_399, dtype=np.uint32)  # 64 pixels over the frame
     exp = np.zeros_like(out)
     sd = seeds.copy()
     oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=pix)
@@ -1129,6 +1130,8 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
         assert info["split_chunks"] == (spp + csz - 1) // csz
         # the long chains ran on their own stream with the 4-lane cooperative seed pass (coop_round)
         assert info["pixels_long"] > 0 and info["split_coop"] == 4 and info["split_guard"] == 0, info
+        # the mesh pixels' chunk seeds jumped ahead from their frame seeds (no seed pass for them)
+        assert info["split_spec"] == 1, info
         assert len(rt.longChains()) == info["pixels_long"]
         oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, p, sd, verts, idx)
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
@@ -1145,6 +1148,46 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
     assert info["split_chunks"] > 0 and info["pixels_long"] > 0 and info["split_coop"] == 4, info
     np.testing.assert_array_equal(bits(got), bits(exp.reshape(H, W, 4)[rows].reshape(-1)), err_msg="tile")
     np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg="tile seeds")
+    rt.close()
+
+
+@pytest.mark.parametrize("spec", ["2", "0"])
+def test_speculated_pixels_repaired_vs_oracle(pt, oracle, monkeypatch, spec):
+    """Speculated mesh pixels (their chunk seeds jumped ahead from the frame seed, DESIGN.md
+    §4.5) whose camera rays miss the mesh after all are repaired: with RT_SPLIT_SPEC=2 every
+    pixel whose probe rays all hit is speculated, silhouettes included, so some chunks meet a
+    camera ray that misses; those pixels are listed and re-rendered (seed pass + chunks) and the
+    frame and seeds equal the oracle bit for bit.  RT_SPLIT_SPEC=0 (no speculation, every mesh
+    pixel through the seed pass) equals it too."""
+    monkeypatch.setenv("RT_SPLIT", "1")
+    monkeypatch.setenv("RT_SPLIT_SPEC", spec)
+    sc = pt.scenes
+    W, H, sr = 128, 96, 8
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    seeds = sc.default_seeds(Wp, Hp, skip=5)
+    S = sc.ply_scene()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    rt = pt.RayTracer(0)
+    rt.setSpheres(S)
+    rt.setCamera(cam)
+    rt.setSampleRate(sr)
+    rt.setMaxPathDepth(6)
+    rt.setMesh(verts, idx)
+    rt.setSeeds(Wp, Hp, seeds)
+    got = np.zeros(W * H * 4, np.float32)
+    rt.rayTrace(got, W, H, 0, kernel=2)
+    info = rt.renderInfo()
+    assert info["split_chunks"] > 0 and info["split_guard"] == 0, info
+    if spec == "2":
+        assert info["split_spec"] == 1 and info["split_repaired"] > 0, info
+    else:
+        assert info["split_spec"] == 0 and info["split_repaired"] == 0, info
+    exp = np.zeros_like(got)
+    sd = seeds.copy()
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx)
+    np.testing.assert_array_equal(bits(got), bits(exp))
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
     rt.close()
 
 

@@ -177,6 +177,97 @@ static Res group(const Scene &s, V o, V d, float tmax, bool any, int G, bool sor
     return {rounds, rounds * G, items, hit};
 }
 
+
+/* existence query, one lane, nearest-first DFS: steps until the first accepted triangle (or the end) */
+static long seq_exist_from(const Scene &s, int root, V o, V d, bool &found)
+{
+    V inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    std::vector<Item> st;
+    st.push_back({root, 0.0f});
+    long steps = 0;
+    Item buf[64];
+    found = false;
+    while (!st.empty()) {
+        Item it = st.back();
+        st.pop_back();
+        if (it.code >= 0) {
+            ++steps;
+            int dummy = 0;
+            int k = children(s, it.code, o, inv, INFINITY, buf, dummy, false);
+            std::sort(buf, buf + k, [](const Item &a, const Item &b) { return a.tn > b.tn; });
+            for (int j = 0; j < k; ++j) st.push_back(buf[j]);
+        } else {
+            int enc = ~it.code, first = enc >> 3, cnt = (enc & 7) + 1;
+            for (int j = 0; j < cnt; ++j) {
+                ++steps;
+                float t;
+                if (mt(s.tris + 12 * (first + j), o, d, t) && !(t < 1e-4f)) {
+                    found = true;
+                    return steps;
+                }
+            }
+        }
+    }
+    return steps;
+}
+
+/* a cut of the tree into at most F items (nodes or leaf codes), expanded breadth-first */
+static std::vector<int> frontier(const Scene &s, int F)
+{
+    std::vector<int> cur{0};
+    for (;;) {
+        bool grew = false;
+        std::vector<int> nxt;
+        size_t i = 0;
+        for (; i < cur.size(); ++i) {
+            int c = cur[i];
+            if (c < 0) { nxt.push_back(c); continue; }
+            const float *f = s.n4 + 32 * c;
+            std::vector<int> ch;
+            for (int k = 0; k < 4; ++k) {
+                int v;
+                memcpy(&v, &f[24 + k], 4);
+                if (v != RT_EMPTY_CHILD) ch.push_back(v);
+            }
+            size_t rest = cur.size() - i - 1;
+            if (nxt.size() + ch.size() + rest <= (size_t)F) {
+                for (int v : ch) nxt.push_back(v);
+                grew = true;
+            } else {
+                nxt.push_back(c);
+            }
+        }
+        cur = nxt;
+        if (!grew) return cur;
+    }
+}
+
+/* subtree-parallel existence: lane l walks subtree frontier[l] alone (after a box test of its
+   root from registers); the query ends at the first round some lane accepts, else when all end */
+static long subtree_exist(const Scene &s, const std::vector<int> &fr, V o, V d, bool &found)
+{
+    long best_hit = -1, longest = 0;
+    for (int c : fr) {
+        bool f = false;
+        long n;
+        if (c >= 0) n = seq_exist_from(s, c, o, d, f);
+        else {
+            /* a leaf item: its triangles one per step */
+            int enc = ~c, first = enc >> 3, cnt = (enc & 7) + 1;
+            n = 0;
+            for (int j = 0; j < cnt && !f; ++j) {
+                ++n;
+                float t;
+                if (mt(s.tris + 12 * (first + j), o, d, t) && !(t < 1e-4f)) f = true;
+            }
+        }
+        if (f && (best_hit < 0 || n < best_hit)) best_hit = n;
+        longest = std::max(longest, n);
+    }
+    found = best_hit >= 0;
+    return found ? best_hit : longest;
+}
+
 int main(int argc, char **argv)
 {
     uint32_t n_tris = argc > 1 ? (uint32_t)atoi(argv[1]) : 871414;
@@ -199,10 +290,26 @@ int main(int argc, char **argv)
     double seq_c = 0, seq_s = 0;
     double g_r[4][4] = {}, g_slots[4][4] = {}, g_items[4][4] = {};
     int hits_c = 0, n_c = 0, n_s = 0;
+    const int Fs[] = {1, 4, 8, 16, 32, 64};
+    std::vector<std::vector<int>> frs;
+    for (int F : Fs) frs.push_back(frontier(s, F));
+    double ex_steps[6] = {}, ex_hit_steps[6] = {};
+    long ex_n = 0, ex_hits = 0;
     auto run_query = [&](V o, V d, float tmax, bool any, int &hit_out) {
         Res r0 = seq(s, o, d, tmax, any);
         hit_out = r0.hit;
         if (!any) {
+            bool f0 = false;
+            for (int fi = 0; fi < 6; ++fi) {
+                bool f = false;
+                long n = subtree_exist(s, frs[fi], o, d, f);
+                if (fi == 0) f0 = f;
+                else if (f != f0) fprintf(stderr, "existence mismatch F %d\n", Fs[fi]);
+                ex_steps[fi] += n;
+                if (f) ex_hit_steps[fi] += n;
+            }
+            ++ex_n;
+            ex_hits += f0;
             seq_c += r0.rounds;
             ++n_c;
             hits_c += r0.hit >= 0;
@@ -276,6 +383,11 @@ int main(int argc, char **argv)
     int nq = n_c + n_s;
     printf("queries: %d closest (%.1f%% hit the mesh), %d shadow\n", n_c, 100.0 * hits_c / n_c, n_s);
     printf("seq: %.2f steps per closest, %.2f per shadow, %.2f mean\n", seq_c / n_c, seq_s / n_s, (seq_c + seq_s) / nq);
+    printf("existence queries %ld (%.1f%% find a triangle)\n", ex_n, 100.0 * ex_hits / ex_n);
+    for (int fi = 0; fi < 6; ++fi)
+        printf("subtree lanes F=%2d (cut of %zu items): %.2f steps per query (hit queries %.2f, miss %.2f)\n", Fs[fi],
+               frs[fi].size(), ex_steps[fi] / ex_n, ex_hit_steps[fi] / std::max(1L, ex_hits),
+               (ex_steps[fi] - ex_hit_steps[fi]) / std::max(1L, ex_n - ex_hits));
     const char *vn[4] = {"lane-order push", "sorted push", "lane-order + pop cull", "sorted + pop cull"};
     for (int gi = 0; gi < 4; ++gi)
         for (int v = 0; v < 4; ++v)

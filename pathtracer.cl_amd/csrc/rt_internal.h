@@ -272,6 +272,11 @@ int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, ui
                       uint32_t row, void *stream);
 int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *slot_pixel,
                       void *stream);
+/* Promotes pixels (pix[0..k)) that are still speculated mesh pixels (class -1) to long chains with
+   slots base, base + 1, ... (their count added to *count): the repaired pixels of the last frame of an
+   unchanged schedule run as long chains from the next frame on. */
+int rt_sched_promote(const uint32_t *pix, uint32_t k, uint32_t npx, uint32_t base, int32_t *cls, uint32_t *slot_pixel,
+                     uint32_t *count, void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed
    buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,

@@ -1159,6 +1159,338 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     }
 }
 
+/* ------------------------------------------------------------------------ */
+/* Subtree-parallel seed pass of the long chains (k_chain_seeds): G lanes per chain.  The seed
+   needs only WHETHER a segment meets the mesh (an accepted triangle anywhere), and that answer
+   is an OR over any cut of the tree: lane `sub` of a group owns edge `sub` of a fixed cut of the
+   tree's top levels (a child slot of a node — chain_cut, breadth first, at most G edges), tests
+   that child's box from an LDS copy of its parent's record when a query starts, and walks the
+   subtree below alone, depth first, with k_tris's one-record step (trav_step_q) and its own
+   stack; the query ends at the first step after which some lane of the group has accepted a
+   triangle, or when every lane's subtree is exhausted.  A camera ray with a candidate list
+   spreads the list's triangles over the lanes in runs of ceil(count / G).  The group's lanes
+   carry the chain's path state alike (the same values computed in every lane), so a path
+   advance costs one lane's instructions; the work of a query is split over G lanes without a
+   shared stack or an item assignment (coop_round's cost: DESIGN.md §4.5). */
+#ifndef RT_CHAIN_IMM
+#define RT_CHAIN_IMM 2 /* path-advance passes per iteration */
+#endif
+#ifndef RT_CHAIN_UNROLL
+#define RT_CHAIN_UNROLL 2 /* traversal steps per iteration */
+#endif
+
+/* child slot k of a compressed node against the ray, unsorted: node_children's box test for one
+   child (the same plane values: byte * 2^e * inv + (origin * inv - o * inv)) and the node's
+   determinant cull.  Culling only. */
+__device__ __forceinline__ bool edge_hit(uint4 q0, uint4 q1, uint4 q2, int k, V3 inv, V3 oi, V3 d)
+{
+    const uint32_t w = q0.w;
+    const float sx = __builtin_amdgcn_ldexpf(inv.x, (int)(w & 31u) + RT_QEXP_MIN);
+    const float sy = __builtin_amdgcn_ldexpf(inv.y, (int)((w >> 5) & 31u) + RT_QEXP_MIN);
+    const float sz = __builtin_amdgcn_ldexpf(inv.z, (int)((w >> 10) & 31u) + RT_QEXP_MIN);
+    const float bx = __builtin_fmaf(__uint_as_float(q0.x), inv.x, -oi.x);
+    const float by = __builtin_fmaf(__uint_as_float(q0.y), inv.y, -oi.y);
+    const float bz = __builtin_fmaf(__uint_as_float(q0.z), inv.z, -oi.z);
+    const bool px = inv.x >= 0.0f, py = inv.y >= 0.0f, pz = inv.z >= 0.0f;
+    const uint32_t sh = 8u * (uint32_t)k;
+    const float nbx = (float)(((px ? q1.x : q1.y) >> sh) & 255u), fbx = (float)(((px ? q1.y : q1.x) >> sh) & 255u);
+    const float nby = (float)(((py ? q1.z : q1.w) >> sh) & 255u), fby = (float)(((py ? q1.w : q1.z) >> sh) & 255u);
+    const float nbz = (float)(((pz ? q2.x : q2.y) >> sh) & 255u), fbz = (float)(((pz ? q2.y : q2.x) >> sh) & 255u);
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaf(nbx, sx, bx), __builtin_fmaf(nby, sy, by)),
+                                     __builtin_fmaxf(__builtin_fmaf(nbz, sz, bz), -1e-3f));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaf(fbx, sx, bx), __builtin_fmaf(fby, sy, by)),
+                                     __builtin_fmaf(fbz, sz, bz));
+    if (!(tn <= tf)) return false;
+    /* the determinant cull of node_children */
+    const uint32_t nlo = q2.z, nhi = q2.w;
+    const float nsc = __builtin_amdgcn_ldexpf(1.0f, (int)(nlo >> 24) - 128);
+    const uint32_t sel_n = (px ? 4u : 0u) | (py ? 5u : 1u) << 8 | (pz ? 6u : 2u) << 16;
+    const uint32_t sel_f = (px ? 0u : 4u) | (py ? 1u : 5u) << 8 | (pz ? 2u : 6u) << 16;
+    const uint32_t nb = __builtin_amdgcn_perm(nhi, nlo, sel_n), fb = __builtin_amdgcn_perm(nhi, nlo, sel_f);
+    const float bias = 128.0f * (d.x + d.y + d.z);
+    const float fhi = __builtin_fmaf(d.x, (float)(nb & 0xffu),
+                                     __builtin_fmaf(d.y, (float)((nb >> 8) & 0xffu),
+                                                    __builtin_fmaf(d.z, (float)((nb >> 16) & 0xffu), -bias)));
+    const float flo = __builtin_fmaf(d.x, (float)(fb & 0xffu),
+                                     __builtin_fmaf(d.y, (float)((fb >> 8) & 0xffu),
+                                                    __builtin_fmaf(d.z, (float)((fb >> 16) & 0xffu), -bias)));
+    const float l1 = __builtin_fabsf(d.x) + __builtin_fabsf(d.y) + __builtin_fabsf(d.z);
+    const float bound = __builtin_fmaf(__builtin_fmaxf(fhi, -flo) * nsc, 1.02f, 5e-7f * l1);
+    return !(bound < 1e-4f);
+}
+
+__device__ __forceinline__ int link_of(uint4 l, int k) { return (int)(k == 0 ? l.x : k == 1 ? l.y : k == 2 ? l.z : l.w); }
+
+/* The cut: the root's used child slots, then, level by level (a pass over the list in order), an
+   edge to an inner node replaced by that node's used slots while the list stays within G edges.
+   Thread 0 of the block, into s_par / s_slot; returns the edge count. */
+template <int G>
+__device__ int chain_cut(const uint4 *__restrict__ qn, uint32_t n_nodes, int *s_par, int *s_slot)
+{
+    if (n_nodes == 0) return 0;
+    int n = 0;
+    {
+        const uint4 l = qn[3];
+        for (int k = 0; k < 4; ++k)
+            if (link_of(l, k) != RT_EMPTY_CHILD && n < G) {
+                s_par[n] = 0;
+                s_slot[n] = k;
+                ++n;
+            }
+    }
+    for (bool grew = true; grew;) {
+        grew = false;
+        for (int i = 0; i < n;) {
+            const int c = link_of(qn[4 * s_par[i] + 3], s_slot[i]);
+            if (c < 0 || c == RT_EMPTY_CHILD || (uint32_t)c >= n_nodes) {
+                ++i;
+                continue;
+            }
+            const uint4 l = qn[4 * c + 3];
+            int m = 0;
+            for (int k = 0; k < 4; ++k) m += link_of(l, k) != RT_EMPTY_CHILD ? 1 : 0;
+            if (m == 0 || n - 1 + m > G) {
+                ++i;
+                continue;
+            }
+            for (int j = n - 1; j > i; --j) {
+                s_par[j + m - 1] = s_par[j];
+                s_slot[j + m - 1] = s_slot[j];
+            }
+            int t = i;
+            for (int k = 0; k < 4; ++k)
+                if (link_of(l, k) != RT_EMPTY_CHILD) {
+                    s_par[t] = c;
+                    s_slot[t] = k;
+                    ++t;
+                }
+            n += m - 1;
+            i += m; /* the new edges are the next level's: not expanded in this pass */
+            grew = true;
+        }
+    }
+    return n;
+}
+
+template <int G>
+__global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLaunch a)
+{
+    static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "a candidate list spreads in runs of at most 8");
+    __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
+    __shared__ uint4 s_erec[G][4]; /* per edge: its parent's record */
+    __shared__ int s_par[G], s_slot[G];
+    __shared__ int s_ne;
+    const uint4 *__restrict__ qn = reinterpret_cast<const uint4 *>(a.nodes);
+    if (threadIdx.x == 0) s_ne = chain_cut<G>(qn, a.n_nodes4, s_par, s_slot);
+    __syncthreads();
+    const int ne = s_ne;
+    for (int i = (int)threadIdx.x; i < 4 * ne; i += RT_BLOCK) s_erec[i >> 2][i & 3] = qn[4 * s_par[i >> 2] + (i & 3)];
+    __syncthreads();
+    __builtin_amdgcn_s_setprio(3); /* the long chains run beside the chunk tasks and set when their own chunks start */
+
+    Stack stk;
+    stk.init(s_stack, a.spill, a.spill_cap);
+    const int lane = (int)(threadIdx.x & 63), sub = lane & (G - 1), gbase = lane & ~(G - 1);
+    const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+    const float4 *__restrict__ nodes = reinterpret_cast<const float4 *>(a.nodes);
+    const float4 *__restrict__ tris = reinterpret_cast<const float4 *>(a.tris);
+    const int eslot = sub < ne ? s_slot[sub] : 0;
+    const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
+    const uint32_t plane = a.Wpad * a.Hpad;
+    const uint32_t tiles_x = (a.W + 7u) >> 3;
+    const uint32_t n_items = a.split_n_dev ? *a.split_n_dev : a.split_n_box;
+    const uint32_t nl = a.n_lights;
+    const float hw = uniform_f(((float)a.W) / 2.0f);
+    const float hh = uniform_f(((float)a.H) / 2.0f);
+    const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
+    const uint32_t gpw = a.split_gpw ? a.split_gpw : 64u / G;
+    bool have = false, next = false, running = false, fin = false, drained = false, live = false, ghit = false;
+    uint32_t x = 0, yl = 0, sample = 0, depth = 0;
+    uint32_t lpack = RT_LPACK_NONE;
+    uint32_t bnext = 0, bend = 0;
+    Seed seed = {0u, 0u};
+    V3 qo = v3(0.0f, 0.0f, 0.0f), qd = v3(0.0f, 0.0f, 1.0f);
+    TravState ts;
+    ts.node = 0;
+    ts.best = -1;
+    ts.best_orig = -1;
+    ts.best_t = kInf;
+    ts.inv = qo;
+    ts.oi = qo;
+    uint32_t st_steps = 0, st_box = 0, st_t0 = 0, q_steps = 0;
+    unsigned long long *const guard = a.counters + RT_CNT_GUARD;
+    /* a query of the tree starts at the lane's edge of the cut; false: no lane of the group
+       enters its child's box (no mesh hit, without a step) */
+    auto start_tree = [&]() -> bool {
+        live = false;
+        if (sub < ne) {
+            const uint4 p0 = s_erec[sub][0], p1 = s_erec[sub][1], p2 = s_erec[sub][2], p3 = s_erec[sub][3];
+            if (edge_hit(p0, p1, p2, eslot, ts.inv, ts.oi, qd)) {
+                live = true;
+                ts.node = link_of(p3, eslot);
+            }
+        }
+        return (__ballot(live) & gmask) != 0ull;
+    };
+    for (;;) {
+        const unsigned long long idle = __ballot(!have && lane == gbase && (uint32_t)(lane / G) < gpw);
+        if (idle && !drained) {
+            uint32_t item = batch_take(a.split_counter, idle, bnext, bend, gpw);
+            item = __shfl(item, gbase);
+            drained = bnext >= n_items;
+            if (!have && item < n_items) {
+                const uint32_t p = a.split_box[item];
+                x = p % a.W;
+                yl = p / a.W;
+                const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                seed.x = a.seeds[slot];
+                seed.y = a.seeds[plane + slot];
+                lpack = list_pack(a, x, yl, tiles_x);
+                sample = 0;
+                have = true;
+                next = true;
+                if (a.pixel_stats) {
+                    st_steps = st_box = 0;
+                    st_t0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                }
+            }
+        }
+        if (!__any(have)) {
+            if (drained) break;
+            continue;
+        }
+        /* the path advance (alike in the group's lanes): a new sample's camera ray, and every
+           query answered without a step, up to RT_CHAIN_IMM passes */
+        for (int pass = 0;; ++pass) {
+            if (next) {
+                next = false;
+                if ((sample == spp || sample % fine == 0u) && lane == gbase) {
+                    const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
+                }
+                if (sample == spp) {
+                    have = false;
+                    if (a.pixel_stats && lane == gbase) {
+                        uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
+                        ps[0] = st_t0;
+                        ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        ps[2] = st_steps;
+                        ps[3] = st_box;
+                        ps[4] = 1u + (uint32_t)RT_SPLIT_BOX;
+                    }
+                } else {
+                    const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
+                    const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
+                    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                    const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
+                    qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+                    qd = camera_dir(a.cam, fa - hw, fb - hh);
+                    depth = 0;
+                    trav_begin(ts, stk, qo, qd, kInf);
+                    q_steps = 0;
+                    running = true;
+                    if (lpack == RT_LPACK_EMPTY) { /* no candidate: no mesh hit */
+                        running = false;
+                        ghit = false;
+                        fin = true;
+                    } else if (lpack != RT_LPACK_NONE) { /* the list's triangles in runs over the lanes */
+                        const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
+                        const uint32_t bs = (pc + (uint32_t)G - 1u) / (uint32_t)G, s0 = (uint32_t)sub * bs;
+                        live = s0 < pc;
+                        const uint32_t cnt = live ? (pc - s0 < bs ? pc - s0 : bs) : 1u;
+                        ts.node = ~(int)(((first + s0) << 3) | (cnt - 1u));
+                    } else if (!start_tree()) {
+                        running = false;
+                        ghit = false;
+                        fin = true;
+                    }
+                }
+            }
+            if (fin) {
+                fin = false;
+                bool sample_done = true;
+                if (ghit) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
+                    for (uint32_t l = 0; l < nl; ++l) {
+                        (void)frand(seed);
+                        (void)frand(seed);
+                    }
+                } else { /* the enclosing box (rtcommon.h:425-466) */
+                    const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
+                    if (depth == 0) ++st_box;
+                    if (hd > RT_SMALL_F && hd < kInf) {
+                        const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
+                        const V3 hn = box_normal(hp, bw, bh, bw);
+                        for (uint32_t l = 0; l < nl; ++l) {
+                            (void)frand(seed);
+                            (void)frand(seed);
+                        }
+                        const float r1 = frand(seed);
+                        const float r2 = frand(seed);
+                        const float ct = rt_sqrtf(1.0f - r1);
+                        const float st = rt_sqrtf(1.0f - ct * ct);
+                        const float phi = RT_M_2PI_F * r2;
+                        float sphi, cphi;
+                        rt_sincosf(phi, &sphi, &cphi);
+                        qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
+                        qo = hp;
+                        ++depth;
+                        if (depth <= a.max_depth) {
+                            sample_done = false;
+                            q_steps = 0;
+                            trav_begin(ts, stk, qo, qd, kInf);
+                            running = true;
+                            if (!start_tree()) { /* misses every subtree's box: no mesh hit, at once */
+                                running = false;
+                                ghit = false;
+                                fin = true;
+                            }
+                        }
+                    }
+                }
+                if (sample_done) {
+                    ++sample;
+                    next = true;
+                }
+            }
+            if (pass + 1 >= RT_CHAIN_IMM || !__any(next || fin)) break;
+        }
+        /* traversal steps: each live lane one record of its subtree; the group's query ends at
+           its first accepted triangle or when no lane has a subtree left */
+#pragma unroll
+        for (int u = 0; u < RT_CHAIN_UNROLL; ++u) {
+            bool found = false;
+            if (running && live) {
+                const int nd = ts.node;
+                const uint32_t enc = ~(uint32_t)nd;
+                const bool bad = nd < 0 ? (enc >> 3) + (enc & 7u) >= a.n_recs : (uint32_t)nd >= a.n_nodes4;
+                if (bad) { /* a defect: reported (rt_synchronize fails the render), the lane ends */
+                    atomicOr(guard, (unsigned long long)RT_GUARD_INDEX);
+                    live = false;
+                } else {
+                    TravCounts tc = {0u, 0u, 0u};
+                    const bool done = trav_step_q<false>(nodes, tris, ts, stk, qo, qd, RT_SMALL_F, false, tc);
+                    found = ts.best >= 0;
+                    if (done) live = false;
+                }
+            }
+            const unsigned long long fb = __ballot(found), lb = __ballot(live);
+            if (running) {
+                ++q_steps;
+                ++st_steps;
+                const bool gf = (fb & gmask) != 0ull, gl = (lb & gmask) != 0ull;
+                /* a query never takes 2^14 steps: a bound every wave reaches (reported) */
+                if (q_steps > (1u << 14) && lane == gbase) atomicOr(guard, (unsigned long long)RT_GUARD_ROUNDS);
+                if (gf || !gl || q_steps > (1u << 14)) {
+                    running = false;
+                    live = false;
+                    fin = true;
+                    ghit = gf;
+                }
+            }
+        }
+    }
+}
+
 /* One MWC generator of frand (rng.h:9-47: x = A (x & 0xffff) + (x >> 16)) advanced by k draws.
    With M = A 2^16 - 1 the step is x -> A x mod M on the states below M (the step keeps them
    there; a fresh seed at or above M gets there within 2 steps, M itself is a fixed point), so
@@ -2428,8 +2760,14 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
     hipStream_t st = (hipStream_t)stream;
     const hipError_t e = hipMemsetAsync(a.split_counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
-    if (a.split_coop) hipLaunchKernelGGL(k_split_seeds<4>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
-    else hipLaunchKernelGGL(k_split_seeds<1>, dim3(a.split_seed_blocks), dim3(RT_BLOCK), 0, st, a);
+    const dim3 g(a.split_seed_blocks), b(RT_BLOCK);
+    if (a.split_which == RT_SPLIT_BOX && a.split_coop >= 8) { /* the long chains: subtree-parallel */
+        if (a.split_coop == 8) hipLaunchKernelGGL(k_chain_seeds<8>, g, b, 0, st, a);
+        else if (a.split_coop == 32) hipLaunchKernelGGL(k_chain_seeds<32>, g, b, 0, st, a);
+        else if (a.split_coop == 64) hipLaunchKernelGGL(k_chain_seeds<64>, g, b, 0, st, a);
+        else hipLaunchKernelGGL(k_chain_seeds<16>, g, b, 0, st, a);
+    } else if (a.split_coop == 4) hipLaunchKernelGGL(k_split_seeds<4>, g, b, 0, st, a);
+    else hipLaunchKernelGGL(k_split_seeds<1>, g, b, 0, st, a);
     return (int)hipGetLastError();
 }
 

@@ -1096,15 +1096,18 @@ def test_traversal_switch_on_a_context_keeps_results(pt, oracle):
     assert split[0] > 0 and split[1] == 0 and split[2] == 0 and split[3] > 0, split
 
 
+@pytest.mark.parametrize("width", [8, 16, 64, 4])
 @pytest.mark.parametrize("sr", [2, 3, 5])
-def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
+def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr, width):
     """Sample-split rendering forced on (RT_SPLIT=1): the seed pass stores each chunk's first
     seed from the pixel's closest-hit queries alone, k_tris renders the chunks as independent
     tasks and k_split_finish sums the samples in order.  Whole frames over two progressive
     frames and a row-stripe tile equal the oracle bit for bit, frames and seeds, with chunkings
     that do not divide the sample count evenly (sr 3: 9 chunks of 1 sample; sr 5: 13 chunks of
-    2, the last of 1)."""
+    2, the last of 1).  The long chains' seed pass runs with `width` lanes per chain: 8-64
+    subtree-parallel lanes (k_chain_seeds, the default 8) or 4 cooperative lanes (coop_round)."""
     monkeypatch.setenv("RT_SPLIT", "1")
+    monkeypatch.setenv("RT_SEED_WIDTH", str(width))
     sc = pt.scenes
     W, H = 72, 40
     Wp, Hp = sc.padded_dims(W, H)
@@ -1128,8 +1131,8 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
         rt.rayTrace(got, W, H, p, kernel=2)
         info = rt.renderInfo()
         assert info["split_chunks"] == (spp + csz - 1) // csz
-        # the long chains ran on their own stream with the 4-lane cooperative seed pass (coop_round)
-        assert info["pixels_long"] > 0 and info["split_coop"] == 4 and info["split_guard"] == 0, info
+        # the long chains ran on their own stream with `width` lanes per chain
+        assert info["pixels_long"] > 0 and info["split_coop"] == width and info["split_guard"] == 0, info
         # the mesh pixels' chunk seeds jumped ahead from their frame seeds (no seed pass for them)
         assert info["split_spec"] == 1, info
         assert len(rt.longChains()) == info["pixels_long"]
@@ -1145,7 +1148,7 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr):
     got = np.zeros(len(rows) * W * 4, np.float32)
     rt.rayTrace(got, W, H, 0, kernel=2, tile=tile)
     info = rt.renderInfo()
-    assert info["split_chunks"] > 0 and info["pixels_long"] > 0 and info["split_coop"] == 4, info
+    assert info["split_chunks"] > 0 and info["pixels_long"] > 0 and info["split_coop"] == width, info
     np.testing.assert_array_equal(bits(got), bits(exp.reshape(H, W, 4)[rows].reshape(-1)), err_msg="tile")
     np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg="tile seeds")
     rt.close()
@@ -1157,7 +1160,8 @@ def test_speculated_pixels_repaired_vs_oracle(pt, oracle, monkeypatch, spec):
     §4.5) whose camera rays miss the mesh after all are repaired: with RT_SPLIT_SPEC=2 every
     pixel whose probe rays all hit is speculated, silhouettes included, so some chunks meet a
     camera ray that misses; those pixels are listed and re-rendered (seed pass + chunks) and the
-    frame and seeds equal the oracle bit for bit.  RT_SPLIT_SPEC=0 (no speculation, every mesh
+    frame and seeds equal the oracle bit for bit; in the next frame of the view they run as long
+    chains (promoted) and that frame equals the oracle's too.  RT_SPLIT_SPEC=0 (no speculation, every mesh
     pixel through the seed pass) equals it too."""
     monkeypatch.setenv("RT_SPLIT", "1")
     monkeypatch.setenv("RT_SPLIT_SPEC", spec)
@@ -1186,6 +1190,17 @@ def test_speculated_pixels_repaired_vs_oracle(pt, oracle, monkeypatch, spec):
     exp = np.zeros_like(got)
     sd = seeds.copy()
     oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx)
+    np.testing.assert_array_equal(bits(got), bits(exp))
+    np.testing.assert_array_equal(rt.getSeeds(), sd)
+    # the next frame of the same view: the repaired pixels run as long chains (promoted), so fewer
+    # repairs, more long chains — the same bits as the oracle's progressive frame 1
+    rt.rayTrace(got, W, H, 1, kernel=2)
+    info1 = rt.renderInfo()
+    assert info1["split_guard"] == 0, info1
+    if spec == "2":
+        assert info1["pixels_long"] > info["pixels_long"], (info, info1)
+        assert info1["split_repaired"] < info["split_repaired"], (info, info1)
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 1, sd, verts, idx)
     np.testing.assert_array_equal(bits(got), bits(exp))
     np.testing.assert_array_equal(rt.getSeeds(), sd)
     rt.close()
@@ -1518,8 +1533,8 @@ def test_sample_split_at_full_size(tracer, pt, monkeypatch):
 def test_long_chains_of_the_8way_dragon_tile_vs_oracle(tracer, pt, oracle):
     """The 8-way row-stripe tile of the headline frame (dragon class, 1920x1080, sampleRate 16 =
     256 spp, maxDepth 6; tile (8, 8, 3): 1 of the 8 ranks of BASELINE's 8-GPU case): a
-    sample-split render whose long chains (box pixels and costly mesh pixels) take the 4-lane
-    cooperative seed pass (coop_round, existence queries) on the second stream.  16 of those
+    sample-split render whose long chains (box pixels and costly mesh pixels) take the 8-lane
+    subtree-parallel seed pass (k_chain_seeds, existence queries) on the second stream.  16 of those
     pixels, spread over the list, equal the oracle's linear loop bit for bit — radiance and both
     seed words (raytracer.cl:205-242, rtcommon.h:371-470) — so the pass that bounds N = 8 is
     pinned against the reference's algorithm at the configuration it serves."""
@@ -1542,7 +1557,7 @@ def test_long_chains_of_the_8way_dragon_tile_vs_oracle(tracer, pt, oracle):
     got = np.zeros(len(rows) * W * 4, np.float32)
     rt.rayTrace(got, W, H, 0, kernel=2, tile=(stripe, n_ranks, rank))
     info = rt.renderInfo()
-    assert info["split_chunks"] == 16 and info["split_coop"] == 4 and info["split_guard"] == 0, info
+    assert info["split_chunks"] == 16 and info["split_coop"] == 8 and info["split_guard"] == 0, info
     long_px = rt.longChains()
     assert len(long_px) == info["pixels_long"] and len(long_px) >= 1000, len(long_px)
     pick = long_px[np.linspace(0, len(long_px) - 1, 16).astype(np.int64)]

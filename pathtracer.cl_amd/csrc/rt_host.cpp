@@ -144,7 +144,7 @@ struct rt_ctx {
     int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (split_wanted) */
     /* the long chains' seed pass with 4 lanes per query (one lane per query: 8-way tile 24 -> 19 ms
        for the chains); 4 x 4 probe rays per pixel to find them */
-    uint32_t seed_width = 8; /* lanes per long chain in the seed pass: 8-64 subtree-parallel (k_chain_seeds), 4 coop_round, 1 */
+    uint32_t seed_width = 8; /* lanes per long chain in the seed pass: 8-64 subtree-parallel (k_chain_seeds), 3 coop_round, 1 */
     uint32_t split_probe = 4;
 #ifndef RT_SPLIT_GPW
 #define RT_SPLIT_GPW 0
@@ -157,8 +157,6 @@ struct rt_ctx {
     uint32_t *d_split_box = nullptr;  /* the box pixels (yl * W + x): their chains run on stream2 */
     size_t split_box_cap = 0;
     uint32_t n_split_box = 0;
-    uint32_t promote = 1;             /* promote repaired pixels to long chains (RT_SPLIT_PROMOTE=0: off) */
-    uint32_t promote_pending = 0;     /* pixels repaired in the last synchronised split render (their list: d_split_repair) */
     int split_box_grid = 0;           /* the box pixels' seed-pass grid of the render being launched */
     hipStream_t stream2 = nullptr;    /* the box pixels' seed pass and chunks, beside the mesh pixels' */
     /* speculated mesh pixels (RT_SPLIT_SPEC, default on): their chunk seeds jumped ahead from the
@@ -474,7 +472,7 @@ int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
    the full grid (further chains queue behind the first); full_grid 0: unbounded. */
 int split_box_blocks(const rt_ctx *c, uint32_t width, int full_grid)
 {
-    const uint32_t per_wave = c->split_gpw ? c->split_gpw : 64u / std::max(1u, width);
+    const uint32_t per_wave = c->split_gpw ? c->split_gpw : 64u / std::max(1u, width == RT_SEED_COOP4 ? 4u : width);
     int n = (int)((c->n_split_box + per_wave * 4u - 1u) / (per_wave * 4u));
     /* subtree-parallel chains (width >= 8) all run at once: each is the critical path */
     if (full_grid > 0) n = std::min(n, std::max(1, width >= 8 ? full_grid : full_grid / RT_BOX_GRID_DIV));
@@ -522,7 +520,7 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
         HIPCHK(c, hipMalloc(&c->d_split_repair, npx * sizeof(uint32_t)));
         c->split_dirty_px = npx;
     }
-    HIPCHK(c, hipMemsetAsync(c->d_split_dirty, 0, npx * sizeof(uint32_t), st));
+    HIPCHK(c, hipMemsetAsync(c->d_split_dirty, 0xff, npx * sizeof(uint32_t), st));
     a.split_spec = 1;
     a.split_spec_draws = draws;
     a.split_spec_mul = c->d_spec_mul;
@@ -577,6 +575,8 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_seed_blocks = 16;
         r.split_chunk = a.split_fine;
         r.split_chunks = (a.sample_rate * a.sample_rate + r.split_chunk - 1u) / r.split_chunk;
+        r.split_restart = a.split_dirty; /* each chain from its first missed chunk on */
+        r.split_restart_chunk = a.split_chunk;
         e = rt_launch_split_seeds(r, st);
         if (!e) e = rt_launch_tris(r, RT_TRAV_BVH4Q, c->counting, 64, st);
         if (e) return hip_fail(c, (hipError_t)e, "repair launches");
@@ -614,39 +614,7 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
     const uint32_t n_t = ((W + 7) / 8) * ((hl + 7) / 8);
     c->schedule_rebuilt = false;
-    if (key == c->order_key) {
-        /* an unchanged schedule: the pixels repaired in its last frame (speculated mesh pixels
-           a camera ray of which missed the mesh) run as long chains from now on, so a steady
-           view stops paying the repair pass (one 4-byte read when there were any) */
-        const uint32_t k = c->promote_pending;
-        c->promote_pending = 0;
-        if (k && c->n_split_box && c->d_split_repair && c->d_class && c->d_split_counter) {
-            const uint32_t n_box = c->n_split_box;
-            if (c->split_box_cap < n_box + k) {
-                uint32_t *nb = nullptr;
-                HIPCHK(c, hipMalloc(&nb, (size_t)(n_box + k) * 4));
-                const hipError_t ce = hipMemcpyAsync(nb, c->d_split_box, (size_t)n_box * 4, hipMemcpyDeviceToDevice, st);
-                if (ce != hipSuccess) {
-                    (void)hipFree(nb);
-                    return hip_fail(c, ce, "long-chain list growth");
-                }
-                HIPCHK(c, hipStreamSynchronize(st));
-                free_dev(c->d_split_box);
-                c->d_split_box = nb;
-                c->split_box_cap = n_box + k;
-            }
-            uint32_t *cnt = c->d_split_counter + 60;
-            HIPCHK(c, hipMemsetAsync(cnt, 0, sizeof(uint32_t), st));
-            const int e = rt_sched_promote(c->d_split_repair, k, W * hl, n_box, c->d_class, c->d_split_box, cnt, st);
-            if (e) return hip_fail(c, (hipError_t)e, "long-chain promotion");
-            uint32_t added = 0;
-            HIPCHK(c, hipMemcpyAsync(&added, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-            HIPCHK(c, hipStreamSynchronize(st));
-            c->n_split_box = n_box + added;
-        }
-        return RT_OK;
-    }
-    c->promote_pending = 0;
+    if (key == c->order_key) return RT_OK;
     c->order_key.clear();
     c->n_split_box = 0;
     if (trav_kind(c) != RT_TRAV_BVH4Q || a.nodes != reinterpret_cast<const float *>(c->d_nodes4q)) {
@@ -751,7 +719,7 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_SPLIT_MB")) c->split_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
-    if (const char *v = getenv("RT_SPLIT_PROMOTE")) c->promote = atoi(v) != 0 ? 1u : 0u;
+    if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) c->seed_width = (uint32_t)std::max(1, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
@@ -1226,10 +1194,11 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                 a.split_n_box = c->n_split_box;
                 a.n_nodes4 = c->bvh.n_nodes4;
                 /* lanes per long chain: seed_width (a power of two, 8-64) subtree-parallel lanes
-                   (k_chain_seeds); else 4 cooperative lanes where the group's LDS stack holds the
-                   tree's worst depth-first stack (+ a candidate list's blocks), else one */
-                a.split_coop = c->seed_width >= 8 ? std::min(64u, 1u << (31 - __builtin_clz(c->seed_width)))
-                             : c->seed_width >= 4 && c->bvh.stack4 + 4 <= RT_COOP_STACK ? 4u : 0u;
+                   (k_chain_seeds); RT_SEED_COOP4 (3): 4 cooperative lanes (coop_round) where the
+                   group's LDS stack holds the tree's worst depth-first stack (+ a candidate list's
+                   blocks); else one */
+                a.split_coop = c->seed_width >= 4 ? std::min(64u, std::max(8u, 1u << (31 - __builtin_clz(c->seed_width))))
+                             : c->seed_width == RT_SEED_COOP4 && c->bvh.stack4 + 4 <= RT_COOP_STACK ? RT_SEED_COOP4 : 0u;
                 /* a round of 4 nodes adds at most 12 entries and a one-item depth-first walk at
                    most the tree's worst stack: rounds take 4 items up to this depth (coop_round) */
                 a.coop_multi_sp = std::max(0, (int)RT_COOP_STACK - 12 - (int)c->bvh.stack4);
@@ -1468,7 +1437,6 @@ int rt_synchronize(rt_ctx *c)
     c->last.pixel_steps_max = h[12];
     c->last.pixels_long = c->last_long;
     c->info.split_repaired = (uint32_t)h[RT_CNT_REPAIR];
-    c->promote_pending = c->promote ? c->info.split_repaired : 0u;
     if (h[RT_CNT_GUARD]) { /* a defect guard of the long chains' seed pass: the frame is not the reference's */
         c->info.split_guard = (uint32_t)h[RT_CNT_GUARD];
         char msg[160];

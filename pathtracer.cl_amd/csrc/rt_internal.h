@@ -197,11 +197,16 @@ struct RtTriLaunch {
     uint32_t split_spec;          /* RT_SPLIT_MESH: the mesh pixels' chunk seeds by jump-ahead */
     uint32_t split_spec_draws;    /* random numbers per sample of a speculated pixel */
     const uint32_t *split_spec_mul; /* per chunk c: a_x^(c chunk D) mod m_x, a_y^(c chunk D) mod m_y */
-    uint32_t *split_dirty;        /* per pixel: 1 once a speculated chunk saw a camera ray miss */
+    uint32_t *split_dirty;        /* per pixel: the first chunk that saw a camera ray miss (~0u: none) */
     uint32_t *split_repair;       /* the marked pixels (yl * W + x) */
     const uint32_t *split_n_dev;  /* RT_SPLIT_BOX: the item count from device memory (NULL: split_n_box) */
+    const uint32_t *split_restart; /* the repair pass: per pixel the first chunk (of split_restart_chunk samples)
+                                      whose camera ray missed — the chain restarts there from the jumped seed,
+                                      the chunks before it stand (NULL: from the frame seed) */
+    uint32_t split_restart_chunk;
 };
 enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
+#define RT_SEED_COOP4 3 /* split_coop: the 4-lane cooperative seed pass (coop_round) */
 #define RT_COOP_STACK (RT_STACK_DEPTH * 4) /* LDS stack entries of a 4-lane query group (k_split_seeds) */
 #ifndef RT_LIST_MAX
 #define RT_LIST_MAX 64
@@ -272,11 +277,6 @@ int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, ui
                       uint32_t row, void *stream);
 int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *slot_pixel,
                       void *stream);
-/* Promotes pixels (pix[0..k)) that are still speculated mesh pixels (class -1) to long chains with
-   slots base, base + 1, ... (their count added to *count): the repaired pixels of the last frame of an
-   unchanged schedule run as long chains from the next frame on. */
-int rt_sched_promote(const uint32_t *pix, uint32_t k, uint32_t npx, uint32_t base, int32_t *cls, uint32_t *slot_pixel,
-                     uint32_t *count, void *stream);
 /* Seed-row halo: copy whole rows (both planes) of the seed layout to / from a packed
    buffer [plane][i][x] of 2 * n * wpad words (rows: device array of n row indices). */
 int rt_launch_seed_rows(uint32_t *seeds, uint32_t wpad, uint32_t hpad, const uint32_t *rows, uint32_t n,

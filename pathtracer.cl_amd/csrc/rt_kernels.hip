@@ -1159,6 +1159,29 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     }
 }
 
+/* One MWC generator of frand (rng.h:9-47: x = A (x & 0xffff) + (x >> 16)) advanced by k draws.
+   With M = A 2^16 - 1 the step is x -> A x mod M on the states below M (the step keeps them
+   there; a fresh seed at or above M gets there within 2 steps, M itself is a fixed point), so
+   k draws are one multiplication by A^k mod M (`mul`, from the host); a^-1 = 2^16 mod M undoes
+   the canonicalising steps.  Small k: the steps themselves. */
+template <uint32_t A>
+__device__ __forceinline__ uint32_t mwc_jump(uint32_t x, uint32_t k, uint32_t mul)
+{
+    constexpr uint32_t M = A * 65536u - 1u;
+    if (k <= 16u) {
+        for (uint32_t i = 0; i < k; ++i) x = A * (x & 65535u) + (x >> 16);
+        return x;
+    }
+    uint32_t k0 = 0;
+    while (x > M) { /* at most 2 steps (every 32-bit state checked, DESIGN.md §4.5) */
+        x = A * (x & 65535u) + (x >> 16);
+        ++k0;
+    }
+    if (x == M) return M;
+    for (uint32_t i = 0; i < k0; ++i) mul = (uint32_t)(((unsigned long long)mul * 65536u) % M);
+    return (uint32_t)(((unsigned long long)x * mul) % M);
+}
+
 /* ------------------------------------------------------------------------ */
 /* Subtree-parallel seed pass of the long chains (k_chain_seeds): G lanes per chain.  The seed
    needs only WHETHER a segment meets the mesh (an accepted triangle anywhere), and that answer
@@ -1272,10 +1295,85 @@ __device__ int chain_cut(const uint4 *__restrict__ qn, uint32_t n_nodes, int *s_
     return n;
 }
 
+/* intersect_box (geometryFuncs.h:86-150) for a group of G >= 8 lanes carrying the same ray: the
+   six slab divisions one per lane (lanes 0-5 of the group), gathered; the same operations on
+   the same values as intersect_box, so the same bits. */
+__device__ __forceinline__ float group_box(V3 o, V3 d, float tmin, float xs, float ys, float zs, int sub, int gbase)
+{
+    const int kk = sub < 6 ? sub : 0, ax = kk >> 1;
+    const float oa = ax == 0 ? o.x : ax == 1 ? o.y : o.z, da = ax == 0 ? d.x : ax == 1 ? d.y : d.z;
+    const float sa = ax == 0 ? xs : ax == 1 ? ys : zs;
+    const float q = ((kk & 1) ? (0.0f + sa) - oa : (0.0f - sa) - oa) / da;
+    const float tx1 = __shfl(q, gbase), tx2 = __shfl(q, gbase + 1), ty1 = __shfl(q, gbase + 2);
+    const float ty2 = __shfl(q, gbase + 3), tz1 = __shfl(q, gbase + 4), tz2 = __shfl(q, gbase + 5);
+    float nt = 0.0f, ft = rt_inff();
+    if (d.x != 0) {
+        nt = rt_minf(tx1, tx2);
+        ft = rt_maxf(tx1, tx2);
+    } else if (rt_fabsf(o.x - 0.0f) > xs) {
+        return 0;
+    }
+    if (d.y != 0) {
+        if (ty1 > ty2) {
+            nt = rt_maxf(ty2, nt);
+            ft = rt_minf(ty1, ft);
+        } else {
+            nt = rt_maxf(ty1, nt);
+            ft = rt_minf(ty2, ft);
+        }
+    } else if (rt_fabsf(o.y - 0.0f) > ys) {
+        return 0;
+    }
+    if (d.z != 0) {
+        if (tz1 > tz2) {
+            nt = rt_maxf(tz2, nt);
+            ft = rt_minf(tz1, ft);
+        } else {
+            nt = rt_maxf(tz1, nt);
+            ft = rt_minf(tz2, ft);
+        }
+    } else if (rt_fabsf(o.z - 0.0f) > zs) {
+        return 0;
+    }
+    if (nt > ft || ft < tmin) return rt_inff();
+    if (nt < tmin) return ft;
+    return nt;
+}
+
+/* box_normal (geometryFuncs.h:71-84): -p / |p| is exactly -1 or +1 for a finite non-zero p, so the
+   division runs only for the rest (0 or infinite: NaN, as the reference's) */
+__device__ __forceinline__ float neg_sign(float p)
+{
+    if (p != 0.0f && rt_fabsf(p) < rt_inff()) return p > 0.0f ? -1.0f : 1.0f;
+    return -p / rt_fabsf(p);
+}
+__device__ __forceinline__ V3 box_normal_signs(V3 p, float xs, float ys, float zs)
+{
+    const float dx = rt_fabsf(rt_fabsf(p.x) - xs);
+    const float dy = rt_fabsf(rt_fabsf(p.y) - ys);
+    const float dz = rt_fabsf(rt_fabsf(p.z) - zs);
+    if (dx < dy && dx < dz) return v3(neg_sign(p.x), 0.0f, 0.0f);
+    if (dy < dz) return v3(0.0f, neg_sign(p.y), 0.0f);
+    return v3(0.0f, 0.0f, neg_sign(p.z));
+}
+
+/* camera_dir for a group of G >= 8 lanes: the three divisions by the length on lanes 0-2 */
+__device__ __forceinline__ V3 group_camera_dir(const rt_camera &cam, float a, float b, int sub, int gbase)
+{
+    const float x = (cam.view.x + cam.right.x * a) + cam.up.x * b;
+    const float y = (cam.view.y + cam.right.y * a) + cam.up.y * b;
+    const float z = (cam.view.z + cam.right.z * a) + cam.up.z * b;
+    const float w = (cam.view.w + cam.right.w * a) + cam.up.w * b;
+    const float len = rt_sqrtf(((x * x + y * y) + z * z) + w * w);
+    const int kk = sub < 3 ? sub : 0;
+    const float q = (kk == 0 ? x : kk == 1 ? y : z) / len;
+    return v3(__shfl(q, gbase), __shfl(q, gbase + 1), __shfl(q, gbase + 2));
+}
+
 template <int G>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLaunch a)
 {
-    static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "a candidate list spreads in runs of at most 8");
+    static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "the advance spreads 6 divisions over the group's lanes");
     __shared__ int s_stack[RT_STACK_DEPTH * RT_BLOCK];
     __shared__ uint4 s_erec[G][4]; /* per edge: its parent's record */
     __shared__ int s_par[G], s_slot[G];
@@ -1345,8 +1443,16 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                 const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                 seed.x = a.seeds[slot];
                 seed.y = a.seeds[plane + slot];
-                lpack = list_pack(a, x, yl, tiles_x);
                 sample = 0;
+                if (a.split_restart) { /* a repaired pixel: from its first missed chunk, whose seed the
+                                          jump gives (every sample before it hit the mesh) */
+                    const uint32_t ch = a.split_restart[p];
+                    const uint32_t k = ch * a.split_restart_chunk * a.split_spec_draws;
+                    seed.x = mwc_jump<36969u>(seed.x, k, a.split_spec_mul[2 * ch]);
+                    seed.y = mwc_jump<18000u>(seed.y, k, a.split_spec_mul[2 * ch + 1]);
+                    sample = ch * a.split_restart_chunk;
+                }
+                lpack = list_pack(a, x, yl, tiles_x);
                 have = true;
                 next = true;
                 if (a.pixel_stats) {
@@ -1359,9 +1465,51 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
             if (drained) break;
             continue;
         }
-        /* the path advance (alike in the group's lanes): a new sample's camera ray, and every
-           query answered without a step, up to RT_CHAIN_IMM passes */
+        /* the path advance (alike in the group's lanes), up to RT_CHAIN_IMM passes: a finished
+           query's bounce (or the end of its sample), a new sample's camera ray, then at most one
+           query start per pass — its ray answered at once when it enters no subtree's box.  The
+           advance's IEEE divisions are spread over the group's lanes (one each, gathered) */
         for (int pass = 0;; ++pass) {
+            bool start = false;
+            if (fin) {
+                fin = false;
+                bool sample_done = true;
+                if (ghit) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
+                    for (uint32_t l = 0; l < nl; ++l) {
+                        (void)frand(seed);
+                        (void)frand(seed);
+                    }
+                } else { /* the enclosing box (rtcommon.h:425-466) */
+                    const float hd = group_box(qo, qd, RT_SMALL_F, bw, bh, bw, sub, gbase);
+                    if (depth == 0) ++st_box;
+                    if (hd > RT_SMALL_F && hd < kInf) {
+                        const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
+                        const V3 hn = box_normal_signs(hp, bw, bh, bw);
+                        for (uint32_t l = 0; l < nl; ++l) {
+                            (void)frand(seed);
+                            (void)frand(seed);
+                        }
+                        const float r1 = frand(seed);
+                        const float r2 = frand(seed);
+                        const float ct = rt_sqrtf(1.0f - r1);
+                        const float st = rt_sqrtf(1.0f - ct * ct);
+                        const float phi = RT_M_2PI_F * r2;
+                        float sphi, cphi;
+                        rt_sincosf(phi, &sphi, &cphi);
+                        qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
+                        qo = hp;
+                        ++depth;
+                        if (depth <= a.max_depth) {
+                            sample_done = false;
+                            start = true;
+                        }
+                    }
+                }
+                if (sample_done) {
+                    ++sample;
+                    next = true;
+                }
+            }
             if (next) {
                 next = false;
                 if ((sample == spp || sample % fine == 0u) && lane == gbase) {
@@ -1379,77 +1527,39 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                         ps[4] = 1u + (uint32_t)RT_SPLIT_BOX;
                     }
                 } else {
+                    /* strat_rand twice (rng.h:45-47): the two draws, then the divisions on two lanes */
+                    const float f1 = frand(seed), f2 = frand(seed);
                     const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
-                    const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
+                    const float num = (float)(sub & 1 ? sy : sx) + (sub & 1 ? f2 : f1);
+                    const float qv = num / (float)a.sample_rate;
+                    const float ua = __shfl(qv, gbase), ub = __shfl(qv, gbase + 1);
+                    const float fa = (float)x + ua;
                     const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
-                    const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
+                    const float fb = (float)y + ub;
                     qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
-                    qd = camera_dir(a.cam, fa - hw, fb - hh);
+                    qd = group_camera_dir(a.cam, fa - hw, fb - hh, sub, gbase);
                     depth = 0;
-                    trav_begin(ts, stk, qo, qd, kInf);
-                    q_steps = 0;
-                    running = true;
-                    if (lpack == RT_LPACK_EMPTY) { /* no candidate: no mesh hit */
-                        running = false;
-                        ghit = false;
-                        fin = true;
-                    } else if (lpack != RT_LPACK_NONE) { /* the list's triangles in runs over the lanes */
-                        const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
-                        const uint32_t bs = (pc + (uint32_t)G - 1u) / (uint32_t)G, s0 = (uint32_t)sub * bs;
-                        live = s0 < pc;
-                        const uint32_t cnt = live ? (pc - s0 < bs ? pc - s0 : bs) : 1u;
-                        ts.node = ~(int)(((first + s0) << 3) | (cnt - 1u));
-                    } else if (!start_tree()) {
-                        running = false;
-                        ghit = false;
-                        fin = true;
-                    }
+                    start = true;
                 }
             }
-            if (fin) {
-                fin = false;
-                bool sample_done = true;
-                if (ghit) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
-                    for (uint32_t l = 0; l < nl; ++l) {
-                        (void)frand(seed);
-                        (void)frand(seed);
-                    }
-                } else { /* the enclosing box (rtcommon.h:425-466) */
-                    const float hd = intersect_box(qo, qd, RT_SMALL_F, bw, bh, bw);
-                    if (depth == 0) ++st_box;
-                    if (hd > RT_SMALL_F && hd < kInf) {
-                        const V3 hp = v3(qo.x + qd.x * hd, qo.y + qd.y * hd, qo.z + qd.z * hd);
-                        const V3 hn = box_normal(hp, bw, bh, bw);
-                        for (uint32_t l = 0; l < nl; ++l) {
-                            (void)frand(seed);
-                            (void)frand(seed);
-                        }
-                        const float r1 = frand(seed);
-                        const float r2 = frand(seed);
-                        const float ct = rt_sqrtf(1.0f - r1);
-                        const float st = rt_sqrtf(1.0f - ct * ct);
-                        const float phi = RT_M_2PI_F * r2;
-                        float sphi, cphi;
-                        rt_sincosf(phi, &sphi, &cphi);
-                        qd = shading_to_world(v3(cphi * st, sphi * st, ct), hn);
-                        qo = hp;
-                        ++depth;
-                        if (depth <= a.max_depth) {
-                            sample_done = false;
-                            q_steps = 0;
-                            trav_begin(ts, stk, qo, qd, kInf);
-                            running = true;
-                            if (!start_tree()) { /* misses every subtree's box: no mesh hit, at once */
-                                running = false;
-                                ghit = false;
-                                fin = true;
-                            }
-                        }
-                    }
-                }
-                if (sample_done) {
-                    ++sample;
-                    next = true;
+            if (start) {
+                trav_begin(ts, stk, qo, qd, kInf);
+                q_steps = 0;
+                running = true;
+                if (depth == 0 && lpack == RT_LPACK_EMPTY) { /* no candidate: no mesh hit */
+                    running = false;
+                    ghit = false;
+                    fin = true;
+                } else if (depth == 0 && lpack != RT_LPACK_NONE) { /* the list's triangles in runs over the lanes */
+                    const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
+                    const uint32_t bs = (pc + (uint32_t)G - 1u) / (uint32_t)G, s0 = (uint32_t)sub * bs;
+                    live = s0 < pc;
+                    const uint32_t cnt = live ? (pc - s0 < bs ? pc - s0 : bs) : 1u;
+                    ts.node = ~(int)(((first + s0) << 3) | (cnt - 1u));
+                } else if (!start_tree()) { /* misses every subtree's box: no mesh hit, at once */
+                    running = false;
+                    ghit = false;
+                    fin = true;
                 }
             }
             if (pass + 1 >= RT_CHAIN_IMM || !__any(next || fin)) break;
@@ -1489,29 +1599,6 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
             }
         }
     }
-}
-
-/* One MWC generator of frand (rng.h:9-47: x = A (x & 0xffff) + (x >> 16)) advanced by k draws.
-   With M = A 2^16 - 1 the step is x -> A x mod M on the states below M (the step keeps them
-   there; a fresh seed at or above M gets there within 2 steps, M itself is a fixed point), so
-   k draws are one multiplication by A^k mod M (`mul`, from the host); a^-1 = 2^16 mod M undoes
-   the canonicalising steps.  Small k: the steps themselves. */
-template <uint32_t A>
-__device__ __forceinline__ uint32_t mwc_jump(uint32_t x, uint32_t k, uint32_t mul)
-{
-    constexpr uint32_t M = A * 65536u - 1u;
-    if (k <= 16u) {
-        for (uint32_t i = 0; i < k; ++i) x = A * (x & 65535u) + (x >> 16);
-        return x;
-    }
-    uint32_t k0 = 0;
-    while (x > M) { /* at most 2 steps (every 32-bit state checked, DESIGN.md §4.5) */
-        x = A * (x & 65535u) + (x >> 16);
-        ++k0;
-    }
-    if (x == M) return M;
-    for (uint32_t i = 0; i < k0; ++i) mul = (uint32_t)(((unsigned long long)mul * 65536u) % M);
-    return (uint32_t)(((unsigned long long)x * mul) % M);
 }
 
 /* ======================================================================== */
@@ -1658,9 +1745,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     if (SPLIT && depth == 0 && a.split_spec && a.split_which == RT_SPLIT_MESH &&
                         sample / a.split_chunk + 1u < a.split_chunks) {
                         /* a speculated pixel's camera ray missed the mesh: its later chunks started
-                           from wrong seeds — listed once for the repair pass (rare path) */
+                           from wrong seeds — listed once for the repair pass, which restarts at the
+                           first such chunk (rare path) */
                         const uint32_t p = yl * a.W + x;
-                        if (atomicExch(a.split_dirty + p, 1u) == 0u)
+                        if (atomicMin(a.split_dirty + p, sample / a.split_chunk) == ~0u)
                             a.split_repair[(uint32_t)atomicAdd(a.counters + RT_CNT_REPAIR, 1ull)] = p;
                     }
                     /* the enclosing box (rtcommon.h:427-433); ray.tmax is still INF */
@@ -1873,7 +1961,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         const uint32_t p = a.split_box[slot];
                         x = p % a.W;
                         yl = p / a.W;
-                        take = true;
+                        /* a repaired pixel: its chunks before the first missed one stand */
+                        take = !a.split_restart || chunk * a.split_chunk >= a.split_restart[p] * a.split_restart_chunk;
                     } else {
                         if (SPLIT) {
                             chunk = tile % a.split_chunks;
@@ -2761,12 +2850,12 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
     const hipError_t e = hipMemsetAsync(a.split_counter, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return (int)e;
     const dim3 g(a.split_seed_blocks), b(RT_BLOCK);
-    if (a.split_which == RT_SPLIT_BOX && a.split_coop >= 8) { /* the long chains: subtree-parallel */
+    if (a.split_which == RT_SPLIT_BOX && a.split_coop >= 8) { /* subtree-parallel */
         if (a.split_coop == 8) hipLaunchKernelGGL(k_chain_seeds<8>, g, b, 0, st, a);
         else if (a.split_coop == 32) hipLaunchKernelGGL(k_chain_seeds<32>, g, b, 0, st, a);
         else if (a.split_coop == 64) hipLaunchKernelGGL(k_chain_seeds<64>, g, b, 0, st, a);
         else hipLaunchKernelGGL(k_chain_seeds<16>, g, b, 0, st, a);
-    } else if (a.split_coop == 4) hipLaunchKernelGGL(k_split_seeds<4>, g, b, 0, st, a);
+    } else if (a.split_coop == RT_SEED_COOP4) hipLaunchKernelGGL(k_split_seeds<4>, g, b, 0, st, a);
     else hipLaunchKernelGGL(k_split_seeds<1>, g, b, 0, st, a);
     return (int)hipGetLastError();
 }

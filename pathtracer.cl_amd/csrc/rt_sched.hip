@@ -136,21 +136,6 @@ __global__ __launch_bounds__(256) void k_classify(const uint32_t *__restrict__ b
     cls[p] = c;
 }
 
-__global__ __launch_bounds__(256) void k_promote(const uint32_t *__restrict__ pix, uint32_t k, uint32_t npx, uint32_t base,
-                                                 int32_t *__restrict__ cls, uint32_t *__restrict__ slot_pixel,
-                                                 uint32_t *__restrict__ count)
-{
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= k) return;
-    const uint32_t p = pix[i];
-    if (p >= npx) return;
-    if (atomicCAS(cls + p, -1, -3) == -1) { /* each pixel once, however often it is listed */
-        const uint32_t s = base + atomicAdd(count, 1u);
-        cls[p] = (int32_t)s;
-        slot_pixel[s] = p;
-    }
-}
-
 } // namespace
 
 void rt_sched_free(RtSchedScratch &s)
@@ -235,15 +220,6 @@ int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, ui
     size_t bytes = s.tmp_bytes;
     e = hipcub::DeviceScan::ExclusiveSum(s.tmp, bytes, s.box, s.scan, (int)npx + 1, st);
     return (int)e;
-}
-
-int rt_sched_promote(const uint32_t *pix, uint32_t k, uint32_t npx, uint32_t base, int32_t *cls, uint32_t *slot_pixel,
-                     uint32_t *count, void *stream)
-{
-    if (k == 0) return 0;
-    hipLaunchKernelGGL(k_promote, dim3((k + 255u) / 256u), dim3(256), 0, (hipStream_t)stream, pix, k, npx, base, cls,
-                       slot_pixel, count);
-    return (int)hipGetLastError();
 }
 
 int rt_sched_classify(const RtSchedScratch &s, uint32_t npx, uint32_t slots, int32_t *cls, uint32_t *slot_pixel,

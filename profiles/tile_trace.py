@@ -9,7 +9,7 @@ import csv
 import glob
 import sys
 
-NAMES = ("k_tris", "k_split_seeds", "k_chain_seeds", "k_split_finish", "k_pixel_lists", "k_probe_cost")
+NAMES = ("k_tris", "k_split_seeds", "k_chain_seeds", "k_chain_wave", "k_split_finish", "k_pixel_lists", "k_probe_cost")
 
 
 def short(name):

@@ -144,7 +144,8 @@ struct rt_ctx {
     int split = -1;                   /* RT_SPLIT: 1 on, 0 off, unset = auto (split_wanted) */
     /* the long chains' seed pass with 4 lanes per query (one lane per query: 8-way tile 24 -> 19 ms
        for the chains); 4 x 4 probe rays per pixel to find them */
-    uint32_t seed_width = 8; /* lanes per long chain in the seed pass: 8-64 subtree-parallel (k_chain_seeds), 3 coop_round, 1 */
+    uint32_t seed_width = 0; /* lanes per long chain in the seed pass: 8-64 subtree-parallel (k_chain_seeds), 3 coop_round,
+                                1 one lane, 0 by the launch (seed_width_auto) */
     uint32_t split_probe = 4;
 #ifndef RT_SPLIT_GPW
 #define RT_SPLIT_GPW 0
@@ -443,6 +444,13 @@ bool split_wanted(const rt_ctx *c, uint64_t npx, uint64_t lanes)
     if (c->sample_rate < 2) return false;
     return c->split == 1 || (c->split < 0 && npx < 2 * lanes && c->sample_rate >= 4);
 }
+
+/* The long chains' seed-pass form for a sample-split launch: below 1.2 pixels per resident lane
+   (the 8-way tile of the 1920x1080 frame: 0.8) the chains are the tile's critical path and take
+   8 subtree-parallel lanes each (k_chain_seeds: 8-way tile 18.5 -> 16.4 ms); above it (the 4-way
+   tile: 1.6) the chunks' throughput is, and the 4-lane cooperative pass, lighter on the chip,
+   wins (4-way tile 32.5 -> 30.1 ms; profiles/r04t). */
+uint32_t seed_width_auto(uint64_t npx, uint64_t lanes) { return npx * 5 < lanes * 6 ? 8u : (uint32_t)RT_SEED_COOP4; }
 
 /* Sample-split buffers: per pixel (nch + 1) seed pairs, per sample and pixel an RGB radiance. */
 int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
@@ -1197,8 +1205,9 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
                    (k_chain_seeds); RT_SEED_COOP4 (3): 4 cooperative lanes (coop_round) where the
                    group's LDS stack holds the tree's worst depth-first stack (+ a candidate list's
                    blocks); else one */
-                a.split_coop = c->seed_width >= 4 ? std::min(64u, std::max(8u, 1u << (31 - __builtin_clz(c->seed_width))))
-                             : c->seed_width == RT_SEED_COOP4 && c->bvh.stack4 + 4 <= RT_COOP_STACK ? RT_SEED_COOP4 : 0u;
+                const uint32_t sw = c->seed_width ? c->seed_width : seed_width_auto((uint64_t)W * hl, (uint64_t)blocks * RT_BLOCK);
+                a.split_coop = sw >= 4 ? std::min(64u, std::max(8u, 1u << (31 - __builtin_clz(sw))))
+                             : sw == RT_SEED_COOP4 && c->bvh.stack4 + 4 <= RT_COOP_STACK ? RT_SEED_COOP4 : 0u;
                 /* a round of 4 nodes adds at most 12 entries and a one-item depth-first walk at
                    most the tree's worst stack: rounds take 4 items up to this depth (coop_round) */
                 a.coop_multi_sp = std::max(0, (int)RT_COOP_STACK - 12 - (int)c->bvh.stack4);

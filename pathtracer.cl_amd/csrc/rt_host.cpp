@@ -168,7 +168,8 @@ struct rt_ctx {
     uint32_t *d_spec_mul = nullptr;   /* per chunk: the two generators' jump multipliers */
     std::vector<uint32_t> h_spec_mul; /* their host copy (the upload's source; re-uploaded on change) */
     uint64_t spec_mul_key = ~0ull;
-    hipEvent_t ev_split0 = nullptr, ev_box = nullptr;
+    hipEvent_t ev_split0 = nullptr, ev_box = nullptr, ev_mesh = nullptr, ev_fin3 = nullptr;
+    hipStream_t stream3 = nullptr;    /* the clean mesh pixels' in-order sums, beside the repair pass */
     uint32_t *d_halo_rows = nullptr; /* seed-row halo: row indices */
     uint32_t *d_halo_buf = nullptr;  /* seed-row halo: staging for host buffers */
     size_t halo_rows_cap = 0, halo_buf_cap = 0;
@@ -473,6 +474,9 @@ int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
     if (!c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     if (!c->ev_split0) HIPCHK(c, hipEventCreateWithFlags(&c->ev_split0, hipEventDisableTiming));
     if (!c->ev_box) HIPCHK(c, hipEventCreateWithFlags(&c->ev_box, hipEventDisableTiming));
+    if (!c->stream3) HIPCHK(c, hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
+    if (!c->ev_mesh) HIPCHK(c, hipEventCreateWithFlags(&c->ev_mesh, hipEventDisableTiming));
+    if (!c->ev_fin3) HIPCHK(c, hipEventCreateWithFlags(&c->ev_fin3, hipEventDisableTiming));
     return RT_OK;
 }
 
@@ -537,10 +541,11 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
     return RT_OK;
 }
 
-/* A sample-split render: the box pixels' seed pass and then their chunks on stream2, beside
-   the mesh pixels' seed pass and chunks on the render stream (the box pixels' chains are the
-   long ones: they overlap the rest of the frame instead of preceding it); then the in-order
-   sums.  Each stream has its own queue cursors and its own part of the spill area. */
+/* A sample-split render: the box pixels' seed pass, their chunks and their in-order sums on
+   stream2, beside the mesh pixels' seed pass (none when speculated) and chunks on the render
+   stream (the box pixels' chains are the long ones: they overlap the rest of the frame instead
+   of preceding it); the clean mesh pixels' sums on stream3 beside the repair pass, then the
+   repaired pixels' sums.  Each stream has its own queue cursors and its own part of the spill area. */
 int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
 {
     const uint32_t n_box = a.split_which == RT_SPLIT_MESH ? a.split_n_box : 0u;
@@ -559,6 +564,9 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         const int chunk_grid = (int)std::min<uint64_t>((uint64_t)blocks, ((uint64_t)n_box * b.split_chunks + RT_BLOCK - 1) / RT_BLOCK);
         int e = rt_launch_split_seeds(b, c->stream2);
         if (!e) e = rt_launch_tris(b, RT_TRAV_BVH4Q, c->counting, std::max(1, chunk_grid), c->stream2);
+        RtTriLaunch f = a; /* the long chains' in-order sums, as soon as their chunks are done */
+        f.finish_part = RT_FIN_LONG;
+        if (!e) e = rt_launch_split_finish(f, c->stream2);
         if (e) return hip_fail(c, (hipError_t)e, "box-pixel split launches");
         HIPCHK(c, hipEventRecord(c->ev_box, c->stream2));
     }
@@ -567,6 +575,15 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     int e = a.split_spec ? 0 : rt_launch_split_seeds(m, st); /* speculated: no seed pass */
     if (!e) e = rt_launch_tris(m, RT_TRAV_BVH4Q, c->counting, blocks, st);
     if (e) return e;
+    if (n_box) { /* the mesh pixels no chunk of which missed: summed on stream3, beside the repair pass */
+        HIPCHK(c, hipEventRecord(c->ev_mesh, st));
+        HIPCHK(c, hipStreamWaitEvent(c->stream3, c->ev_mesh, 0));
+        RtTriLaunch f = a;
+        f.finish_part = RT_FIN_MESH;
+        e = rt_launch_split_finish(f, c->stream3);
+        if (e) return hip_fail(c, (hipError_t)e, "mesh-pixel sums");
+        HIPCHK(c, hipEventRecord(c->ev_fin3, c->stream3));
+    }
     if (a.split_spec) {
         /* the repair pass: the speculated pixels a camera ray of which missed the mesh, as long
            chains (seed pass, then every chunk), their count read on the device (usually none:
@@ -589,8 +606,16 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         if (!e) e = rt_launch_tris(r, RT_TRAV_BVH4Q, c->counting, 64, st);
         if (e) return hip_fail(c, (hipError_t)e, "repair launches");
     }
-    if (n_box) HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0));
-    return rt_launch_split_finish(a, st);
+    if (!n_box) return rt_launch_split_finish(a, st);
+    if (a.split_spec) { /* the repaired pixels */
+        RtTriLaunch f = a;
+        f.finish_part = RT_FIN_DIRTY;
+        e = rt_launch_split_finish(f, st);
+        if (e) return hip_fail(c, (hipError_t)e, "repaired-pixel sums");
+    }
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0));
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev_fin3, 0));
+    return RT_OK;
 }
 
 /* LPT scheduling of the pixel queue.  The reference's per-pixel cost is set by its paths: a
@@ -766,6 +791,9 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_split_box);
     if (c->ev_split0) (void)hipEventDestroy(c->ev_split0);
     if (c->ev_box) (void)hipEventDestroy(c->ev_box);
+    if (c->ev_mesh) (void)hipEventDestroy(c->ev_mesh);
+    if (c->ev_fin3) (void)hipEventDestroy(c->ev_fin3);
+    if (c->stream3) (void)hipStreamDestroy(c->stream3);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     free_dev(c->d_halo_rows);
     free_dev(c->d_halo_buf);

@@ -2454,40 +2454,123 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLa
     seed_pass<G>(a, s_stack);
 }
 
-/* Sample-split tiles, step 3: per pixel, the samples' radiance summed in sample order
+/* Sample-split tiles, step 3 (per part: the long chains after their chunks on the second stream,
+   the clean mesh pixels after theirs on a third, the repaired after the repair pass): per pixel,
+   the samples' radiance summed in sample order
    (raytracer.cl:228-230: the same additions on the same values as one lane's loop), the
    pixel written (:234-240) and its final seed (:241-242). */
 __global__ __launch_bounds__(RT_BLOCK) void k_split_finish(RtTriLaunch a)
 {
     const uint32_t npx = a.W * a.Hl;
-    const uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x;
-    if (p >= npx) return;
-    const uint32_t spp = a.sample_rate * a.sample_rate;
-    float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
-    for (uint32_t s = 0; s < spp; ++s) {
-        const float *c = a.split_col + ((size_t)s * npx + p) * 3u;
-        acc_x += c[0];
-        acc_y += c[1];
-        acc_z += c[2];
+    /* the items: every pixel, or a part's list (the long chains; the repaired pixels, their count
+       on the device), over a grid-stride loop */
+    const uint32_t n = a.finish_part == RT_FIN_LONG    ? a.split_n_box
+                       : a.finish_part == RT_FIN_DIRTY ? (uint32_t)a.counters[RT_CNT_REPAIR]
+                                                        : npx;
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < n; i += gridDim.x * RT_BLOCK) {
+        const uint32_t p = a.finish_part == RT_FIN_LONG ? a.split_box[i] : a.finish_part == RT_FIN_DIRTY ? a.split_repair[i] : i;
+        if (p >= npx) continue;
+        if (a.finish_part == RT_FIN_MESH && (a.pixel_class[p] >= 0 || (a.split_dirty && a.split_dirty[p] != ~0u)))
+            continue; /* the mesh pixels no chunk of which missed */
+        const uint32_t spp = a.sample_rate * a.sample_rate;
+        float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
+        /* 16 samples' loads issued together, then added in sample order (a part's few pixels are
+           latency-bound: one load per add would wait out each) */
+        for (uint32_t s0 = 0; s0 < spp; s0 += 16u) {
+            float v[48];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t s = s0 + (uint32_t)j < spp ? s0 + (uint32_t)j : spp - 1u;
+                const float *c = a.split_col + ((size_t)s * npx + p) * 3u;
+                v[3 * j] = c[0];
+                v[3 * j + 1] = c[1];
+                v[3 * j + 2] = c[2];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (s0 + (uint32_t)j < spp) {
+                    acc_x += v[3 * j];
+                    acc_y += v[3 * j + 1];
+                    acc_z += v[3 * j + 2];
+                }
+            }
+        }
+        const float nf = (float)spp;
+        float4 px = make_float4(acc_x / nf, acc_y / nf, acc_z / nf, 0.0f / nf);
+        float4 *dst = reinterpret_cast<float4 *>(a.out) + p;
+        if (a.progressive > 0) {
+            const float4 old = *dst;
+            const float t = 1.0f / (float)a.progressive;
+            px.x = old.x + (px.x - old.x) * t;
+            px.y = old.y + (px.y - old.y) * t;
+            px.z = old.z + (px.z - old.z) * t;
+            px.w = old.w + (px.w - old.w) * t;
+        }
+        *dst = px;
+        const uint32_t x = p % a.W, yl = p / a.W;
+        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+        const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * a.split_nseed + a.split_nseed - 1u];
+        a.seeds[slot] = sd.x;
+        a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
     }
-    const float n = (float)spp;
-    float4 px = make_float4(acc_x / n, acc_y / n, acc_z / n, 0.0f / n);
-    float4 *dst = reinterpret_cast<float4 *>(a.out) + p;
-    if (a.progressive > 0) {
-        const float4 old = *dst;
-        const float t = 1.0f / (float)a.progressive;
-        px.x = old.x + (px.x - old.x) * t;
-        px.y = old.y + (px.y - old.y) * t;
-        px.z = old.z + (px.z - old.z) * t;
-        px.w = old.w + (px.w - old.w) * t;
-    }
-    *dst = px;
-    const uint32_t x = p % a.W, yl = p / a.W;
-    const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
-    const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * a.split_nseed + a.split_nseed - 1u];
-    a.seeds[slot] = sd.x;
-    a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
 }
+
+/* The in-order sums of a part's listed pixels (the long chains, the repaired): a wave per pixel —
+   its lanes load the samples together (4 each per 256), then the wave adds them in sample order
+   through readlane, the same additions as k_split_finish's loop.  A part is a few thousand pixels
+   at most, latency-bound when one lane walks a pixel's samples. */
+__global__ __launch_bounds__(RT_BLOCK) void k_split_finish_list(RtTriLaunch a)
+{
+    const uint32_t npx = a.W * a.Hl, lane = threadIdx.x & 63u;
+    const uint32_t n = a.finish_part == RT_FIN_LONG ? a.split_n_box : (uint32_t)a.counters[RT_CNT_REPAIR];
+    const uint32_t spp = a.sample_rate * a.sample_rate;
+    for (uint32_t i = blockIdx.x * (RT_BLOCK / 64u) + (threadIdx.x >> 6); i < n; i += gridDim.x * (RT_BLOCK / 64u)) {
+        const uint32_t p = a.finish_part == RT_FIN_LONG ? a.split_box[i] : a.split_repair[i];
+        if (p >= npx) continue;
+        float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
+        for (uint32_t b = 0; b < spp; b += 256u) {
+            float v[12];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t s = b + lane * 4u + (uint32_t)j;
+                const float *c = a.split_col + ((size_t)(s < spp ? s : 0u) * npx + p) * 3u;
+                v[3 * j] = c[0];
+                v[3 * j + 1] = c[1];
+                v[3 * j + 2] = c[2];
+            }
+            const uint32_t lanes = (spp - b + 3u) / 4u < 64u ? (spp - b + 3u) / 4u : 64u;
+            for (uint32_t l = 0; l < lanes; ++l) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (b + l * 4u + (uint32_t)j < spp) {
+                        acc_x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[3 * j]), (int)l));
+                        acc_y += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[3 * j + 1]), (int)l));
+                        acc_z += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v[3 * j + 2]), (int)l));
+                    }
+                }
+            }
+        }
+        if (lane != 0u) continue;
+        const float nf = (float)spp;
+        float4 px = make_float4(acc_x / nf, acc_y / nf, acc_z / nf, 0.0f / nf);
+        float4 *dst = reinterpret_cast<float4 *>(a.out) + p;
+        if (a.progressive > 0) {
+            const float4 old = *dst;
+            const float t = 1.0f / (float)a.progressive;
+            px.x = old.x + (px.x - old.x) * t;
+            px.y = old.y + (px.y - old.y) * t;
+            px.z = old.z + (px.z - old.z) * t;
+            px.w = old.w + (px.w - old.w) * t;
+        }
+        *dst = px;
+        const uint32_t x = p % a.W, yl = p / a.W;
+        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+        const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * a.split_nseed + a.split_nseed - 1u];
+        a.seeds[slot] = sd.x;
+        a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
+    }
+}
+
 
 /* Camera-ray candidate lists.  A pixel's sampleRate^2 camera rays share the camera position
    and leave through the pixel's square (strat_rand offsets in [0, 1], raytracer.cl:216-224), so
@@ -2862,6 +2945,12 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
 
 int rt_launch_split_finish(const RtTriLaunch &a, void *stream)
 {
+    if (a.finish_part == RT_FIN_LONG || a.finish_part == RT_FIN_DIRTY) { /* a wave per listed pixel */
+        const uint32_t n = a.finish_part == RT_FIN_LONG ? a.split_n_box : 4096u; /* repairs: grid-stride */
+        const uint32_t blocks = std::min(2048u, std::max(1u, (n + 3u) / 4u));
+        hipLaunchKernelGGL(k_split_finish_list, dim3(blocks), dim3(RT_BLOCK), 0, (hipStream_t)stream, a);
+        return (int)hipGetLastError();
+    }
     hipLaunchKernelGGL(k_split_finish, dim3((a.W * a.Hl + RT_BLOCK - 1) / RT_BLOCK), dim3(RT_BLOCK), 0,
                        (hipStream_t)stream, a);
     return (int)hipGetLastError();

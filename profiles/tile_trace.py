@@ -1,7 +1,7 @@
 """Per-kernel spans of the last render in a rocprofv3 kernel trace of profiles/render_tile.py:
 each path-tracer kernel's start and end (ms, from the render's first kernel) and duration, so the
-two streams of a sample-split tile (the long chains' seed pass and chunks beside the mesh pixels'
-seed pass and chunks) can be read apart.
+streams of a sample-split tile (the long chains' seed pass, chunks and sums beside the mesh
+pixels' chunks, the repair pass and the sums) can be read apart.
 
     python profiles/tile_trace.py <rocprofv3 output dir>
 """
@@ -24,13 +24,16 @@ def main():
     path = glob.glob(f"{sys.argv[1]}/**/*kernel_trace.csv", recursive=True)[0]
     rows = [r for r in csv.DictReader(open(path)) if short(r["Kernel_Name"])]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # renders are separated by the k_split_finish (sample-split) or by the last k_tris launch
-    groups, cur = [], []
+    # renders are separated by idle gaps of the device (the host synchronises between them): a
+    # kernel starting 0.1 ms or more after every earlier kernel has ended opens a new render
+    groups, cur, busy_to = [], [], None
     for r in rows:
-        cur.append(r)
-        if "k_split_finish" in r["Kernel_Name"]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if cur and busy_to is not None and s - busy_to >= 100_000:
             groups.append(cur)
             cur = []
+        cur.append(r)
+        busy_to = e if busy_to is None else max(busy_to, e)
     if cur:
         groups.append(cur)
     last = groups[-1]

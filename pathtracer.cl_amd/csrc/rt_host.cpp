@@ -80,6 +80,12 @@ uint32_t probe_n(uint32_t sample_rate) { return sample_rate >= 2 ? kProbeN : 1u;
 #define RT_FETCH_K 24
 #endif
 constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
+#ifndef RT_LONG_FINE
+#define RT_LONG_FINE 1 /* samples per stored seed (and per chunk task) of the subtree-parallel long chains */
+#endif
+#ifndef RT_REPAIR_SLOTS
+#define RT_REPAIR_SLOTS 4096u /* repaired pixels with per-sample seeds by slot (8.4 MB at 256 spp) */
+#endif
 #ifndef RT_BOX_GRID_DIV
 #define RT_BOX_GRID_DIV 4 /* the long chains' seed pass takes at most 1/RT_BOX_GRID_DIV of the persistent grid */
 #endif
@@ -156,6 +162,10 @@ struct rt_ctx {
     uint32_t *d_split_counter = nullptr; /* [0]: the seed pass's cursor, [32]: the box pixels' (own line) */
     size_t split_seed_bytes = 0, split_col_bytes = 0;
     uint32_t *d_split_box = nullptr;  /* the box pixels (yl * W + x): their chains run on stream2 */
+    uint32_t *d_long_seed = nullptr;  /* the long chains' seeds by slot, one per RT_LONG_FINE samples */
+    size_t long_seed_bytes = 0;
+    uint32_t *d_repair_seed = nullptr; /* the repaired pixels' seeds by slot (the first RT_REPAIR_SLOTS of them) */
+    size_t repair_seed_bytes = 0;
     size_t split_box_cap = 0;
     uint32_t n_split_box = 0;
     int split_box_grid = 0;           /* the box pixels' seed-pass grid of the render being launched */
@@ -561,11 +571,32 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         b.split_chunks = (a.sample_rate * a.sample_rate + b.split_chunk - 1u) / b.split_chunk;
         HIPCHK(c, hipEventRecord(c->ev_split0, st));
         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split0, 0));
+        if (a.split_coop >= 8) {
+            /* the subtree-parallel pass stores a long chain's seed every RT_LONG_FINE samples into
+               a buffer of its own, by slot: their chunk tasks are that short, so the long chains'
+               last chunks (box paths, the costliest samples) do not trail the frame */
+            const uint32_t spp = a.sample_rate * a.sample_rate;
+            b.split_fine = RT_LONG_FINE;
+            b.split_chunk = RT_LONG_FINE;
+            b.split_chunks = (spp + RT_LONG_FINE - 1u) / RT_LONG_FINE;
+            b.split_nseed = b.split_chunks + 1u;
+            const size_t bytes = (size_t)n_box * b.split_nseed * 8u;
+            if (c->long_seed_bytes < bytes) {
+                free_dev(c->d_long_seed);
+    free_dev(c->d_repair_seed);
+                c->d_long_seed = nullptr;
+                c->long_seed_bytes = 0;
+                HIPCHK(c, hipMalloc(&c->d_long_seed, bytes));
+                c->long_seed_bytes = bytes;
+            }
+            b.split_seed = c->d_long_seed;
+            b.split_seed_slot = 1;
+        }
         const int chunk_grid = (int)std::min<uint64_t>((uint64_t)blocks, ((uint64_t)n_box * b.split_chunks + RT_BLOCK - 1) / RT_BLOCK);
         int e = rt_launch_split_seeds(b, c->stream2);
         if (!e) e = rt_launch_tris(b, RT_TRAV_BVH4Q, c->counting, std::max(1, chunk_grid), c->stream2);
-        RtTriLaunch f = a; /* the long chains' in-order sums, as soon as their chunks are done */
-        f.finish_part = RT_FIN_LONG;
+        RtTriLaunch f = b; /* the long chains' in-order sums, as soon as their chunks are done */
+        f.finish_part = RT_FIN_LIST;
         if (!e) e = rt_launch_split_finish(f, c->stream2);
         if (e) return hip_fail(c, (hipError_t)e, "box-pixel split launches");
         HIPCHK(c, hipEventRecord(c->ev_box, c->stream2));
@@ -584,10 +615,13 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         if (e) return hip_fail(c, (hipError_t)e, "mesh-pixel sums");
         HIPCHK(c, hipEventRecord(c->ev_fin3, c->stream3));
     }
+    if (!n_box) return rt_launch_split_finish(a, st);
     if (a.split_spec) {
         /* the repair pass: the speculated pixels a camera ray of which missed the mesh, as long
-           chains (seed pass, then every chunk), their count read on the device (usually none:
-           the grids find no item and end) */
+           chains from their first missed chunk (seed pass, chunks, sums), their count read on
+           the device (usually none: the grids find no item and end).  With the subtree-parallel
+           pass the first RT_REPAIR_SLOTS of them store a seed per sample by slot, so their chunk
+           tasks are single samples; any beyond take the per-pixel seeds */
         RtTriLaunch r = a;
         r.split_spec = 0;
         r.split_which = RT_SPLIT_BOX;
@@ -602,16 +636,35 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_chunks = (a.sample_rate * a.sample_rate + r.split_chunk - 1u) / r.split_chunk;
         r.split_restart = a.split_dirty; /* each chain from its first missed chunk on */
         r.split_restart_chunk = a.split_chunk;
+        r.finish_part = RT_FIN_LIST;
+        if (a.split_coop >= 8) {
+            const uint32_t spp = a.sample_rate * a.sample_rate;
+            RtTriLaunch s = r;
+            s.split_fine = RT_LONG_FINE;
+            s.split_chunk = RT_LONG_FINE;
+            s.split_chunks = (spp + RT_LONG_FINE - 1u) / RT_LONG_FINE;
+            s.split_nseed = s.split_chunks + 1u;
+            s.split_item_cap = RT_REPAIR_SLOTS;
+            const size_t bytes = (size_t)RT_REPAIR_SLOTS * s.split_nseed * 8u;
+            if (c->repair_seed_bytes < bytes) {
+                free_dev(c->d_repair_seed);
+                c->d_repair_seed = nullptr;
+                c->repair_seed_bytes = 0;
+                HIPCHK(c, hipMalloc(&c->d_repair_seed, bytes));
+                c->repair_seed_bytes = bytes;
+            }
+            s.split_seed = c->d_repair_seed;
+            s.split_seed_slot = 1;
+            e = rt_launch_split_seeds(s, st);
+            if (!e) e = rt_launch_tris(s, RT_TRAV_BVH4Q, c->counting, 128, st);
+            if (!e) e = rt_launch_split_finish(s, st);
+            if (e) return hip_fail(c, (hipError_t)e, "repair launches");
+            r.split_item_base = RT_REPAIR_SLOTS; /* the rest, if any */
+        }
         e = rt_launch_split_seeds(r, st);
         if (!e) e = rt_launch_tris(r, RT_TRAV_BVH4Q, c->counting, 64, st);
+        if (!e) e = rt_launch_split_finish(r, st);
         if (e) return hip_fail(c, (hipError_t)e, "repair launches");
-    }
-    if (!n_box) return rt_launch_split_finish(a, st);
-    if (a.split_spec) { /* the repaired pixels */
-        RtTriLaunch f = a;
-        f.finish_part = RT_FIN_DIRTY;
-        e = rt_launch_split_finish(f, st);
-        if (e) return hip_fail(c, (hipError_t)e, "repaired-pixel sums");
     }
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0));
     HIPCHK(c, hipStreamWaitEvent(st, c->ev_fin3, 0));
@@ -783,6 +836,7 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_flags);
     free_dev(c->d_class);
     free_dev(c->d_split_seed);
+    free_dev(c->d_long_seed);
     free_dev(c->d_split_col);
     free_dev(c->d_split_counter);
     free_dev(c->d_split_dirty);

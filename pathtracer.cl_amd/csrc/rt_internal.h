@@ -205,10 +205,14 @@ struct RtTriLaunch {
                                       the chunks before it stand (NULL: from the frame seed) */
     uint32_t split_restart_chunk;
     uint32_t finish_part; /* k_split_finish: RT_FIN_ALL, or the pixels of one part (pixel_class, split_dirty) */
+    uint32_t split_seed_slot; /* RT_SPLIT_BOX: split_seed indexed by the item (the chain's slot in its list, minus
+                                 split_item_base: its own buffer, a seed per split_fine samples), not by pixel */
+    uint32_t split_item_base, split_item_cap; /* RT_SPLIT_BOX: the items split_box[base ...], at most cap (0: all) */
 };
 enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
-/* k_split_finish parts: every pixel; the long chains; the mesh pixels no chunk of which missed; the repaired */
-enum { RT_FIN_ALL = 0, RT_FIN_LONG = 1, RT_FIN_MESH = 2, RT_FIN_DIRTY = 3 };
+/* k_split_finish parts: every pixel; a list's pixels (split_box: the long chains, the repaired); the mesh
+   pixels no chunk of which missed */
+enum { RT_FIN_ALL = 0, RT_FIN_LIST = 1, RT_FIN_MESH = 2 };
 #define RT_SEED_COOP4 3 /* split_coop: the 4-lane cooperative seed pass (coop_round) */
 #define RT_COOP_STACK (RT_STACK_DEPTH * 4) /* LDS stack entries of a 4-lane query group (k_split_seeds) */
 #ifndef RT_LIST_MAX

@@ -578,6 +578,15 @@ __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long 
     return item;
 }
 
+/* RT_SPLIT_BOX launches: the number of items of split_box[split_item_base ...] this launch takes
+   (the list's length from the device when split_n_dev is set), at most split_item_cap */
+__device__ __forceinline__ uint32_t box_items(const RtTriLaunch &a)
+{
+    const uint32_t n = a.split_n_dev ? *a.split_n_dev : a.split_n_box;
+    const uint32_t m = n > a.split_item_base ? n - a.split_item_base : 0u;
+    return a.split_item_cap && m > a.split_item_cap ? a.split_item_cap : m;
+}
+
 /* shader-clock timestamp (s_memtime), counting launches only */
 __device__ __forceinline__ unsigned long long wave_clock()
 {
@@ -902,7 +911,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3, tiles_y = (a.Hl + 7u) >> 3;
-    const uint32_t n_items = a.split_which == RT_SPLIT_BOX ? (a.split_n_dev ? *a.split_n_dev : a.split_n_box)
+    const uint32_t n_items = a.split_which == RT_SPLIT_BOX ? box_items(a)
                                                            : tiles_x * tiles_y * 64u;
     const uint32_t nl = a.n_lights;
     const float hw = uniform_f(((float)a.W) / 2.0f);
@@ -944,7 +953,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 if (item < n_items) {
                     bool take;
                     if (a.split_which == RT_SPLIT_BOX) { /* the box pixels (long chains), by slot */
-                        const uint32_t p = a.split_box[item];
+                        const uint32_t p = a.split_box[a.split_item_base + item];
                         x = p % a.W;
                         yl = p / a.W;
                         take = true;
@@ -1378,6 +1387,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
     __shared__ uint4 s_erec[G][4]; /* per edge: its parent's record */
     __shared__ int s_par[G], s_slot[G];
     __shared__ int s_ne;
+    if (box_items(a) == 0u) return; /* an empty list (the repair pass, mostly): no cut to make */
     const uint4 *__restrict__ qn = reinterpret_cast<const uint4 *>(a.nodes);
     if (threadIdx.x == 0) s_ne = chain_cut<G>(qn, a.n_nodes4, s_par, s_slot);
     __syncthreads();
@@ -1396,14 +1406,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
     const uint32_t spp = a.sample_rate * a.sample_rate, fine = a.split_fine, nseed = a.split_nseed;
     const uint32_t plane = a.Wpad * a.Hpad;
     const uint32_t tiles_x = (a.W + 7u) >> 3;
-    const uint32_t n_items = a.split_n_dev ? *a.split_n_dev : a.split_n_box;
+    const uint32_t n_items = box_items(a);
     const uint32_t nl = a.n_lights;
     const float hw = uniform_f(((float)a.W) / 2.0f);
     const float hh = uniform_f(((float)a.H) / 2.0f);
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
     const uint32_t gpw = a.split_gpw ? a.split_gpw : 64u / G;
     bool have = false, next = false, running = false, fin = false, drained = false, live = false, ghit = false;
-    uint32_t x = 0, yl = 0, sample = 0, depth = 0;
+    uint32_t x = 0, yl = 0, sample = 0, depth = 0, pslot = 0; /* pslot: the chain's seeds (pixel or slot) */
     uint32_t lpack = RT_LPACK_NONE;
     uint32_t bnext = 0, bend = 0;
     Seed seed = {0u, 0u};
@@ -1437,7 +1447,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
             item = __shfl(item, gbase);
             drained = bnext >= n_items;
             if (!have && item < n_items) {
-                const uint32_t p = a.split_box[item];
+                const uint32_t p = a.split_box[a.split_item_base + item];
+                pslot = a.split_seed_slot ? item : p;
                 x = p % a.W;
                 yl = p / a.W;
                 const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
@@ -1514,7 +1525,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                 next = false;
                 if ((sample == spp || sample % fine == 0u) && lane == gbase) {
                     const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
-                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)pslot * nseed + c] = make_uint2(seed.x, seed.y);
                 }
                 if (sample == spp) {
                     have = false;
@@ -1671,7 +1682,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const uint32_t tiles_y = (a.Hl + 7u) >> 3;
     const uint32_t n_items = tiles_x * tiles_y * 64u;
     const uint32_t n_tasks =
-        SPLIT ? (a.split_which == RT_SPLIT_BOX ? (a.split_n_dev ? *a.split_n_dev : a.split_n_box) : n_items) * a.split_chunks
+        SPLIT ? (a.split_which == RT_SPLIT_BOX ? box_items(a) : n_items) * a.split_chunks
               : n_items;
     /* launch-uniform values pinned to SGPRs (readfirstlane), so they neither occupy nor
        spill vector registers */
@@ -1858,7 +1869,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 dst[2] = col_z;
                 ++sample;
                 mode = (sample >= spp || sample % a.split_chunk == 0u) ? M_IDLE : M_NEWSAMPLE;
-                if (sample >= spp) /* the pixel's final seed, from its last chunk's own draws */
+                if (sample >= spp && !a.split_seed_slot) /* the pixel's final seed, from its last chunk's own draws
+                                                            (a slotted long chain's: from its seed pass) */
                     reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + a.split_nseed - 1u] =
                         make_uint2(seed.x, seed.y);
                 if (mode == M_IDLE) {
@@ -1954,13 +1966,15 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                        pixels: a pixel's chunks in turn */
                     uint32_t tile = item >> 6, chunk = 0;
                     const uint32_t in = item & 63u;
+                    uint32_t sbase = 0; /* the task's seeds in split_seed (x split_nseed): its pixel or its long-chain slot */
                     bool take;
                     if (SPLIT && a.split_which == RT_SPLIT_BOX) {
                         const uint32_t slot = item / a.split_chunks;
                         chunk = item - slot * a.split_chunks;
-                        const uint32_t p = a.split_box[slot];
+                        const uint32_t p = a.split_box[a.split_item_base + slot];
                         x = p % a.W;
                         yl = p / a.W;
+                        sbase = a.split_seed_slot ? slot : p;
                         /* a repaired pixel: its chunks before the first missed one stand */
                         take = !a.split_restart || chunk * a.split_chunk >= a.split_restart[p] * a.split_restart_chunk;
                     } else {
@@ -1972,6 +1986,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         x = (tile % tiles_x) * 8u + (in & 7u);
                         yl = (tile / tiles_x) * 8u + (in >> 3);
                         take = x < a.W && yl < a.Hl;
+                        sbase = yl * a.W + x;
                         if (SPLIT && take && a.split_which == RT_SPLIT_MESH)
                             take = a.pixel_class[(size_t)yl * a.W + x] == -1;
                     }
@@ -1991,7 +2006,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         seed.y = mwc_jump<18000u>(a.seeds[plane + slot], k, a.split_spec_mul[2 * chunk + 1]);
                     } else if (SPLIT && take) { /* the chunk's first seed, from the seed pass */
                         const uint2 sd = reinterpret_cast<const uint2 *>(
-                            a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + chunk * a.split_chunk / a.split_fine];
+                            a.split_seed)[(size_t)sbase * a.split_nseed + chunk * a.split_chunk / a.split_fine];
                         seed.x = sd.x;
                         seed.y = sd.y;
                     }
@@ -2462,13 +2477,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_split_seeds(RtTriLa
 __global__ __launch_bounds__(RT_BLOCK) void k_split_finish(RtTriLaunch a)
 {
     const uint32_t npx = a.W * a.Hl;
-    /* the items: every pixel, or a part's list (the long chains; the repaired pixels, their count
-       on the device), over a grid-stride loop */
-    const uint32_t n = a.finish_part == RT_FIN_LONG    ? a.split_n_box
-                       : a.finish_part == RT_FIN_DIRTY ? (uint32_t)a.counters[RT_CNT_REPAIR]
-                                                        : npx;
+    /* every pixel, or the clean mesh pixels (RT_FIN_MESH), over a grid-stride loop */
+    const uint32_t n = npx;
     for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < n; i += gridDim.x * RT_BLOCK) {
-        const uint32_t p = a.finish_part == RT_FIN_LONG ? a.split_box[i] : a.finish_part == RT_FIN_DIRTY ? a.split_repair[i] : i;
+        const uint32_t p = i;
         if (p >= npx) continue;
         if (a.finish_part == RT_FIN_MESH && (a.pixel_class[p] >= 0 || (a.split_dirty && a.split_dirty[p] != ~0u)))
             continue; /* the mesh pixels no chunk of which missed */
@@ -2522,10 +2534,10 @@ __global__ __launch_bounds__(RT_BLOCK) void k_split_finish(RtTriLaunch a)
 __global__ __launch_bounds__(RT_BLOCK) void k_split_finish_list(RtTriLaunch a)
 {
     const uint32_t npx = a.W * a.Hl, lane = threadIdx.x & 63u;
-    const uint32_t n = a.finish_part == RT_FIN_LONG ? a.split_n_box : (uint32_t)a.counters[RT_CNT_REPAIR];
+    const uint32_t n = box_items(a);
     const uint32_t spp = a.sample_rate * a.sample_rate;
     for (uint32_t i = blockIdx.x * (RT_BLOCK / 64u) + (threadIdx.x >> 6); i < n; i += gridDim.x * (RT_BLOCK / 64u)) {
-        const uint32_t p = a.finish_part == RT_FIN_LONG ? a.split_box[i] : a.split_repair[i];
+        const uint32_t p = a.split_box[a.split_item_base + i];
         if (p >= npx) continue;
         float acc_x = 0.0f, acc_y = 0.0f, acc_z = 0.0f;
         for (uint32_t b = 0; b < spp; b += 256u) {
@@ -2565,7 +2577,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_split_finish_list(RtTriLaunch a)
         *dst = px;
         const uint32_t x = p % a.W, yl = p / a.W;
         const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
-        const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * a.split_nseed + a.split_nseed - 1u];
+        const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)(a.split_seed_slot ? i : p) * a.split_nseed + a.split_nseed - 1u];
         a.seeds[slot] = sd.x;
         a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
     }
@@ -2945,8 +2957,8 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
 
 int rt_launch_split_finish(const RtTriLaunch &a, void *stream)
 {
-    if (a.finish_part == RT_FIN_LONG || a.finish_part == RT_FIN_DIRTY) { /* a wave per listed pixel */
-        const uint32_t n = a.finish_part == RT_FIN_LONG ? a.split_n_box : 4096u; /* repairs: grid-stride */
+    if (a.finish_part == RT_FIN_LIST) { /* a wave per listed pixel */
+        const uint32_t n = a.split_n_dev ? 4096u : a.split_n_box; /* a count on the device: grid-stride */
         const uint32_t blocks = std::min(2048u, std::max(1u, (n + 3u) / 4u));
         hipLaunchKernelGGL(k_split_finish_list, dim3(blocks), dim3(RT_BLOCK), 0, (hipStream_t)stream, a);
         return (int)hipGetLastError();

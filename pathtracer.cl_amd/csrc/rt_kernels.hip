@@ -1207,6 +1207,9 @@ __device__ __forceinline__ uint32_t mwc_jump(uint32_t x, uint32_t k, uint32_t mu
 #ifndef RT_CHAIN_IMM
 #define RT_CHAIN_IMM 2 /* path-advance passes per iteration */
 #endif
+#ifndef RT_REPAIR_RUNS
+#define RT_REPAIR_RUNS 1 /* the repair pass takes its chains' hit samples in runs of G - 1 */
+#endif
 #ifndef RT_CHAIN_UNROLL
 #define RT_CHAIN_UNROLL 3 /* traversal steps per iteration (1 / 2 / 3 / 4: 8-way tile 16.8 / 16.4 / 16.3 / 16.4 ms, r04h2) */
 #endif
@@ -1379,7 +1382,7 @@ __device__ __forceinline__ V3 group_camera_dir(const rt_camera &cam, float a, fl
     return v3(__shfl(q, gbase), __shfl(q, gbase + 1), __shfl(q, gbase + 2));
 }
 
-template <int G>
+template <int G, bool RUNS = false> /* RUNS: the repair pass's runs of hit samples */
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLaunch a)
 {
     static_assert(G >= 8 && G <= 64 && (G & (G - 1)) == 0, "the advance spreads 6 divisions over the group's lanes");
@@ -1521,7 +1524,51 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                     next = true;
                 }
             }
-            if (next) {
+            bool run_on = false;
+            if (RT_REPAIR_RUNS && RUNS && next && a.split_restart && sample < spp && lpack != RT_LPACK_NONE &&
+                lpack != RT_LPACK_EMPTY) {
+                /* the repair pass (a speculated pixel's chain): a run of up to G - 1 samples at once,
+                   one per lane, each from the seed it has if every earlier sample of the run hit the
+                   mesh (split_spec_draws numbers each, rtcommon.h:411-421), its camera ray tested
+                   against the pixel's candidate list; the chain takes the run up to its first miss */
+                const uint32_t D = a.split_spec_draws, rem = spp - sample;
+                const uint32_t runmax = rem < (uint32_t)(G - 1) ? rem : (uint32_t)(G - 1);
+                Seed sl = seed;
+                for (uint32_t i = 0; i < (uint32_t)sub * D; ++i) { /* frand's state steps (rng.h:24-42) */
+                    sl.x = 36969u * (sl.x & 65535u) + (sl.x >> 16);
+                    sl.y = 18000u * (sl.y & 65535u) + (sl.y >> 16);
+                }
+                bool hit = false;
+                if ((uint32_t)sub < runmax) {
+                    const uint32_t s = sample + (uint32_t)sub;
+                    Seed sc = sl;
+                    const uint32_t sx = s / a.sample_rate, sy = s % a.sample_rate;
+                    const float fa = (float)x + strat_rand(sc, (int)sx, (int)a.sample_rate);
+                    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                    const float fb = (float)y + strat_rand(sc, (int)sy, (int)a.sample_rate);
+                    const V3 o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
+                    const V3 dd = camera_dir(a.cam, fa - hw, fb - hh);
+                    const uint32_t pc = (lpack & (RT_LIST_MAX - 1u)) + 1u, first = (lpack >> RT_LIST_BITS) << 3;
+                    for (uint32_t t = 0; t < pc && !hit; ++t) {
+                        const uint32_t r = first + t;
+                        float tt = 0.0f;
+                        const bool h = mt_test(o, dd, tris[3 * r], tris[3 * r + 1], tris[3 * r + 2], tt);
+                        hit = h && !(tt < RT_SMALL_F) && tt <= kInf; /* the closest-hit acceptance */
+                    }
+                }
+                const uint32_t hm = (uint32_t)((__ballot(hit) & gmask) >> gbase);
+                const uint32_t m = (uint32_t)__builtin_ctz(~hm); /* the run's hits before its first miss */
+                if ((uint32_t)sub < m && (sample + (uint32_t)sub) % fine == 0u)
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)pslot * nseed + (sample + (uint32_t)sub) / fine] =
+                        make_uint2(sl.x, sl.y);
+                seed.x = (uint32_t)__shfl((int)sl.x, gbase + (int)m);
+                seed.y = (uint32_t)__shfl((int)sl.y, gbase + (int)m);
+                sample += m;
+                /* a whole run of hits: the next run in the next pass; else the missed sample (or the
+                   chain's end) goes on below */
+                run_on = m == runmax && sample < spp;
+            }
+            if (next && !run_on) {
                 next = false;
                 if ((sample == spp || sample % fine == 0u) && lane == gbase) {
                     const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
@@ -2946,7 +2993,8 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
     if (e != hipSuccess) return (int)e;
     const dim3 g(a.split_seed_blocks), b(RT_BLOCK);
     if (a.split_which == RT_SPLIT_BOX && a.split_coop >= 8) { /* subtree-parallel */
-        if (a.split_coop == 8) hipLaunchKernelGGL(k_chain_seeds<8>, g, b, 0, st, a);
+        if (a.split_coop == 8 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<8, true>), g, b, 0, st, a);
+        else if (a.split_coop == 8) hipLaunchKernelGGL(k_chain_seeds<8>, g, b, 0, st, a);
         else if (a.split_coop == 32) hipLaunchKernelGGL(k_chain_seeds<32>, g, b, 0, st, a);
         else if (a.split_coop == 64) hipLaunchKernelGGL(k_chain_seeds<64>, g, b, 0, st, a);
         else hipLaunchKernelGGL(k_chain_seeds<16>, g, b, 0, st, a);

@@ -1154,8 +1154,9 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr, width):
     rt.close()
 
 
+@pytest.mark.parametrize("width", [8, 3])
 @pytest.mark.parametrize("spec", ["2", "0"])
-def test_speculated_pixels_repaired_vs_oracle(pt, oracle, monkeypatch, spec):
+def test_speculated_pixels_repaired_vs_oracle(pt, oracle, monkeypatch, spec, width):
     """Speculated mesh pixels (their chunk seeds jumped ahead from the frame seed, DESIGN.md
     §4.5) whose camera rays miss the mesh after all are repaired: with RT_SPLIT_SPEC=2 every
     pixel whose probe rays all hit is speculated, silhouettes included, so some chunks meet a
@@ -1165,6 +1166,7 @@ def test_speculated_pixels_repaired_vs_oracle(pt, oracle, monkeypatch, spec):
     pixel through the seed pass) equals it too."""
     monkeypatch.setenv("RT_SPLIT", "1")
     monkeypatch.setenv("RT_SPLIT_SPEC", spec)
+    monkeypatch.setenv("RT_SEED_WIDTH", str(width))  # the long chains' (and repairs') pass: 8 lanes / cooperative
     sc = pt.scenes
     W, H, sr = 128, 96, 8
     Wp, Hp = sc.padded_dims(W, H)

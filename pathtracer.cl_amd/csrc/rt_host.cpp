@@ -83,6 +83,9 @@ constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
 #ifndef RT_LONG_FINE
 #define RT_LONG_FINE 1 /* samples per stored seed (and per chunk task) of the subtree-parallel long chains */
 #endif
+#ifndef RT_REPAIR_WIDTH
+#define RT_REPAIR_WIDTH 16u /* lanes per repaired chain: its hit samples in runs of 15 */
+#endif
 #ifndef RT_REPAIR_SLOTS
 #define RT_REPAIR_SLOTS 4096u /* repaired pixels with per-sample seeds by slot (8.4 MB at 256 spp) */
 #endif
@@ -639,6 +642,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.finish_part = RT_FIN_LIST;
         if (a.split_coop >= 8) {
             const uint32_t spp = a.sample_rate * a.sample_rate;
+            r.split_coop = RT_REPAIR_WIDTH; /* runs of width - 1 hit samples (k_chain_seeds<width, true>) */
             RtTriLaunch s = r;
             s.split_fine = RT_LONG_FINE;
             s.split_chunk = RT_LONG_FINE;

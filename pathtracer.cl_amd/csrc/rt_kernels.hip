@@ -2993,7 +2993,8 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
     if (e != hipSuccess) return (int)e;
     const dim3 g(a.split_seed_blocks), b(RT_BLOCK);
     if (a.split_which == RT_SPLIT_BOX && a.split_coop >= 8) { /* subtree-parallel */
-        if (a.split_coop == 8 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<8, true>), g, b, 0, st, a);
+        if (a.split_coop == 16 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<16, true>), g, b, 0, st, a);
+        else if (a.split_coop == 8 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<8, true>), g, b, 0, st, a);
         else if (a.split_coop == 8) hipLaunchKernelGGL(k_chain_seeds<8>, g, b, 0, st, a);
         else if (a.split_coop == 32) hipLaunchKernelGGL(k_chain_seeds<32>, g, b, 0, st, a);
         else if (a.split_coop == 64) hipLaunchKernelGGL(k_chain_seeds<64>, g, b, 0, st, a);

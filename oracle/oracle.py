@@ -56,6 +56,18 @@ class Oracle:
         L.or_render_tris.restype = i32
         L.or_closest_hits.argtypes = [vp, u32, vp, vp, u32, vp, vp]
         L.or_any_hits.argtypes = [vp, u32, vp, vp, u32, vp]
+        L.or_render_tris_bvh.argtypes = L.or_render_tris.argtypes + [vp]
+        L.or_render_tris_bvh.restype = i32
+        L.or_bvh_build.argtypes = [vp, u32, vp, u32]
+        L.or_bvh_build.restype = vp
+        L.or_bvh_free.argtypes = [vp]
+        L.or_bvh_free.restype = None
+        L.or_bvh_nodes.argtypes = [vp]
+        L.or_bvh_nodes.restype = u32
+        L.or_bvh_depth.argtypes = [vp]
+        L.or_bvh_depth.restype = u32
+        L.or_closest_hits_bvh.argtypes = [vp, u32, vp, vp, vp, vp, vp]
+        L.or_any_hits_bvh.argtypes = [vp, u32, vp, vp, vp, vp]
         for f in ("sin", "cos", "exp", "log"):
             fn = getattr(L, f"or_math_{f}")
             fn.argtypes = [ctypes.c_float]
@@ -68,7 +80,7 @@ class Oracle:
     def render_spheres(self, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds,
                        single_sample=False, nthreads=None):
         c = Counters()
-        nthreads = nthreads or min(os.cpu_count() or 1, 16)
+        nthreads = nthreads or _threads()
         st = self.lib.or_render_spheres(_p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad, sample_rate,
                                         max_depth, progressive, _p(seeds), int(single_sample), nthreads,
                                         ctypes.byref(c))
@@ -76,16 +88,42 @@ class Oracle:
         return c.closest, c.shadow
 
     def render_tris(self, out, cam, spheres, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds, verts,
-                    idx, pixels=None, max_samples=0, nthreads=None):
+                    idx, pixels=None, max_samples=0, nthreads=None, bvh: "MeshBVH | None" = None):
+        """raytrace_tris (raytracer.cl:184-243); bvh=None: the reference's linear loops, else the
+        independent BVH mode over the same mesh (same results, O(log N) per ray)."""
         c = Counters()
-        nthreads = nthreads or min(os.cpu_count() or 1, 16)
+        nthreads = nthreads or _threads()
         n_tris = idx.size // 3
+        if pixels is not None:
+            pixels = np.ascontiguousarray(pixels, np.uint32)  # a strided view would pass other pixels
         npx = 0 if pixels is None else len(pixels)
-        st = self.lib.or_render_tris(_p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad, sample_rate,
-                                     max_depth, progressive, _p(seeds), _p(verts), _p(idx), n_tris, _p(pixels), npx,
-                                     max_samples, nthreads, ctypes.byref(c))
+        args = (_p(out), _p(cam), _p(spheres), len(spheres), W, H, Wpad, Hpad, sample_rate, max_depth, progressive,
+                _p(seeds), _p(verts), _p(idx), n_tris, _p(pixels), npx, max_samples, nthreads, ctypes.byref(c))
+        if bvh is None:
+            st = self.lib.or_render_tris(*args)
+        else:
+            assert bvh.n_tris == n_tris
+            st = self.lib.or_render_tris_bvh(*args, ctypes.c_void_p(bvh.handle))
         assert st == 0
         return c.closest, c.shadow
+
+    def build_bvh(self, verts, idx) -> "MeshBVH":
+        """The oracle's own BVH over the mesh (oracle/pt_oracle.c or_bvh_build)."""
+        return MeshBVH(self, verts, idx)
+
+    def closest_hits_bvh(self, rays, bvh):
+        n = len(rays)
+        oi = np.empty(n, np.int32)
+        ot = np.empty(n, np.float32)
+        self.lib.or_closest_hits_bvh(_p(rays), n, _p(bvh.verts), _p(bvh.idx), ctypes.c_void_p(bvh.handle), _p(oi),
+                                     _p(ot))
+        return oi, ot
+
+    def any_hits_bvh(self, rays, bvh):
+        n = len(rays)
+        oi = np.empty(n, np.int32)
+        self.lib.or_any_hits_bvh(_p(rays), n, _p(bvh.verts), _p(bvh.idx), ctypes.c_void_p(bvh.handle), _p(oi))
+        return oi
 
     MATH_FN = {"sin": 0, "cos": 1, "exp": 2, "log": 3, "pow": 4, "sincos_s": 5, "sincos_c": 6}
 
@@ -109,6 +147,42 @@ class Oracle:
         oi = np.empty(n, np.int32)
         self.lib.or_any_hits(_p(rays), n, _p(verts), _p(idx), idx.size // 3, _p(oi))
         return oi
+
+
+def _threads() -> int:
+    """Worker threads for oracle renders: the CPUs this process may run on (the GPU box grants
+    a share of a large machine, os.cpu_count() shows all of it), at most 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+class MeshBVH:
+    """Handle of an or_bvh (the oracle's independent BVH mode); keeps the mesh arrays alive."""
+
+    def __init__(self, orc: Oracle, verts, idx):
+        self.lib = orc.lib
+        self.verts = np.ascontiguousarray(verts, np.float32)
+        self.idx = np.ascontiguousarray(idx, np.int32)
+        self.n_tris = self.idx.size // 3
+        self.handle = self.lib.or_bvh_build(_p(self.verts), self.verts.size // 3, _p(self.idx), self.n_tris)
+        if not self.handle:
+            raise ValueError("or_bvh_build failed (empty mesh or index out of range)")
+        self.n_nodes = self.lib.or_bvh_nodes(ctypes.c_void_p(self.handle))
+        self.depth = self.lib.or_bvh_depth(ctypes.c_void_p(self.handle))
+
+    def close(self):
+        if self.handle:
+            self.lib.or_bvh_free(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Reference:

@@ -21,6 +21,8 @@
  * Build: gcc -O2 -ffp-contract=off -fno-fast-math (x86-64 SSE: no excess
  * precision, no FMA).
  */
+#include <float.h>
+#include <math.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -36,10 +38,13 @@ typedef struct or_counters {
     uint64_t shadow;  /* any-hit queries (visibility_test[_tri]) */
 } or_counters;
 
+struct or_bvh;
+
 typedef struct or_mesh {
     const rt_vec3 *verts;
     const int32_t *idx;
     uint32_t n_tris;
+    const struct or_bvh *bvh; /* NULL: the reference's linear loops; else the independent BVH mode */
 } or_mesh;
 
 /* ------------------------------------------------------------------ rng.h */
@@ -379,6 +384,415 @@ OR_API int or_visibility_test_tri(const rt_ray *ray, const rt_vec3 *verts, const
     return 1;
 }
 
+/* ------------------------------------------- independent BVH mode (oracle) */
+/*
+ * A second, independent way to answer rtcommon.h:39-52 and :59-68 exactly: a plain binary BVH
+ * over the mesh (binned SAH on centroids, leaves of at most 4 triangles), boxes in binary64,
+ * no quantisation, no determinant cull, no unhittable-triangle cull, no candidate lists — none
+ * of the product's (csrc/rt_bvh.cpp, rt_quant.h) machinery.  It exists so that whole frames at
+ * the BASELINE sizes can be checked bit for bit in seconds instead of days (the linear loop is
+ * O(N) per ray).  Its answers are the linear loop's by construction:
+ *   - every triangle is tested with the reference's own Moller-Trumbore arithmetic
+ *     (or_get_triangle + mt_core: the same IEEE operations as or_intersects_triangle);
+ *   - closest hit: the linear loop accepts tmin <= t <= (its current tmax), so it ends on the
+ *     minimum accepted t with ties to the HIGHEST index; here: accept iff t >= tmin, t <= the
+ *     ray's tmax, and (t < best_t or (t == best_t and index > best_index)) — order-free;
+ *   - any hit: strict tmin < t < tmax (intersects_triangle_p), any order, first found;
+ *   - culling is conservative: a node is skipped only if no triangle below it can be accepted.
+ *     The float test accepts a line whose exact barycentrics lie within the MT rounding error
+ *     of the triangle, and reports a t within its own rounding error of the exact crossing.
+ *     Per node visit both are bounded from the node's largest |e1||e2| and |e1|+|e2|, the ray
+ *     origin's distance to the node (|T| = |o - v0|) and the threshold |det| >= 1e-4
+ *     (geometryFuncs.h:167): with u = 2^-24,
+ *        det_lo = 1e-4 - 8u|d|A,  Db = u(9 L|T||d| + 9 A|d|) / det_lo + 3u   (barycentric error),
+ *        pad    = 16 Db L + 4u|T|                                           (spatial error),
+ *        Dt     = 4 [u(9|T|A + 8 tb|d|A) / det_lo + 2u tb],  tb = (|T| + pad)/|d|  (t error),
+ *     i.e. four times the first-order bounds of the operations (cross and dot products: 2-3
+ *     roundings each, the division: one).  The node box is widened by pad and
+ *     the ray's interval by Dt before the slab test (binary64).  A node whose det_lo would fall
+ *     below 0.5e-4 (|e1||e2| > ~100: no such triangle in any scene here) is always visited.
+ * Pinned on the CPU against the linear loop on the golden fixtures and on random and grazing
+ * rays (tests/test_oracle_golden.py), and against the reference kernel on strided pixels.
+ */
+typedef struct or_bnode {
+    double lo[3], hi[3]; /* box of the subtree's float triangles (v0, v0 + e1, v0 + e2) */
+    double amax, lmax;   /* max |e1||e2| and max |e1| + |e2| over the subtree */
+    int32_t a, b;        /* inner: children a, b; leaf: a = -1 - first (into tri), b = count */
+} or_bnode;
+
+typedef struct or_bvh {
+    or_bnode *nodes;
+    uint32_t *tri; /* leaf order -> original triangle index */
+    uint32_t n_nodes, n_tris, depth;
+} or_bvh;
+
+/* rtcommon.h/geometryFuncs.h:160-202 up to t: 1 if the barycentric tests pass, t written. */
+static int mt_core(const rt_ray *ray, const rt_triangle *tri, float *t_out)
+{
+    rt_vec3 p = cross_vec(ray->d, tri->e2);
+    float det = dot3(p, tri->e1);
+    if (rt_fabsf(det) < RT_SMALL_F) return 0;
+    det = 1.0f / det;
+    rt_vec3 to = {ray->o.x - tri->v0.x, ray->o.y - tri->v0.y, ray->o.z - tri->v0.z};
+    rt_vec3 q = cross_vec(to, tri->e1);
+    float e0 = dot3(p, to) * det;
+    if (e0 < 0 || e0 > 1) return 0;
+    float e1 = dot3(q, ray->d) * det;
+    if (e1 < 0 || e1 + e0 > 1) return 0;
+    *t_out = dot3(q, tri->e2) * det;
+    return 1;
+}
+
+typedef struct bvh_item {
+    double lo[3], hi[3], c[3];
+    double a, l;
+} bvh_item;
+
+typedef struct bvh_build {
+    bvh_item *items;
+    uint32_t *perm;
+    or_bnode *nodes;
+    uint32_t n_nodes, cap, depth;
+} bvh_build;
+
+static void box_of(const bvh_item *it, const uint32_t *perm, uint32_t n, or_bnode *nd)
+{
+    for (int k = 0; k < 3; ++k) {
+        nd->lo[k] = INFINITY;
+        nd->hi[k] = -INFINITY;
+    }
+    nd->amax = nd->lmax = 0.0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const bvh_item *t = &it[perm[i]];
+        for (int k = 0; k < 3; ++k) {
+            if (t->lo[k] < nd->lo[k]) nd->lo[k] = t->lo[k];
+            if (t->hi[k] > nd->hi[k]) nd->hi[k] = t->hi[k];
+        }
+        if (t->a > nd->amax) nd->amax = t->a;
+        if (t->l > nd->lmax) nd->lmax = t->l;
+    }
+}
+
+static double half_area(const double *lo, const double *hi)
+{
+    const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+    return (x < 0 || y < 0 || z < 0) ? 0.0 : x * y + y * z + z * x;
+}
+
+#define OR_BVH_BINS 16
+#define OR_BVH_LEAF 4
+
+/* Builds the subtree over perm[0, n) into node `ni`; binned SAH on the widest centroid axis,
+   a median split when SAH finds nothing better than a leaf of > OR_BVH_LEAF triangles. */
+static int build_node(bvh_build *B, uint32_t ni, uint32_t first, uint32_t n, uint32_t depth)
+{
+    if (depth > B->depth) B->depth = depth;
+    or_bnode *nd = &B->nodes[ni];
+    box_of(B->items, B->perm + first, n, nd);
+    if (n <= OR_BVH_LEAF || depth >= 60) {
+        nd->a = -1 - (int32_t)first;
+        nd->b = (int32_t)n;
+        return 0;
+    }
+    double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < n; ++i) {
+        const double *c = B->items[B->perm[first + i]].c;
+        for (int k = 0; k < 3; ++k) {
+            if (c[k] < clo[k]) clo[k] = c[k];
+            if (c[k] > chi[k]) chi[k] = c[k];
+        }
+    }
+    int axis = 0;
+    for (int k = 1; k < 3; ++k)
+        if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+    const double ext = chi[axis] - clo[axis];
+    uint32_t mid = n / 2;
+    if (ext > 0) {
+        uint32_t cnt[OR_BVH_BINS] = {0};
+        double blo[OR_BVH_BINS][3], bhi[OR_BVH_BINS][3];
+        for (int b = 0; b < OR_BVH_BINS; ++b)
+            for (int k = 0; k < 3; ++k) {
+                blo[b][k] = INFINITY;
+                bhi[b][k] = -INFINITY;
+            }
+        const double scale = OR_BVH_BINS / ext;
+        for (uint32_t i = 0; i < n; ++i) {
+            const bvh_item *t = &B->items[B->perm[first + i]];
+            int b = (int)((t->c[axis] - clo[axis]) * scale);
+            if (b >= OR_BVH_BINS) b = OR_BVH_BINS - 1;
+            if (b < 0) b = 0;
+            cnt[b]++;
+            for (int k = 0; k < 3; ++k) {
+                if (t->lo[k] < blo[b][k]) blo[b][k] = t->lo[k];
+                if (t->hi[k] > bhi[b][k]) bhi[b][k] = t->hi[k];
+            }
+        }
+        double right_cost[OR_BVH_BINS];
+        double rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        uint32_t rc = 0;
+        for (int b = OR_BVH_BINS - 1; b > 0; --b) {
+            rc += cnt[b];
+            for (int k = 0; k < 3; ++k) {
+                if (blo[b][k] < rlo[k]) rlo[k] = blo[b][k];
+                if (bhi[b][k] > rhi[k]) rhi[k] = bhi[b][k];
+            }
+            right_cost[b] = rc ? half_area(rlo, rhi) * rc : 0.0;
+        }
+        double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        uint32_t lc = 0;
+        double best = INFINITY;
+        int best_b = -1;
+        for (int b = 0; b < OR_BVH_BINS - 1; ++b) {
+            lc += cnt[b];
+            for (int k = 0; k < 3; ++k) {
+                if (blo[b][k] < llo[k]) llo[k] = blo[b][k];
+                if (bhi[b][k] > lhi[k]) lhi[k] = bhi[b][k];
+            }
+            if (lc == 0 || lc == n) continue;
+            const double cost = half_area(llo, lhi) * lc + right_cost[b + 1];
+            if (cost < best) {
+                best = cost;
+                best_b = b;
+            }
+        }
+        if (best_b >= 0) {
+            uint32_t i = 0, j = n;
+            while (i < j) { /* partition: bin <= best_b first */
+                const bvh_item *t = &B->items[B->perm[first + i]];
+                int b = (int)((t->c[axis] - clo[axis]) * scale);
+                if (b >= OR_BVH_BINS) b = OR_BVH_BINS - 1;
+                if (b <= best_b) {
+                    ++i;
+                } else {
+                    --j;
+                    const uint32_t tmp = B->perm[first + i];
+                    B->perm[first + i] = B->perm[first + j];
+                    B->perm[first + j] = tmp;
+                }
+            }
+            mid = i;
+        }
+    }
+    if (mid == 0 || mid == n) mid = n / 2; /* equal centroids: split the range in half */
+    if (B->n_nodes + 2 > B->cap) return -1;
+    const uint32_t ca = B->n_nodes++, cb = B->n_nodes++;
+    nd->a = (int32_t)ca;
+    nd->b = (int32_t)cb;
+    if (build_node(B, ca, first, mid, depth + 1)) return -1;
+    return build_node(B, cb, first + mid, n - mid, depth + 1);
+}
+
+OR_API or_bvh *or_bvh_build(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris)
+{
+    if (!verts || !idx || !n_tris) return NULL;
+    for (uint64_t i = 0; i < 3ull * n_tris; ++i)
+        if (idx[i] < 0 || (uint32_t)idx[i] >= n_verts) return NULL;
+    bvh_build B;
+    memset(&B, 0, sizeof(B));
+    B.items = (bvh_item *)malloc(sizeof(bvh_item) * n_tris);
+    B.perm = (uint32_t *)malloc(sizeof(uint32_t) * n_tris);
+    B.cap = 2 * n_tris + 1;
+    B.nodes = (or_bnode *)malloc(sizeof(or_bnode) * B.cap);
+    or_bvh *out = (or_bvh *)calloc(1, sizeof(or_bvh));
+    if (!B.items || !B.perm || !B.nodes || !out) goto fail;
+    for (uint32_t i = 0; i < n_tris; ++i) {
+        rt_triangle t;
+        or_get_triangle(&t, i, (const rt_vec3 *)verts, idx);
+        const double p[3][3] = {{t.v0.x, t.v0.y, t.v0.z},
+                                {(double)t.v0.x + t.e1.x, (double)t.v0.y + t.e1.y, (double)t.v0.z + t.e1.z},
+                                {(double)t.v0.x + t.e2.x, (double)t.v0.y + t.e2.y, (double)t.v0.z + t.e2.z}};
+        bvh_item *it = &B.items[i];
+        for (int k = 0; k < 3; ++k) {
+            double lo = p[0][k], hi = p[0][k];
+            for (int v = 1; v < 3; ++v) {
+                if (p[v][k] < lo) lo = p[v][k];
+                if (p[v][k] > hi) hi = p[v][k];
+            }
+            it->lo[k] = lo;
+            it->hi[k] = hi;
+            it->c[k] = 0.5 * (lo + hi);
+        }
+        const double l1 = sqrt((double)t.e1.x * t.e1.x + (double)t.e1.y * t.e1.y + (double)t.e1.z * t.e1.z);
+        const double l2 = sqrt((double)t.e2.x * t.e2.x + (double)t.e2.y * t.e2.y + (double)t.e2.z * t.e2.z);
+        it->a = l1 * l2;
+        it->l = l1 + l2;
+        B.perm[i] = i;
+    }
+    B.n_nodes = 1;
+    if (build_node(&B, 0, 0, n_tris, 0)) goto fail;
+    free(B.items);
+    out->nodes = B.nodes;
+    out->tri = B.perm;
+    out->n_nodes = B.n_nodes;
+    out->n_tris = n_tris;
+    out->depth = B.depth;
+    return out;
+fail:
+    free(B.items);
+    free(B.perm);
+    free(B.nodes);
+    free(out);
+    return NULL;
+}
+
+OR_API void or_bvh_free(or_bvh *b)
+{
+    if (!b) return;
+    free(b->nodes);
+    free(b->tri);
+    free(b);
+}
+
+OR_API uint32_t or_bvh_nodes(const or_bvh *b) { return b ? b->n_nodes : 0u; }
+OR_API uint32_t or_bvh_depth(const or_bvh *b) { return b ? b->depth : 0u; }
+
+/* Per ray, once: the ray in binary64 and its direction's inverse and length. */
+typedef struct bvh_ray {
+    double o[3], d[3], inv[3], dl;
+} bvh_ray;
+
+static void bvh_ray_setup(bvh_ray *r, const rt_ray *ray)
+{
+    r->o[0] = ray->o.x;
+    r->o[1] = ray->o.y;
+    r->o[2] = ray->o.z;
+    r->d[0] = ray->d.x;
+    r->d[1] = ray->d.y;
+    r->d[2] = ray->d.z;
+    for (int k = 0; k < 3; ++k) r->inv[k] = r->d[k] != 0.0 ? 1.0 / r->d[k] : 0.0;
+    r->dl = sqrt(r->d[0] * r->d[0] + r->d[1] * r->d[1] + r->d[2] * r->d[2]);
+}
+
+/* Can a triangle below `nd` be accepted with t in [t_lo, t_hi]?  Conservative (see above):
+   |T| is bounded by the L1 distance of the origin to the box centre plus the box's L1 half
+   diagonal (both at least their Euclidean values); the slab distances are formed with the
+   inverse direction (a few binary64 roundings, absorbed by the 1e-12 relative slack). */
+static int node_may_hold(const or_bnode *nd, const bvh_ray *r, double t_lo, double t_hi)
+{
+    const double u = 5.9604644775390625e-8; /* 2^-24 */
+    const double dl = r->dl;
+    if (!(dl > 0)) return 1;
+    double T = 0.0;
+    for (int k = 0; k < 3; ++k) T += fabs(r->o[k] - 0.5 * (nd->lo[k] + nd->hi[k])) + 0.5 * (nd->hi[k] - nd->lo[k]);
+    const double A = nd->amax, L = nd->lmax;
+    const double det_lo = 0.9999e-4 - 8.0 * u * dl * A;
+    if (det_lo < 0.5e-4) return 1;
+    const double idet = 1.0 / det_lo;
+    const double db = u * (9.0 * L * T * dl + 9.0 * A * dl) * idet + 3.0 * u;
+    const double pad = 16.0 * db * L + 4.0 * u * T;
+    const double tb = (T + pad) / dl;
+    const double dt = 4.0 * (u * (9.0 * T * A + 8.0 * tb * dl * A) * idet + 2.0 * u * tb);
+    double tn = t_lo - dt, tf = t_hi + dt;
+    for (int k = 0; k < 3; ++k) {
+        const double lo = nd->lo[k] - pad, hi = nd->hi[k] + pad;
+        if (r->d[k] == 0.0) {
+            if (r->o[k] < lo || r->o[k] > hi) return 0;
+            continue;
+        }
+        double a = (lo - r->o[k]) * r->inv[k], b = (hi - r->o[k]) * r->inv[k];
+        if (a > b) {
+            const double s = a;
+            a = b;
+            b = s;
+        }
+        a -= 1e-12 * (fabs(a) + 1.0);
+        b += 1e-12 * (fabs(b) + 1.0);
+        if (a > tn) tn = a;
+        if (b < tf) tf = b;
+        if (tn > tf) return 0;
+    }
+    return 1;
+}
+
+/* rtcommon.h:39-52 answered through the BVH: the linear loop's hit (see the accept rule above). */
+static int32_t bvh_closest(rt_ray *ray, const or_mesh *m)
+{
+    const or_bvh *bv = m->bvh;
+    const float tmin = ray->tmin, tmax0 = ray->tmax;
+    float best_t = tmax0;
+    int32_t best = -1;
+    bvh_ray br;
+    bvh_ray_setup(&br, ray);
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const or_bnode *nd = &bv->nodes[stack[--sp]];
+        if (!node_may_hold(nd, &br, tmin, best_t)) continue;
+        if (nd->a < 0) {
+            const uint32_t first = (uint32_t)(-1 - nd->a);
+            for (int32_t j = 0; j < nd->b; ++j) {
+                const uint32_t i = bv->tri[first + (uint32_t)j];
+                rt_triangle tri;
+                float t;
+                or_get_triangle(&tri, i, m->verts, m->idx);
+                if (!mt_core(ray, &tri, &t)) continue;
+                if (!(t >= tmin && t <= tmax0)) continue;
+                if (t < best_t || (t == best_t && (int32_t)i > best)) {
+                    best_t = t;
+                    best = (int32_t)i;
+                }
+            }
+            continue;
+        }
+        if (sp + 2 > 128) abort(); /* depth is capped at 60 */
+        /* nearer child last (popped first): by the distance of the box centres along d */
+        const or_bnode *ca = &bv->nodes[nd->a], *cb = &bv->nodes[nd->b];
+        double pa = 0.0, pb = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            pa += br.d[k] * (ca->lo[k] + ca->hi[k]);
+            pb += br.d[k] * (cb->lo[k] + cb->hi[k]);
+        }
+        if (pa <= pb) {
+            stack[sp++] = (uint32_t)nd->b;
+            stack[sp++] = (uint32_t)nd->a;
+        } else {
+            stack[sp++] = (uint32_t)nd->a;
+            stack[sp++] = (uint32_t)nd->b;
+        }
+    }
+    if (best >= 0) ray->tmax = best_t;
+    return best;
+}
+
+/* rtcommon.h:59-68 answered through the BVH: 1 if no triangle occludes (tmin < t < tmax). */
+static int bvh_visible(const rt_ray *ray, const or_mesh *m)
+{
+    const or_bvh *bv = m->bvh;
+    bvh_ray br;
+    bvh_ray_setup(&br, ray);
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const or_bnode *nd = &bv->nodes[stack[--sp]];
+        if (!node_may_hold(nd, &br, ray->tmin, ray->tmax)) continue;
+        if (nd->a < 0) {
+            const uint32_t first = (uint32_t)(-1 - nd->a);
+            for (int32_t j = 0; j < nd->b; ++j) {
+                rt_triangle tri;
+                or_get_triangle(&tri, bv->tri[first + (uint32_t)j], m->verts, m->idx);
+                if (or_intersects_triangle_p(ray, &tri)) return 0;
+            }
+            continue;
+        }
+        if (sp + 2 > 128) abort();
+        stack[sp++] = (uint32_t)nd->b;
+        stack[sp++] = (uint32_t)nd->a;
+    }
+    return 1;
+}
+
+static int32_t mesh_closest(rt_ray *ray, const or_mesh *m)
+{
+    return m->bvh ? bvh_closest(ray, m) : or_scene_intersection_tri(ray, m->verts, m->idx, m->n_tris);
+}
+
+static int mesh_visible(const rt_ray *ray, const or_mesh *m)
+{
+    return m->bvh ? bvh_visible(ray, m) : or_visibility_test_tri(ray, m->verts, m->idx, m->n_tris);
+}
+
 /* rtcommon.h:78-105 — one sample per emissive sphere, triangles occlude. */
 static rt_vec3 sample_direct_illumination_tri(const rt_hit_info *hit, const or_mesh *m, const rt_sphere *lights,
                                               uint32_t n_lights, rt_seed *seed, or_counters *cnt)
@@ -396,7 +810,7 @@ static rt_vec3 sample_direct_illumination_tri(const rt_hit_info *hit, const or_m
             float r2 = or_frand(seed);
             or_sphere_emissive_radiance(&ray, light->center, light->radius, r1, r2);
             cnt->shadow++;
-            if (or_visibility_test_tri(&ray, m->verts, m->idx, m->n_tris)) {
+            if (mesh_visible(&ray, m)) {
                 float cw = ray.d.x * hit->surface_normal.x + ray.d.y * hit->surface_normal.y +
                            ray.d.z * hit->surface_normal.z;
                 if (cw > 0) {
@@ -592,7 +1006,7 @@ OR_API rt_vec3 or_trace_path_tri(rt_ray ray, const or_mesh *m, const rt_sphere *
     rt_triangle ht;
     for (uint32_t depth = 0; depth <= max_depth; ++depth) {
         cnt->closest++;
-        int32_t ti = or_scene_intersection_tri(&ray, m->verts, m->idx, m->n_tris);
+        int32_t ti = mesh_closest(&ray, m);
         if (ti >= 0) {
             or_get_triangle(&ht, (uint32_t)ti, m->verts, m->idx);
             rt_hit_info hit;
@@ -765,13 +1179,15 @@ static void *worker(void *arg)
 {
     or_job *j = (or_job *)arg;
     const or_frame *f = j->f;
+    or_counters cnt = {0, 0}; /* thread-local: the jobs' counters share cache lines */
     if (f->pixels) {
         for (uint32_t i = (uint32_t)j->tid; i < f->n_pixels; i += (uint32_t)j->nthreads)
-            render_pixel(f, f->pixels[i] % f->W, f->pixels[i] / f->W, &j->cnt);
+            render_pixel(f, f->pixels[i] % f->W, f->pixels[i] / f->W, &cnt);
     } else {
         for (uint32_t y = (uint32_t)j->tid; y < f->H; y += (uint32_t)j->nthreads)
-            for (uint32_t x = 0; x < f->W; ++x) render_pixel(f, x, y, &j->cnt);
+            for (uint32_t x = 0; x < f->W; ++x) render_pixel(f, x, y, &cnt);
     }
+    j->cnt = cnt;
     return NULL;
 }
 
@@ -826,14 +1242,16 @@ OR_API int or_render_spheres(float *out, const rt_camera *cam, const rt_sphere *
 }
 
 /* raytrace_tris over the whole frame, or over a pixel subset with at most
-   max_samples samples per pixel (0 = all). */
-OR_API int or_render_tris(float *out, const rt_camera *cam, const rt_sphere *s, uint32_t n, uint32_t W, uint32_t H,
-                          uint32_t Wpad, uint32_t Hpad, uint32_t sample_rate, uint32_t max_depth,
-                          uint32_t progressive, uint32_t *seeds, const float *verts, const int32_t *idx,
-                          uint32_t n_tris, const uint32_t *pixels, uint32_t n_pixels, uint32_t max_samples,
-                          int nthreads, or_counters *cnt)
+   max_samples samples per pixel (0 = all); bvh: NULL for the reference's linear loops, or a
+   tree from or_bvh_build over the same verts / idx (the same results, O(log N) per ray). */
+OR_API int or_render_tris_bvh(float *out, const rt_camera *cam, const rt_sphere *s, uint32_t n, uint32_t W,
+                              uint32_t H, uint32_t Wpad, uint32_t Hpad, uint32_t sample_rate, uint32_t max_depth,
+                              uint32_t progressive, uint32_t *seeds, const float *verts, const int32_t *idx,
+                              uint32_t n_tris, const uint32_t *pixels, uint32_t n_pixels, uint32_t max_samples,
+                              int nthreads, or_counters *cnt, const or_bvh *bvh)
 {
-    or_mesh m = {(const rt_vec3 *)verts, idx, n_tris};
+    if (bvh && bvh->n_tris != n_tris) return -1;
+    or_mesh m = {(const rt_vec3 *)verts, idx, n_tris, bvh};
     or_frame f;
     memset(&f, 0, sizeof(f));
     f.out = out;
@@ -856,6 +1274,16 @@ OR_API int or_render_tris(float *out, const rt_camera *cam, const rt_sphere *s, 
     return run_frame(&f, nthreads, cnt);
 }
 
+OR_API int or_render_tris(float *out, const rt_camera *cam, const rt_sphere *s, uint32_t n, uint32_t W, uint32_t H,
+                          uint32_t Wpad, uint32_t Hpad, uint32_t sample_rate, uint32_t max_depth,
+                          uint32_t progressive, uint32_t *seeds, const float *verts, const int32_t *idx,
+                          uint32_t n_tris, const uint32_t *pixels, uint32_t n_pixels, uint32_t max_samples,
+                          int nthreads, or_counters *cnt)
+{
+    return or_render_tris_bvh(out, cam, s, n, W, H, Wpad, Hpad, sample_rate, max_depth, progressive, seeds, verts, idx,
+                              n_tris, pixels, n_pixels, max_samples, nthreads, cnt, NULL);
+}
+
 /* Primary-ray closest hits for a batch of rays (hit index + t), linear
    traversal exactly as rtcommon.h:39-52.  Used for the hit-index parity
    tests against the GPU BVH. */
@@ -874,6 +1302,25 @@ OR_API void or_any_hits(const rt_ray *rays, uint32_t n_rays, const float *verts,
 {
     for (uint32_t i = 0; i < n_rays; ++i)
         out_occluded[i] = !or_visibility_test_tri(&rays[i], (const rt_vec3 *)verts, idx, n_tris);
+}
+
+/* The same two queries through the independent BVH mode (or_bvh_build over verts / idx). */
+OR_API void or_closest_hits_bvh(const rt_ray *rays, uint32_t n_rays, const float *verts, const int32_t *idx,
+                                const or_bvh *bvh, int32_t *out_idx, float *out_t)
+{
+    or_mesh m = {(const rt_vec3 *)verts, idx, bvh->n_tris, bvh};
+    for (uint32_t i = 0; i < n_rays; ++i) {
+        rt_ray r = rays[i];
+        out_idx[i] = bvh_closest(&r, &m);
+        out_t[i] = r.tmax;
+    }
+}
+
+OR_API void or_any_hits_bvh(const rt_ray *rays, uint32_t n_rays, const float *verts, const int32_t *idx,
+                            const or_bvh *bvh, int32_t *out_occluded)
+{
+    or_mesh m = {(const rt_vec3 *)verts, idx, bvh->n_tris, bvh};
+    for (uint32_t i = 0; i < n_rays; ++i) out_occluded[i] = !bvh_visible(&rays[i], &m);
 }
 
 /* Host camera helper restated for the KAT (RayTracer.cpp:33-47 and

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "pathtracer_rt.h"
+#include "rt_internal.h"
 
 #define RT_COMM_MAX_RANKS 64
 
@@ -134,17 +135,17 @@ uint32_t tile_rows(uint32_t H, uint32_t stripe, uint32_t n, uint32_t r)
 extern "C" {
 
 int rt_comm_get_unique_id(uint8_t id[RT_COMM_ID_BYTES])
-{
+try {
     static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RT_COMM_ID_BYTES != NCCL_UNIQUE_ID_BYTES");
     if (!id) return RT_ERR_ARG;
     ncclUniqueId u;
     if (ncclGetUniqueId(&u) != ncclSuccess) return RT_ERR_HIP;
     std::memcpy(id, &u, sizeof(u));
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 int rt_comm_create(const uint8_t id[RT_COMM_ID_BYTES], int n_ranks, int rank, int device, rt_comm **out)
-{
+try {
     if (!out) return RT_ERR_ARG;
     *out = nullptr;
     if (!id || n_ranks < 1 || n_ranks > RT_COMM_MAX_RANKS || rank < 0 || rank >= n_ranks) return RT_ERR_ARG;
@@ -165,10 +166,10 @@ int rt_comm_create(const uint8_t id[RT_COMM_ID_BYTES], int n_ranks, int rank, in
     }
     *out = m;
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 int rt_comm_destroy(rt_comm *m)
-{
+try {
     if (!m) return RT_ERR_ARG;
     (void)hipSetDevice(m->device);
     if (m->stream) (void)hipStreamSynchronize(m->stream);
@@ -178,19 +179,19 @@ int rt_comm_destroy(rt_comm *m)
     if (m->stream) (void)hipStreamDestroy(m->stream);
     delete m;
     return RT_OK;
-}
+} RT_CATCH(m ? &const_cast<rt_comm *>(m)->err : nullptr)
 
 const char *rt_comm_last_error(const rt_comm *m) { return m ? m->err.c_str() : "null communicator"; }
 
 int rt_comm_count(const rt_comm *m, int *n)
-{
+try {
     if (!m || !n) return RT_ERR_ARG;
     return ncclCommCount(m->nccl, n) == ncclSuccess ? RT_OK : RT_ERR_HIP;
-}
+} RT_CATCH(m ? &const_cast<rt_comm *>(m)->err : nullptr)
 
 int rt_assemble_tiles(const float *const *tiles, uint32_t n, uint32_t W, uint32_t H, uint32_t stripe, float *frame,
                       int device)
-{
+try {
     if (!tiles || !frame || n < 1 || n > RT_COMM_MAX_RANKS || stripe == 0) return RT_ERR_ARG;
     for (uint32_t r = 0; r < n; ++r)
         if (!tiles[r] && tile_rows(H, stripe, n, r) > 0) return RT_ERR_ARG;
@@ -199,11 +200,11 @@ int rt_assemble_tiles(const float *const *tiles, uint32_t n, uint32_t W, uint32_
     rt_comm tmp;
     if (assemble(&tmp, tiles, n, W, H, stripe, frame, nullptr) != RT_OK) return RT_ERR_HIP;
     return hipStreamSynchronize(nullptr) == hipSuccess ? RT_OK : RT_ERR_HIP;
-}
+} RT_CATCH(nullptr)
 
 int rt_comm_gather_frame(rt_comm *m, const float *tile, float *frame, uint32_t W, uint32_t H, uint32_t stripe,
                          int root)
-{
+try {
     if (!m) return RT_ERR_ARG;
     const uint32_t n = (uint32_t)m->n_ranks, me = (uint32_t)m->rank;
     if (stripe == 0 || root < 0 || root >= m->n_ranks) return fail(m, RT_ERR_ARG, "bad stripe or root");
@@ -238,11 +239,11 @@ int rt_comm_gather_frame(rt_comm *m, const float *tile, float *frame, uint32_t W
     }
     HIPC(m, hipStreamSynchronize(m->stream));
     return RT_OK;
-}
+} RT_CATCH(m ? &const_cast<rt_comm *>(m)->err : nullptr)
 
 int rt_seed_halo_plan(int32_t *writer, uint32_t H, uint32_t hpad, uint32_t stripe, uint32_t n, uint32_t shift,
                       uint32_t *src, uint32_t *dst, uint32_t *rows, uint32_t *n_moves)
-{
+try {
     if (!writer || !n_moves || stripe == 0 || n == 0 || hpad < H) return RT_ERR_ARG;
     /* moves grouped by (src, dst) pair in pair order, rows in pixel-row order within a
        pair (the order dist.SeedHalo.plan produces) */
@@ -265,12 +266,12 @@ int rt_seed_halo_plan(int32_t *writer, uint32_t H, uint32_t hpad, uint32_t strip
     *n_moves = k;
     for (uint32_t y = 0; y < H; ++y) writer[((uint64_t)y + shift) % hpad] = (int32_t)row_rank(y, stripe, n);
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 int rt_seed_halo_peer_blocks(const uint32_t *src, const uint32_t *dst, const uint32_t *rows, uint32_t k, uint32_t n,
                              uint32_t me, uint32_t *send_rows, uint32_t *send_counts, uint32_t *recv_rows,
                              uint32_t *recv_counts)
-{
+try {
     if (n == 0 || me >= n || !send_counts || !recv_counts || (k && (!src || !dst || !rows || !send_rows || !recv_rows)))
         return RT_ERR_ARG;
     std::vector<std::vector<uint32_t>> to(n), from(n);
@@ -287,19 +288,19 @@ int rt_seed_halo_peer_blocks(const uint32_t *src, const uint32_t *dst, const uin
         for (uint32_t r : from[p]) recv_rows[ro++] = r;
     }
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 int rt_comm_reset_halo(rt_comm *m)
-{
+try {
     if (!m) return RT_ERR_ARG;
     m->writer.clear();
     m->key_ctx = nullptr;
     return RT_OK;
-}
+} RT_CATCH(m ? &const_cast<rt_comm *>(m)->err : nullptr)
 
 int rt_comm_render(rt_comm *m, rt_ctx *c, float *frame, uint32_t W, uint32_t H, uint32_t prog, int kernel,
                    uint32_t stripe, int root)
-{
+try {
     if (!m || !c) return RT_ERR_ARG;
     if (stripe == 0 || root < 0 || root >= m->n_ranks) return fail(m, RT_ERR_ARG, "bad stripe or root");
     if (W == 0 || H == 0) return RT_OK;
@@ -383,6 +384,6 @@ int rt_comm_render(rt_comm *m, rt_ctx *c, float *frame, uint32_t W, uint32_t H, 
        kernels row y */
     for (uint32_t y = 0; y < H; ++y) m->writer[((uint64_t)y + shift) % m->hpad] = (int32_t)row_rank(y, stripe, n);
     return rt_comm_gather_frame(m, m->tile, frame, W, H, stripe, root);
-}
+} RT_CATCH(m ? &const_cast<rt_comm *>(m)->err : nullptr)
 
 } /* extern "C" */

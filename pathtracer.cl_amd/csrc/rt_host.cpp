@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -169,6 +170,7 @@ struct rt_ctx {
     size_t long_seed_bytes = 0;
     uint32_t *d_repair_seed = nullptr; /* the repaired pixels' seeds by slot (the first RT_REPAIR_SLOTS of them) */
     size_t repair_seed_bytes = 0;
+    uint32_t repair_slots = RT_REPAIR_SLOTS; /* RT_REPAIR_SLOTS (env, test knob): repaired pixels with per-sample seeds */
     size_t split_box_cap = 0;
     uint32_t n_split_box = 0;
     int split_box_grid = 0;           /* the box pixels' seed-pass grid of the render being launched */
@@ -533,7 +535,12 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
             c->h_spec_mul[2 * ch] = powmod(36969u, k, 36969ull * 65536u - 1u);
             c->h_spec_mul[2 * ch + 1] = powmod(18000u, k, 18000ull * 65536u - 1u);
         }
-        HIPCHK(c, hipMemcpy(c->d_spec_mul, c->h_spec_mul.data(), 2 * 64 * sizeof(uint32_t), hipMemcpyHostToDevice));
+        /* on the render stream, after the previous frame's chunk tasks and repair pass (which read
+           the multipliers: split_render ends with the render stream waiting on the other two); the
+           wait keeps the host copy alive until the upload is done (a rare event: the key changes
+           with the chunking or the light count) */
+        HIPCHK(c, hipMemcpyAsync(c->d_spec_mul, c->h_spec_mul.data(), 2 * 64 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipStreamSynchronize(st));
         c->spec_mul_key = key;
     }
     if (c->split_dirty_px < npx) {
@@ -586,7 +593,6 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
             const size_t bytes = (size_t)n_box * b.split_nseed * 8u;
             if (c->long_seed_bytes < bytes) {
                 free_dev(c->d_long_seed);
-    free_dev(c->d_repair_seed);
                 c->d_long_seed = nullptr;
                 c->long_seed_bytes = 0;
                 HIPCHK(c, hipMalloc(&c->d_long_seed, bytes));
@@ -648,8 +654,8 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
             s.split_chunk = RT_LONG_FINE;
             s.split_chunks = (spp + RT_LONG_FINE - 1u) / RT_LONG_FINE;
             s.split_nseed = s.split_chunks + 1u;
-            s.split_item_cap = RT_REPAIR_SLOTS;
-            const size_t bytes = (size_t)RT_REPAIR_SLOTS * s.split_nseed * 8u;
+            s.split_item_cap = c->repair_slots;
+            const size_t bytes = (size_t)c->repair_slots * s.split_nseed * 8u;
             if (c->repair_seed_bytes < bytes) {
                 free_dev(c->d_repair_seed);
                 c->d_repair_seed = nullptr;
@@ -663,7 +669,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
             if (!e) e = rt_launch_tris(s, RT_TRAV_BVH4Q, c->counting, 128, st);
             if (!e) e = rt_launch_split_finish(s, st);
             if (e) return hip_fail(c, (hipError_t)e, "repair launches");
-            r.split_item_base = RT_REPAIR_SLOTS; /* the rest, if any */
+            r.split_item_base = c->repair_slots; /* the rest, if any */
         }
         e = rt_launch_split_seeds(r, st);
         if (!e) e = rt_launch_tris(r, RT_TRAV_BVH4Q, c->counting, 64, st);
@@ -773,6 +779,32 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
 
 } // namespace
 
+int rt_exception_status(std::string *err) noexcept
+{
+    int code = RT_ERR_STATE;
+    const char *what = "unknown exception";
+    try {
+        throw;
+    } catch (const std::bad_alloc &e) {
+        code = RT_ERR_ALLOC;
+        what = e.what();
+    } catch (const std::length_error &e) {
+        code = RT_ERR_ALLOC;
+        what = e.what();
+    } catch (const std::exception &e) {
+        code = RT_ERR_ARG;
+        what = e.what();
+    } catch (...) {
+    }
+    if (err) {
+        try {
+            *err = std::string("host exception: ") + what;
+        } catch (...) {
+        }
+    }
+    return code;
+}
+
 extern "C" {
 
 const char *rt_status_string(int s)
@@ -791,7 +823,7 @@ const char *rt_status_string(int s)
 }
 
 int rt_create(int device, rt_ctx **out)
-{
+try {
     if (!out) return RT_ERR_ARG;
     *out = nullptr;
     int n = 0;
@@ -810,8 +842,13 @@ int rt_create(int device, rt_ctx **out)
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
-    if (const char *v = getenv("RT_SEED_WIDTH")) c->seed_width = (uint32_t)std::max(1, atoi(v)); /* A/B knob */
+    if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
+        const int w = atoi(v);
+        if (w == 0 || w == 1 || w == 3 || (w >= 8 && w <= 64 && (w & (w - 1)) == 0)) c->seed_width = (uint32_t)w;
+        else fprintf(stderr, "[rtmi] RT_SEED_WIDTH=%s ignored (0, 1, 3 or a power of two from 8 to 64)\n", v);
+    }
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
+    c->repair_slots = std::max(1u, env_u32("RT_REPAIR_SLOTS", RT_REPAIR_SLOTS)); /* test knob: the path beyond them */
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -821,13 +858,14 @@ int rt_create(int device, rt_ctx **out)
         rt_destroy(c);
         return RT_ERR_HIP;
     }
+    memset(c->h_counters, 0, kCounterBytes + sizeof(unsigned long long)); /* no stale guard before any render */
     c->d_work = reinterpret_cast<uint32_t *>(c->d_counters + RT_COUNTER_WORDS);
     *out = c;
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 int rt_destroy(rt_ctx *c)
-{
+try {
     if (!c) return RT_ERR_ARG;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -841,6 +879,7 @@ int rt_destroy(rt_ctx *c)
     free_dev(c->d_class);
     free_dev(c->d_split_seed);
     free_dev(c->d_long_seed);
+    free_dev(c->d_repair_seed);
     free_dev(c->d_split_col);
     free_dev(c->d_split_counter);
     free_dev(c->d_split_dirty);
@@ -870,12 +909,12 @@ int rt_destroy(rt_ctx *c)
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 const char *rt_last_error(const rt_ctx *c) { return c ? c->err.c_str() : "null context"; }
 
 int rt_set_spheres(rt_ctx *c, const rt_sphere *s, uint32_t n)
-{
+try {
     if (!c || (n && !s)) return RT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     c->spheres.assign(s, s + n);
@@ -895,10 +934,10 @@ int rt_set_spheres(rt_ctx *c, const rt_sphere *s, uint32_t n)
                             hipMemcpyHostToDevice));
     }
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris)
-{
+try {
     if (!c || !verts || !idx || !n_verts || !n_tris) return fail(c, RT_ERR_ARG, "empty mesh");
     HIPCHK(c, hipSetDevice(c->device));
     std::string err;
@@ -964,10 +1003,10 @@ int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *
     c->bvh.build_seconds = b.build_seconds;
     c->bvh.n_hit = b.n_hit;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_mesh_info(const rt_ctx *c, rt_mesh_stats *out)
-{
+try {
     if (!c || !out) return RT_ERR_ARG;
     if (!c->n_tris) return RT_ERR_NO_MESH;
     out->n_tris = c->n_tris;
@@ -980,131 +1019,131 @@ int rt_mesh_info(const rt_ctx *c, rt_mesh_stats *out)
     out->build_seconds = c->bvh.build_seconds;
     out->n_tris_tree = c->bvh.n_hit;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_view_matrix(rt_ctx *c, const float m[16])
-{
+try {
     if (!c || !m) return RT_ERR_ARG;
     for (int col = 0; col < 4; ++col)
         for (int row = 0; row < 4; ++row) c->view[row][col] = m[col * 4 + row];
     c->cam_override = false;
     c->cam_dirty = true;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_camera_spherical(rt_ctx *c, float tx, float ty, float tz, float el, float az, float dist)
-{
+try {
     if (!c) return RT_ERR_ARG;
     spherical_view(tx, ty, tz, el, az, dist, c->view);
     c->cam_override = false;
     c->cam_dirty = true;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_fov(rt_ctx *c, float fov)
-{
+try {
     if (!c) return RT_ERR_ARG;
     c->fov = fov;
     c->cam_override = false;
     c->cam_dirty = true;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_camera(rt_ctx *c, const rt_camera *cam)
-{
+try {
     if (!c || !cam) return RT_ERR_ARG;
     c->cam_explicit = *cam;
     c->cam_override = true;
     c->cam_dirty = true;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_camera_spherical(float tx, float ty, float tz, float el, float az, float dist, float fov, uint32_t width,
                         rt_camera *out)
-{
+try {
     if (!out) return RT_ERR_ARG;
     float m[4][4];
     spherical_view(tx, ty, tz, el, az, dist, m);
     camera_from_view(m, fov, width, out);
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 int rt_set_params(rt_ctx *c, uint32_t sample_rate, uint32_t max_depth)
-{
+try {
     if (!c) return RT_ERR_ARG;
     if (sample_rate > 4096) return fail(c, RT_ERR_ARG, "sample rate too large");
     c->sample_rate = sample_rate;
     c->max_depth = max_depth;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_builder(rt_ctx *c, int builder)
-{
+try {
     if (!c || (builder != RT_BUILD_HOST && builder != RT_BUILD_GPU)) return RT_ERR_ARG;
     c->builder = builder;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_traversal(rt_ctx *c, int t)
-{
+try {
     if (!c || !(t == RT_TRAVERSAL_BVH || t == RT_TRAVERSAL_LINEAR || t == RT_TRAVERSAL_BVH4F)) return RT_ERR_ARG;
     c->traversal = t;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_ndrange(rt_ctx *c, uint32_t nd_y)
-{
+try {
     if (!c || nd_y == 0 || nd_y > 1024) return RT_ERR_ARG;
     c->nd_y = nd_y;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_seed_layout(rt_ctx *c, uint32_t wpad, uint32_t hpad)
-{
+try {
     if (!c || !wpad || !hpad) return RT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     const int r = ensure_seeds(c, wpad, hpad, nullptr);
     if (r == RT_OK) c->user_seeds = true;
     return r;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_seeds(rt_ctx *c, const uint32_t *seeds, size_t count)
-{
+try {
     if (!c || !seeds) return RT_ERR_ARG;
     if (!c->wpad || count != 2ull * c->wpad * c->hpad) return fail(c, RT_ERR_STATE, "seed count != 2*Wpad*Hpad");
     HIPCHK(c, hipSetDevice(c->device));
     const int r = ensure_seeds(c, c->wpad, c->hpad, seeds);
     if (r == RT_OK) c->user_seeds = true;
     return r;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_get_seeds(const rt_ctx *c, uint32_t *out, size_t count)
-{
+try {
     if (!c || !out) return RT_ERR_ARG;
     if (!c->wpad || count != 2ull * c->wpad * c->hpad) return RT_ERR_STATE;
     if (hipSetDevice(c->device) != hipSuccess) return RT_ERR_HIP;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return RT_ERR_HIP;
     if (hipMemcpy(out, c->d_seeds, count * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_seed_layout(const rt_ctx *c, uint32_t *wpad, uint32_t *hpad)
-{
+try {
     if (!c) return RT_ERR_ARG;
     if (wpad) *wpad = c->wpad;
     if (hpad) *hpad = c->hpad;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_glibc_rand_fill(uint32_t seed, uint32_t *out, size_t count, uint32_t skip)
-{
+try {
     if (!out && count) return RT_ERR_ARG;
     GlibcRand g;
     g.seed(seed);
     for (uint32_t i = 0; i < skip; ++i) (void)g.next();
     for (size_t i = 0; i < count; ++i) out[i] = g.next();
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 uint32_t rt_tile_rows(uint32_t height, const rt_tile *t)
 {
@@ -1121,7 +1160,7 @@ uint32_t rt_tile_rows(uint32_t height, const rt_tile *t)
 
 int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int kernel, const rt_tile *tile,
                     int flags, void *stream)
-{
+try {
     if (!c) return RT_ERR_ARG;
     if (W == 0 || H == 0) return RT_OK; /* RayTracerCL.cpp:219-220 */
     if (!out) return fail(c, RT_ERR_ARG, "null output buffer");
@@ -1161,7 +1200,16 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
     if (c->wpad < W || c->hpad < H) return fail(c, RT_ERR_STATE, "seed layout smaller than the frame");
 
     const uint32_t hl = rt_tile_rows(H, tile);
-    if (hl == 0) return RT_OK;
+    if (hl == 0) { /* a rank with no rows: nothing rendered, and nothing of an earlier render reported */
+        if (c->sync_stream) HIPCHK(c, hipStreamSynchronize(c->sync_stream)); /* its counter copy has landed */
+        memset(c->h_counters, 0, kCounterBytes + sizeof(unsigned long long));
+        c->info = rt_render_info{};
+        c->info.kernel = (uint32_t)kernel;
+        c->info_list_pending = false;
+        c->last_long = 0;
+        c->sync_stream = nullptr;
+        return RT_OK;
+    }
     const size_t out_bytes = (size_t)W * hl * 4 * sizeof(float);
     float *dout = out;
     if (!(flags & RT_OUT_DEVICE)) {
@@ -1502,10 +1550,10 @@ int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog
     c->last_bytes = out_bytes;
     if (!(flags & RT_OUT_DEVICE)) HIPCHK(c, hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, st));
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_synchronize(rt_ctx *c)
-{
+try {
     if (!c) return RT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1542,15 +1590,15 @@ int rt_synchronize(rt_ctx *c)
         return fail(c, RT_ERR_STATE, msg);
     }
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_render(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int kernel, const rt_tile *tile,
               int flags)
-{
+try {
     const int r = rt_render_async(c, out, W, H, prog, kernel, tile, flags, nullptr);
     if (r != RT_OK) return r;
     return rt_synchronize(c); /* cmdQueue.finish(), RayTracerCL.cpp:292 */
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 static int seed_rows_io(rt_ctx *c, const uint32_t *rows, uint32_t n, uint32_t *buf, int flags, bool unpack)
 {
@@ -1591,17 +1639,17 @@ static int seed_rows_io(rt_ctx *c, const uint32_t *rows, uint32_t n, uint32_t *b
 }
 
 int rt_pack_seed_rows(rt_ctx *c, const uint32_t *rows, uint32_t n, uint32_t *buf, int flags)
-{
+try {
     return seed_rows_io(c, rows, n, buf, flags, false);
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_unpack_seed_rows(rt_ctx *c, const uint32_t *rows, uint32_t n, const uint32_t *buf, int flags)
-{
+try {
     return seed_rows_io(c, rows, n, const_cast<uint32_t *>(buf), flags, true);
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_read(rt_ctx *c, float *host, size_t n_floats)
-{
+try {
     if (!c || !host) return RT_ERR_ARG;
     if (!c->last_out) return fail(c, RT_ERR_STATE, "rt_read before any render");
     if (n_floats * sizeof(float) < c->last_bytes) return fail(c, RT_ERR_ARG, "rt_read: host buffer too small");
@@ -1609,10 +1657,10 @@ int rt_read(rt_ctx *c, float *host, size_t n_floats)
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(host, c->last_out, c->last_bytes, hipMemcpyDeviceToHost));
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_last_render_info(rt_ctx *c, rt_render_info *out)
-{
+try {
     if (!c || !out) return RT_ERR_ARG;
     if (c->info_list_pending) { /* how much of the list area the render's lists took */
         HIPCHK(c, hipSetDevice(c->device));
@@ -1630,10 +1678,10 @@ int rt_last_render_info(rt_ctx *c, rt_render_info *out)
     }
     *out = c->info;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_last_long_chains(rt_ctx *c, uint32_t *out, uint32_t cap, uint32_t *n)
-{
+try {
     if (!c || !n || (cap && !out)) return RT_ERR_ARG;
     *n = c->last_long;
     const uint32_t k = std::min(cap, c->last_long);
@@ -1642,41 +1690,41 @@ int rt_last_long_chains(rt_ctx *c, uint32_t *out, uint32_t cap, uint32_t *n)
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipMemcpy(out, c->d_split_box, (size_t)k * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_get_counters(const rt_ctx *c, rt_counters *out)
-{
+try {
     if (!c || !out) return RT_ERR_ARG;
     *out = c->last;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_set_counting(rt_ctx *c, int enable)
-{
+try {
     if (!c) return RT_ERR_ARG;
     c->counting = enable != 0;
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_last_kernel_split_ms(const rt_ctx *c, float *prepass_ms, float *main_ms)
-{
+try {
     if (!c || !prepass_ms || !main_ms) return RT_ERR_ARG;
     if (!c->have_timing) return RT_ERR_STATE;
     if (hipEventSynchronize(c->ev1) != hipSuccess) return RT_ERR_HIP;
     if (hipEventElapsedTime(prepass_ms, c->ev0, c->evm) != hipSuccess) return RT_ERR_HIP;
     return hipEventElapsedTime(main_ms, c->evm, c->ev1) == hipSuccess ? RT_OK : RT_ERR_HIP;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_last_kernel_ms(const rt_ctx *c, float *ms)
-{
+try {
     if (!c || !ms) return RT_ERR_ARG;
     if (!c->have_timing) return RT_ERR_STATE;
     if (hipEventSynchronize(c->ev1) != hipSuccess) return RT_ERR_HIP;
     return hipEventElapsedTime(ms, c->ev0, c->ev1) == hipSuccess ? RT_OK : RT_ERR_HIP;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_t *out_idx, float *out_t)
-{
+try {
     if (!c || !rays || !out_idx) return RT_ERR_ARG;
     if (!c->n_tris) return fail(c, RT_ERR_NO_MESH, "no mesh set");
     if (n == 0) return RT_OK;
@@ -1741,7 +1789,7 @@ int rt_trace_rays(rt_ctx *c, const rt_ray *rays, uint32_t n, int any_hit, int32_
     cleanup();
     if (e != hipSuccess) return hip_fail(c, e, "rt_trace_rays");
     return RT_OK;
-}
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
 /* ---- synthetic meshes ---------------------------------------------------- */
 
@@ -1761,7 +1809,7 @@ uint32_t rt_mesh_vertex_count(uint32_t n_tris)
 }
 
 int rt_make_mesh(uint32_t n_tris, float cx, float cy, float cz, float r, float *verts, int32_t *idx)
-{
+try {
     if (!n_tris || !verts || !idx) return RT_ERR_ARG;
     uint32_t nt, np;
     mesh_grid(n_tris, &nt, &np);
@@ -1802,6 +1850,6 @@ int rt_make_mesh(uint32_t n_tris, float cx, float cy, float cz, float r, float *
         }
     for (uint32_t j = 0; j < np; ++j) tri(ring(nt - 1, j), (int32_t)bottom, ring(nt - 1, j + 1));
     return k == n_tris ? RT_OK : RT_ERR_STATE;
-}
+} RT_CATCH(nullptr)
 
 } /* extern "C" */

@@ -13,6 +13,15 @@
 
 #include "rt_types.h"
 
+/* No C++ exception crosses the C ABI (the reference lets cl::Error escape,
+   RayTracerCL.cpp:102-107): every extern "C" entry that can allocate or parse is a
+   function-try-block ending in RT_CATCH(err), which maps the exception in flight to a status —
+   std::bad_alloc / std::length_error to RT_ERR_ALLOC, any other std::exception to RT_ERR_ARG,
+   anything else to RT_ERR_STATE — and stores its message in *err (may be NULL). */
+int rt_exception_status(std::string *err) noexcept;
+#define RT_CATCH(err_ptr)                                                                                              \
+    catch (...) { return rt_exception_status(err_ptr); }
+
 /* Traversal stack entries per lane kept in LDS (20 x 256 lanes x 4 B = 20 KB per block, which
    with k_tris's other per-lane LDS — pixel sum and throughput, list word, hit normal: 31,232 B
    per block in all — keeps 5 blocks per CU; one block more of LDS measured 3.5 % slower:

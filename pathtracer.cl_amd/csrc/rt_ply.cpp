@@ -19,6 +19,7 @@
  */
 #include <algorithm>
 #include <cerrno>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -29,6 +30,7 @@
 #include <vector>
 
 #include "pathtracer_rt.h"
+#include "rt_internal.h"
 
 struct rt_ply {
     std::vector<float> verts;  /* xyz per vertex */
@@ -106,6 +108,8 @@ public:
         if (c != EOF) ++pos_;
         return c;
     }
+    /* bytes of the file consumed so far */
+    uint64_t consumed() const { return base_ + pos_; }
     /* one line without the newline; false at EOF with nothing read */
     bool line(std::string &s)
     {
@@ -135,6 +139,7 @@ public:
 private:
     bool fill()
     {
+        base_ += len_;
         len_ = std::fread(buf_.data(), 1, buf_.size(), f_);
         pos_ = 0;
         return len_ > 0;
@@ -142,6 +147,7 @@ private:
     FILE *f_;
     std::vector<uint8_t> buf_;
     size_t pos_ = 0, len_ = 0;
+    uint64_t base_ = 0;
 };
 
 bool read_binary(Reader &r, Type t, bool big, double &v)
@@ -179,6 +185,26 @@ bool read_value(Reader &r, Format fmt, Type t, double &v, std::string &tok)
 
 std::string g_err;
 
+/* The fewest bytes one stored value of type t can take: its size in a binary body; in an ascii
+   body one character (the separator may be the end of the file) */
+uint64_t min_value_bytes(Format fmt, Type t) { return fmt == F_ASCII ? 1u : (uint64_t)type_size(t); }
+
+/* The fewest bytes one instance of element e can take (a list counts its count only) */
+uint64_t min_element_bytes(Format fmt, const Element &e)
+{
+    uint64_t b = 0;
+    for (const Property &p : e.props) b += min_value_bytes(fmt, p.count_type != T_NONE ? p.count_type : p.type);
+    return b;
+}
+
+/* The body is checked against the header before anything is sized from it: an element count
+   (or a list length) the rest of the file cannot hold is a malformed file, reported as such
+   instead of a multi-gigabyte allocation (a header saying `element face 4000000000000000000`
+   used to end in std::length_error). */
+struct Malformed {
+    const char *what;
+};
+
 } // namespace
 
 extern "C" {
@@ -186,7 +212,7 @@ extern "C" {
 const char *rt_ply_last_error(void) { return g_err.c_str(); }
 
 int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_tris)
-{
+try {
     g_err.clear();
     if (!path || !out) return RT_ERR_ARG;
     *out = nullptr;
@@ -271,6 +297,36 @@ int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_t
         g_err = "missing format line";
         return RT_ERR_ARG;
     }
+    uint64_t file_bytes = 0;
+    {
+        const long here = std::ftell(f);
+        if (here < 0 || std::fseek(f, 0, SEEK_END) != 0) {
+            g_err = "cannot size the file";
+            return RT_ERR_ARG;
+        }
+        const long end = std::ftell(f);
+        if (end < 0 || std::fseek(f, here, SEEK_SET) != 0) {
+            g_err = "cannot size the file";
+            return RT_ERR_ARG;
+        }
+        file_bytes = (uint64_t)end;
+    }
+    {
+        uint64_t left = file_bytes > r.consumed() ? file_bytes - r.consumed() : 0;
+        for (const Element &e : elems) {
+            const uint64_t per = min_element_bytes(fmt, e);
+            if (per && e.count > left / per) {
+                g_err = "element " + e.name + " declares " + std::to_string(e.count) + " instances of at least " +
+                        std::to_string(per) + " bytes, but the body has " + std::to_string(left) + " bytes left";
+                return RT_ERR_ARG;
+            }
+            if (!per && e.count) { /* no properties: nothing to read, and nothing bounds the count */
+                g_err = "element " + e.name + " has instances but no properties";
+                return RT_ERR_ARG;
+            }
+            left -= per * e.count;
+        }
+    }
     std::unique_ptr<rt_ply> ply(new (std::nothrow) rt_ply);
     if (!ply) return RT_ERR_ALLOC;
     uint64_t nv_total = 0;
@@ -308,7 +364,7 @@ int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_t
                 g_err = "face element without vertex_indices";
                 return RT_ERR_ARG;
             }
-            if (is_face) ply->tris.reserve(3 * e.count);
+            if (is_face) ply->tris.reserve((size_t)std::min<uint64_t>(3 * e.count, 1ull << 26)); /* fans may add more */
             std::vector<int64_t> face;
             for (uint64_t j = 0; j < e.count; ++j) {
                 for (size_t i = 0; i < e.props.size(); ++i) {
@@ -316,17 +372,26 @@ int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_t
                     double v = 0;
                     if (p.count_type != T_NONE) {
                         double cnt = 0;
-                        if (!read_value(r, fmt, p.count_type, cnt, tok) || cnt < 0) throw 1;
-                        const uint64_t n = (uint64_t)cnt;
+                        if (!read_value(r, fmt, p.count_type, cnt, tok)) throw 1;
+                        if (!(cnt >= 0)) throw Malformed{"negative list length"};
+                        const uint64_t n = (uint64_t)cnt; /* an integer type's value: exact, below 2^32 */
+                        const uint64_t item = min_value_bytes(fmt, p.type);
+                        const uint64_t left = file_bytes > r.consumed() ? file_bytes - r.consumed() : 0;
+                        if (item && n > left / item) throw Malformed{"truncated (a list runs past the end of the file)"};
                         const bool keep = is_face && (int)i == ilist;
                         if (keep) face.clear();
                         for (uint64_t q = 0; q < n; ++q) {
                             if (!read_value(r, fmt, p.type, v, tok)) throw 1;
-                            if (keep) face.push_back((int64_t)v);
+                            if (keep) {
+                                if (!(v >= 0.0 && v < 2147483647.0)) throw Malformed{"face index out of range"};
+                                face.push_back((int64_t)v);
+                            }
                         }
                         continue;
                     }
                     if (!read_value(r, fmt, p.type, v, tok)) throw 1;
+                    if (is_vertex && ((int)i == ix || (int)i == iy || (int)i == iz) && !(std::fabs(v) <= (double)FLT_MAX))
+                        throw Malformed{"vertex coordinate not a finite float"};
                     if (is_vertex) {
                         if ((int)i == ix) ply->verts[3 * j + 0] = (float)v;
                         else if ((int)i == iy) ply->verts[3 * j + 1] = (float)v;
@@ -343,16 +408,14 @@ int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_t
                         ply->tris.push_back((int32_t)face[q]);
                         ply->tris.push_back((int32_t)face[q + 1]);
                     }
-                    for (int64_t vi : face)
-                        if (vi < 0 || vi >= (int64_t)0x7FFFFFFF) {
-                            g_err = "face index out of range";
-                            return RT_ERR_ARG;
-                        }
                 }
             }
         }
     } catch (int) {
         g_err = "truncated or malformed PLY body";
+        return RT_ERR_ARG;
+    } catch (const Malformed &m) {
+        g_err = std::string("malformed PLY body: ") + m.what;
         return RT_ERR_ARG;
     } catch (const std::bad_alloc &) {
         g_err = "out of memory";
@@ -375,26 +438,26 @@ int rt_ply_open(const char *path, rt_ply **out, uint32_t *n_verts, uint32_t *n_t
     if (n_tris) *n_tris = (uint32_t)(ply->tris.size() / 3);
     *out = ply.release();
     return RT_OK;
-}
+} RT_CATCH(&g_err)
 
 int rt_ply_read(const rt_ply *ply, float *verts_xyz, int32_t *idx)
-{
-    if (!ply || !verts_xyz || !idx) return RT_ERR_ARG;
-    std::memcpy(verts_xyz, ply->verts.data(), ply->verts.size() * sizeof(float));
-    std::memcpy(idx, ply->tris.data(), ply->tris.size() * sizeof(int32_t));
+try {
+    if (!ply || (!verts_xyz && !ply->verts.empty()) || (!idx && !ply->tris.empty())) return RT_ERR_ARG;
+    if (!ply->verts.empty()) std::memcpy(verts_xyz, ply->verts.data(), ply->verts.size() * sizeof(float));
+    if (!ply->tris.empty()) std::memcpy(idx, ply->tris.data(), ply->tris.size() * sizeof(int32_t));
     return RT_OK;
-}
+} RT_CATCH(&g_err)
 
 uint32_t rt_ply_dropped_faces(const rt_ply *ply) { return ply ? ply->dropped : 0u; }
 
 int rt_ply_close(rt_ply *ply)
-{
+try {
     delete ply;
     return RT_OK;
-}
+} RT_CATCH(&g_err)
 
 int rt_normalize_mesh(float *verts_xyz, uint32_t n_verts, float max_extent, float floor_y)
-{
+try {
     if (!verts_xyz || !n_verts || !(max_extent > 0)) return RT_ERR_ARG;
     double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint32_t i = 0; i < n_verts; ++i)
@@ -414,6 +477,6 @@ int rt_normalize_mesh(float *verts_xyz, uint32_t n_verts, float max_extent, floa
         v[2] = (float)((v[2] - cz) * s);
     }
     return RT_OK;
-}
+} RT_CATCH(nullptr)
 
 } /* extern "C" */

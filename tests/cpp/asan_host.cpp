@@ -1,0 +1,266 @@
+/*
+ * asan_host.cpp — TEST PROGRAM (CPU, no GPU): the host C++ of librtmi and the oracle under
+ * AddressSanitizer + UndefinedBehaviorSanitizer (the reference's latent bugs are
+ * exactly this class — the stack-VLA seed buffer of RayTracerCL.cpp:152-164, uninitialised
+ * members of RayTracerCL.h:64-72).  Built by `make -C tests/cpp asan` from the library's own
+ * sources compiled with -fsanitize=address,undefined on the host side
+ * (pathtracer.cl_amd/csrc `make asan`); run by tests/test_asan.py.
+ *
+ *   asan_host ply FILE...   rt_ply_open on each file: "status<TAB>n_verts<TAB>n_tris<TAB>message"
+ *   asan_host host          camera, glibc rand, tiles, synthetic mesh, both BVH builders' host
+ *                           checks, the seed-halo planner, rt_create without a device, the
+ *                           exception guard of the C ABI
+ *   asan_host oracle        oracle frames (spheres, triangles: linear and BVH mode, equal)
+ * Any sanitizer report aborts with a non-zero status; a failed check prints FAIL and exits 1.
+ */
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pathtracer_rt.h"
+#include "rt_internal.h"
+
+extern "C" {
+struct or_bvh;
+struct or_counters {
+    uint64_t closest, shadow;
+};
+or_bvh *or_bvh_build(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris);
+void or_bvh_free(or_bvh *b);
+int or_render_spheres(float *out, const rt_camera *cam, const rt_sphere *s, uint32_t n, uint32_t W, uint32_t H,
+                      uint32_t Wpad, uint32_t Hpad, uint32_t sample_rate, uint32_t max_depth, uint32_t progressive,
+                      uint32_t *seeds, int single_sample, int nthreads, or_counters *cnt);
+int or_render_tris_bvh(float *out, const rt_camera *cam, const rt_sphere *s, uint32_t n, uint32_t W, uint32_t H,
+                       uint32_t Wpad, uint32_t Hpad, uint32_t sample_rate, uint32_t max_depth, uint32_t progressive,
+                       uint32_t *seeds, const float *verts, const int32_t *idx, uint32_t n_tris,
+                       const uint32_t *pixels, uint32_t n_pixels, uint32_t max_samples, int nthreads,
+                       or_counters *cnt, const or_bvh *bvh);
+}
+
+namespace {
+
+int g_fail = 0;
+
+void check(bool ok, const char *what)
+{
+    if (!ok) {
+        std::printf("FAIL %s\n", what);
+        g_fail = 1;
+    }
+}
+
+int run_ply(int argc, char **argv)
+{
+    for (int i = 0; i < argc; ++i) {
+        rt_ply *p = nullptr;
+        uint32_t nv = 0, nt = 0;
+        const int st = rt_ply_open(argv[i], &p, &nv, &nt);
+        if (st == RT_OK) {
+            std::vector<float> v(3ull * nv);
+            std::vector<int32_t> t(3ull * nt);
+            check(rt_ply_read(p, v.data(), t.data()) == RT_OK, "rt_ply_read");
+            for (int32_t k : t) check(k >= 0 && (uint32_t)k < nv, "index range");
+            rt_ply_close(p);
+        }
+        std::printf("%d\t%u\t%u\t%s\n", st, nv, nt, st == RT_OK ? "" : rt_ply_last_error());
+    }
+    return g_fail;
+}
+
+/* A function-try-block like every C-ABI entry: the exception in flight becomes a status. */
+int throws(int kind, std::string *err)
+try {
+    if (kind == 0) throw std::bad_alloc();
+    if (kind == 1) throw std::length_error("vector::reserve");
+    if (kind == 2) throw std::runtime_error("boom");
+    throw 7;
+} RT_CATCH(err)
+
+int run_host()
+{
+    /* the exception guard */
+    std::string err;
+    check(throws(0, &err) == RT_ERR_ALLOC, "bad_alloc -> RT_ERR_ALLOC");
+    check(throws(1, &err) == RT_ERR_ALLOC && err.find("vector::reserve") != std::string::npos, "length_error");
+    check(throws(2, &err) == RT_ERR_ARG && err.find("boom") != std::string::npos, "std::exception");
+    check(throws(3, nullptr) == RT_ERR_STATE, "unknown exception");
+
+    /* camera (RayTracer.cpp:33-47, RayTracerCL.cpp:178-215) */
+    rt_camera cam;
+    check(rt_camera_spherical(0, -4, 0, 14, 118, 5, 53, 512, &cam) == RT_OK, "camera");
+    check(std::fabs(cam.position.x - 4.283601f) < 1e-5f, "camera position");
+    check(rt_camera_spherical(0, 0, 0, 0, 0, 1, 53, 64, nullptr) == RT_ERR_ARG, "camera null");
+
+    /* glibc rand() stream */
+    std::vector<uint32_t> r(1000);
+    check(rt_glibc_rand_fill(1, r.data(), r.size(), 0) == RT_OK, "rand");
+    srand(1);
+    for (int i = 0; i < 1000; ++i) check(r[i] == (uint32_t)rand(), "rand == libc rand()");
+
+    /* tiles */
+    rt_tile t = {8, 3, 2};
+    uint32_t sum = 0;
+    for (uint32_t k = 0; k < 3; ++k) {
+        t.rank = k;
+        sum += rt_tile_rows(1080, &t);
+    }
+    check(sum == 1080, "tile rows sum");
+    t.rank = 5;
+    check(rt_tile_rows(1080, &t) == 0, "bad tile rank");
+
+    /* synthetic mesh + the host BVH builder (and its input checks) */
+    const uint32_t nt = 20000, nv = rt_mesh_vertex_count(nt);
+    std::vector<float> verts(3ull * nv);
+    std::vector<int32_t> idx(3ull * nt);
+    check(rt_make_mesh(nt, 0, -2.2f, 0, 2.5f, verts.data(), idx.data()) == RT_OK, "make mesh");
+    RtBvh b;
+    check(rt_build_bvh(verts.data(), nv, idx.data(), nt, b, err), "bvh build");
+    check(b.n_nodes4 > 0 && !b.nodes4q.empty() && b.tris.size() >= 12ull * b.n_hit, "bvh shape");
+    std::vector<int32_t> bad = idx;
+    bad[5] = (int32_t)nv;
+    RtBvh b2;
+    check(!rt_build_bvh(verts.data(), nv, bad.data(), nt, b2, err), "index out of range rejected");
+    bad[5] = -1;
+    check(!rt_build_bvh(verts.data(), nv, bad.data(), nt, b2, err), "negative index rejected");
+    std::vector<float> vnan = verts;
+    vnan[7] = NAN;
+    check(!rt_validate_mesh(vnan.data(), nv, idx.data(), nt, err), "NaN vertex rejected");
+    vnan[7] = INFINITY;
+    check(!rt_validate_mesh(vnan.data(), nv, idx.data(), nt, err), "inf vertex rejected");
+    /* a flat, degenerate mesh (every triangle a line): still a valid tree */
+    std::vector<float> flat(9 * 50);
+    std::vector<int32_t> fidx(3 * 50);
+    for (int i = 0; i < 50; ++i) {
+        for (int k = 0; k < 3; ++k) {
+            flat[9 * i + 3 * k + 0] = (float)i;
+            flat[9 * i + 3 * k + 1] = (float)k;
+            flat[9 * i + 3 * k + 2] = 0.0f;
+            fidx[3 * i + k] = 3 * i + k;
+        }
+    }
+    RtBvh b3;
+    check(rt_build_bvh(flat.data(), 150, fidx.data(), 50, b3, err), "degenerate mesh");
+
+    /* the seed-row halo planner (rt_comm.hip host code) over N = 2..8 ranks */
+    for (uint32_t n = 2; n <= 8; ++n) {
+        const uint32_t H = 203, hpad = 208, stripe = 8;
+        std::vector<int32_t> writer(hpad, -1);
+        std::vector<uint32_t> src(hpad), dst(hpad), rows(hpad);
+        for (uint32_t shift = 0; shift < 12; ++shift) {
+            uint32_t k = 0;
+            check(rt_seed_halo_plan(writer.data(), H, hpad, stripe, n, shift, src.data(), dst.data(), rows.data(),
+                                    &k) == RT_OK,
+                  "halo plan");
+            check(k <= hpad, "halo move count");
+            for (uint32_t me = 0; me < n; ++me) {
+                std::vector<uint32_t> sr(k + 1), sc(n), rr(k + 1), rc(n);
+                check(rt_seed_halo_peer_blocks(src.data(), dst.data(), rows.data(), k, n, me, sr.data(), sc.data(),
+                                               rr.data(), rc.data()) == RT_OK,
+                      "peer blocks");
+            }
+        }
+        std::vector<uint32_t> sc(n), rc(n);
+        check(rt_seed_halo_peer_blocks(nullptr, nullptr, nullptr, 0, n, n, nullptr, sc.data(), nullptr, rc.data()) ==
+                  RT_ERR_ARG,
+              "peer blocks: rank out of range");
+    }
+
+    /* no device: rt_create fails with a status, nothing leaks */
+    rt_ctx *c = nullptr;
+    const int st = rt_create(0, &c);
+    check(st != RT_OK ? c == nullptr : c != nullptr, "rt_create status");
+    if (c) rt_destroy(c);
+    check(rt_create(0, nullptr) == RT_ERR_ARG, "rt_create null");
+    check(rt_render(nullptr, nullptr, 1, 1, 0, RT_KERNEL_TRIS, nullptr, 0) == RT_ERR_ARG, "render null ctx");
+    std::printf("host ok\n");
+    return g_fail;
+}
+
+int run_oracle()
+{
+    /* the main.cpp scene: 5 spheres + light (values as scenes.py main_scene) */
+    std::vector<rt_sphere> s(6);
+    std::memset(s.data(), 0, s.size() * sizeof(rt_sphere));
+    const float cen[6][3] = {{-2, -4, -2}, {2, -3, 2}, {0, -4, 0}, {2, -4, -2}, {-2, -4, 2}, {2.2f, 1, 2}};
+    for (int i = 0; i < 6; ++i) {
+        s[i].center = {cen[i][0], cen[i][1], cen[i][2]};
+        s[i].radius = 1.0f;
+        s[i].mat.specExp = 1e6f;
+        s[i].mat.refExp = 1e6f;
+        s[i].mat.ior = 1.0f;
+    }
+    s[0].mat.kd = 1.0f;
+    s[0].mat.diffuse = {0.0f, 0.7f, 0.7f};
+    s[1].mat.ks = 0.2f;
+    s[1].mat.kt = 0.8f;
+    s[1].mat.extinction = {0.99f, 0.95f, 0.95f};
+    s[1].mat.ior = 1.1f;
+    s[2].mat.ks = 1.0f;
+    s[3].mat.kd = 0.2f;
+    s[3].mat.ks = 0.8f;
+    s[3].mat.diffuse = {0.7f, 0.7f, 0.0f};
+    s[3].mat.specExp = 100.0f;
+    s[4].mat.kd = 0.6f;
+    s[4].mat.ks = 0.4f;
+    s[4].mat.diffuse = {0.7f, 0.0f, 0.8f};
+    s[4].mat.specExp = 1000.0f;
+    s[5].radius = 0.5f;
+    s[5].mat.emission_power = 1.0f;
+    s[5].mat.emission = {1.8f, 1.8f, 1.8f};
+    const uint32_t W = 40, H = 30, Wp = 64, Hp = 32;
+    rt_camera cam;
+    rt_camera_spherical(0, -4, 0, 14, 118, 5, 53, W, &cam);
+    std::vector<uint32_t> seeds(2ull * Wp * Hp);
+    rt_glibc_rand_fill(1, seeds.data(), seeds.size(), 0);
+    for (uint32_t &v : seeds) v = v < 2 ? 2 : v;
+    std::vector<float> out(4ull * W * H, 0.0f);
+    or_counters cnt;
+    for (uint32_t p = 0; p < 3; ++p)
+        check(or_render_spheres(out.data(), &cam, s.data(), 6, W, H, Wp, Hp, 2, 6, p, seeds.data(), 0, 3, &cnt) == 0,
+              "oracle spheres");
+    check(cnt.closest > 0, "sphere rays");
+
+    /* triangles: the linear loop and the BVH mode give the same bits */
+    const uint32_t nt = 3000, nv = rt_mesh_vertex_count(nt);
+    std::vector<float> verts(3ull * nv);
+    std::vector<int32_t> idx(3ull * nt);
+    rt_make_mesh(nt, 0, -2.2f, 0, 2.5f, verts.data(), idx.data());
+    or_bvh *bvh = or_bvh_build(verts.data(), nv, idx.data(), nt);
+    check(bvh != nullptr, "oracle bvh");
+    check(or_bvh_build(verts.data(), nv - 1, idx.data(), nt) == nullptr, "oracle bvh: index range");
+    std::vector<float> a(4ull * W * H, 0.0f), b(4ull * W * H, 0.0f);
+    std::vector<uint32_t> sa = seeds, sb = seeds;
+    or_counters ca, cb;
+    for (uint32_t p = 0; p < 2; ++p) {
+        check(or_render_tris_bvh(a.data(), &cam, s.data(), 6, W, H, Wp, Hp, 2, 6, p, sa.data(), verts.data(),
+                                 idx.data(), nt, nullptr, 0, 0, 3, &ca, nullptr) == 0,
+              "oracle tris linear");
+        check(or_render_tris_bvh(b.data(), &cam, s.data(), 6, W, H, Wp, Hp, 2, 6, p, sb.data(), verts.data(),
+                                 idx.data(), nt, nullptr, 0, 0, 3, &cb, bvh) == 0,
+              "oracle tris bvh");
+    }
+    check(std::memcmp(a.data(), b.data(), a.size() * 4) == 0 && sa == sb, "linear == bvh");
+    check(ca.closest == cb.closest && ca.shadow == cb.shadow, "ray counts");
+    or_bvh_free(bvh);
+    std::printf("oracle ok\n");
+    return g_fail;
+}
+
+} // namespace
+
+int main(int argc, char **argv)
+{
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: asan_host ply FILE... | host | oracle\n");
+        return 2;
+    }
+    const std::string mode = argv[1];
+    if (mode == "ply") return run_ply(argc - 2, argv + 2);
+    if (mode == "host") return run_host();
+    if (mode == "oracle") return run_oracle();
+    return 2;
+}

@@ -1499,74 +1499,3 @@ def test_stepping_knobs_change_no_bits(tracer, pt, monkeypatch):
     for f, s in frames[1:]:
         np.testing.assert_array_equal(f, frames[0][0])
         np.testing.assert_array_equal(s, frames[0][1])
-
-
-def test_sample_split_at_full_size(tracer, pt, monkeypatch):
-    """Sample-split rendering on the dragon-class frame at full size, sampleRate 16 (16 chunks
-    of 16 samples), as a row-stripe tile of 8 (259k pixels: fewer than the resident lanes):
-    the same bits and seeds as whole-pixel tasks (RT_SPLIT=0), which the oracle pins."""
-    sc = pt.scenes
-    W, H, sr = 1920, 1080, 16
-    Wp, Hp = sc.padded_dims(W, H)
-    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
-    seeds = sc.default_seeds(Wp, Hp, skip=4)
-    tile = (8, 8, 5)
-    rows = len(np.arange(H)[(np.arange(H) // 8) % 8 == 5])
-    res = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("RT_SPLIT", mode)
-        rt = pt.RayTracer(0)
-        rt.setSpheres(sc.ply_scene())
-        rt.setCamera(sc.camera_spherical(W, **sc.PLY_CAMERA))
-        rt.setSampleRate(sr)
-        rt.setMaxPathDepth(6)
-        rt.setMesh(verts, idx)
-        rt.setSeeds(Wp, Hp, seeds)
-        out = np.zeros(W * rows * 4, np.float32)
-        rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
-        assert (rt.renderInfo()["split_chunks"] == 16) == (mode == "1")
-        res[mode] = (bits(out).copy(), rt.getSeeds().copy())
-        rt.close()
-    np.testing.assert_array_equal(res["1"][0], res["0"][0])
-    np.testing.assert_array_equal(res["1"][1], res["0"][1])
-
-
-def test_long_chains_of_the_8way_dragon_tile_vs_oracle(tracer, pt, oracle):
-    """The 8-way row-stripe tile of the headline frame (dragon class, 1920x1080, sampleRate 16 =
-    256 spp, maxDepth 6; tile (8, 8, 3): 1 of the 8 ranks of BASELINE's 8-GPU case): a
-    sample-split render whose long chains (box pixels and costly mesh pixels) take the 8-lane
-    subtree-parallel seed pass (k_chain_seeds, existence queries) on the second stream.  16 of those
-    pixels, spread over the list, equal the oracle's linear loop bit for bit — radiance and both
-    seed words (raytracer.cl:205-242, rtcommon.h:371-470) — so the pass that bounds N = 8 is
-    pinned against the reference's algorithm at the configuration it serves."""
-    sc = pt.scenes
-    W, H, sr = 1920, 1080, 16
-    Wp, Hp = sc.padded_dims(W, H)
-    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
-    S = sc.ply_scene()
-    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
-    seeds = sc.default_seeds(Wp, Hp, skip=9)
-    stripe, n_ranks, rank = 8, 8, 3
-    rows = np.arange(H)[(np.arange(H) // stripe) % n_ranks == rank]
-    rt = tracer
-    rt.setSpheres(S)
-    rt.setCamera(cam)
-    rt.setSampleRate(sr)
-    rt.setMaxPathDepth(6)
-    rt.setMesh(verts, idx)
-    rt.setSeeds(Wp, Hp, seeds)
-    got = np.zeros(len(rows) * W * 4, np.float32)
-    rt.rayTrace(got, W, H, 0, kernel=2, tile=(stripe, n_ranks, rank))
-    info = rt.renderInfo()
-    assert info["split_chunks"] == 16 and info["split_coop"] == 8 and info["split_guard"] == 0, info
-    long_px = rt.longChains()
-    assert len(long_px) == info["pixels_long"] and len(long_px) >= 1000, len(long_px)
-    pick = long_px[np.linspace(0, len(long_px) - 1, 16).astype(np.int64)]
-    yl, x = pick // W, pick % W
-    gpix = (rows[yl] * W + x).astype(np.uint32)  # the tile's local rows -> frame rows
-    exp = np.zeros(W * H * 4, np.float32)
-    sd = seeds.copy()
-    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, sd, verts, idx, pixels=gpix)
-    np.testing.assert_array_equal(bits(got.reshape(-1, 4)[pick]), bits(exp.reshape(-1, 4)[gpix]))
-    np.testing.assert_array_equal(_pixel_seeds(rt.getSeeds(), gpix, Wp, Hp, W), _pixel_seeds(sd, gpix, Wp, Hp, W))
-    assert got.reshape(-1, 4)[pick, :3].max() > 0

@@ -299,6 +299,15 @@ def main():
     rt.rayTrace(out, W, H, 0, kernel=kernel, tile=tile)
     cnt = rt.counters()
     rt.setCounting(False)
+    # the whole frame's query counts: at N > 1 (strong scaling) every rank's counting launch
+    # covers its own stripes, so the frame's totals are the sum over ranks (the roofline below
+    # stays rank 0's: its tile's counts against its own kernel time)
+    cnt_frame = {k: int(cnt.get(k, 0)) for k in ("rays_closest", "rays_shadow", "rays_skipped")}
+    if dist and n_ranks > 1:
+        v = torch.tensor([cnt_frame[k] for k in ("rays_closest", "rays_shadow", "rays_skipped")],
+                         dtype=torch.float64, device=f"cuda:{device}")
+        dist.all_reduce(v, op=dist.ReduceOp.SUM)
+        cnt_frame = dict(zip(("rays_closest", "rays_shadow", "rays_skipped"), (int(x) for x in v.tolist())))
     chain = None
     if world == 1 and kernel == pt.RayTracer.KERNEL_TRIS and not args.linear:
         chain = critical_chain(rt, pt, W, H, Wp, Hp, seeds0, kernel)
@@ -402,6 +411,8 @@ def main():
             else:
                 gpu_linear = {"skipped": f"~{est_s:.0f} s estimated for {W}x{H} x {n_tris} triangles per query"}
 
+    frame_rays = cnt_frame["rays_closest"] + cnt_frame["rays_shadow"]
+    traversed_share = (frame_rays - cnt_frame["rays_skipped"]) / max(frame_rays, 1)
     line = {
         "metric": (METRIC_WEAK if frames_per_rank else METRIC) if cfg == "dragon" else CONFIG_METRIC.get(
             cfg, f"Mrays/sec + frames/sec, {cfg}"),
@@ -415,8 +426,8 @@ def main():
         "frames_per_sec": round(steps * (world if frames_per_rank else 1) / elapsed, 4),
         # the same frames counting only the queries that ran a traversal (rank 0's counting
         # launch share; DESIGN.md §5: shadow rays answered without one are still rays)
-        "mrays_traversed_per_sec": round(mrays * (rays_cnt - cnt.get("rays_skipped", 0)) / max(rays_cnt, 1), 2),
-        "value_traversed": round(mrays * (rays_cnt - cnt.get("rays_skipped", 0)) / max(rays_cnt, 1), 2),
+        "mrays_traversed_per_sec": round(mrays * traversed_share, 2),
+        "value_traversed": round(mrays * traversed_share, 2),
         "value_rule": ("value counts the reference's queries (closest-hit + shadow, equal to the oracle's counts); "
                        "value_traversed leaves out the shadow rays answered without a traversal (tmax <= tmin, or "
                        "cos(wi) <= 0, whose term rtcommon.h:93-95 drops after the visibility test)"),
@@ -436,7 +447,8 @@ def main():
                    "rays_per_frame": int(rays / steps / (world if frames_per_rank else 1)),
                    # rays = the reference's queries (oracle-equal counts); shadow rays whose answer
                    # cannot change the pixel are answered without a traversal
-                   "rays_traversed_per_frame": int(rays_cnt - cnt.get("rays_skipped", 0)),
+                   "rays_traversed_per_frame": int(cnt_frame["rays_closest"] + cnt_frame["rays_shadow"]
+                                                   - cnt_frame["rays_skipped"]),
                    "mesh": mesh_info},
         "roofline": roofline,
         "cpu_baseline": cpu,

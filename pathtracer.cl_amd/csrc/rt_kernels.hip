@@ -238,6 +238,9 @@ __device__ __forceinline__ int node_children(uint4 q0, uint4 q1, uint4 q2, uint4
     const uint32_t nyw = py ? q1.z : q1.w, fyw = py ? q1.w : q1.z;
     const uint32_t nzw = pz ? q2.x : q2.y, fzw = pz ? q2.y : q2.x;
     int nhit = 0;
+    /* the any-hit order's per-query terms (below): -1 selects the longest-segment key, and the
+       penalty that sends boxes holding the ray origin last */
+    const float lsel = longest ? -1.0f : 0.0f, pen = any_hit ? 1e4f : 0.0f;
     /* Plane bytes as f16 subnormals: v_perm_b32 spreads two bytes of a plane word into
        the low bytes of two 16-bit halves (0x00bb = b * 2^-24 as f16, exact), and
        v_fma_mix_f32 converts a half and does the FMA in one instruction, with the
@@ -267,8 +270,8 @@ __device__ __forceinline__ int node_children(uint4 q0, uint4 q1, uint4 q2, uint4
            last, and a ray leaving the mesh (`longest`) takes the others by the length of
            its box segment, longest first — measured on the CPU model to find an occluder
            in the fewest steps; rays from the box walls keep nearest first. */
-        const float key = longest ? tn - tf : tn;
-        t[i] = h ? (any_hit && tn <= 0.0f ? key + 1e4f : key) : kInf;
+        const float key = __builtin_fmaf(lsel, tf, tn); /* tn - tf (longest) or tn, exactly */
+        t[i] = h ? (tn <= 0.0f ? key + pen : key) : kInf;
         nhit += h ? 1 : 0;
     }
     /* Determinant cull (rt_quant.h): the node's normal box bounds d . N = det over its

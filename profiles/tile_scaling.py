@@ -1,5 +1,6 @@
-"""Single-GPU rehearsal of strong scaling: time one rank's row-stripe tile of the bench
-frame for N = 1, 2, 4, 8 ranks (rank 0 and the slowest rank) against 1/N of the full frame.
+"""Single-GPU rehearsal of strong scaling: time every rank's row-stripe tile of the bench frame
+for N = 1, 2, 4, 8 ranks against the full frame, plus the root's assembly (the staging copy of
+the other ranks' tiles and k_assemble, HIP events) and a one-link xGMI model of the transfer.
 
     python profiles/tile_scaling.py [--config dragon] [--stripe 8]
 """
@@ -38,15 +39,20 @@ def main():
     rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS[args.config]))
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     res = {}
+    ptdist = ptload.submodule("dist")
+    frame = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     for n in (1, 2, 4, 8):
-        times, repaired, longc = [], [], []
+        times, repaired, longc, tiles = [], [], [], []
         for r in range(n):  # every rank's tile: the slowest sets the N-GPU frame time
             tile = (args.stripe, n, r) if n > 1 else None
+            rows = len(ptdist.tile_rows(H, args.stripe, n, r)) if n > 1 else H
+            buf = torch.zeros(rows * W * 4, dtype=torch.float32, device="cuda:0")
             best = 1e9
             for _ in range(args.reps):
-                rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
+                rt.rayTrace(buf, W, H, 0, kernel=2, tile=tile)
                 best = min(best, rt.lastKernelMs())
             times.append(best)
+            tiles.append(buf)
             info = rt.renderInfo()
             repaired.append(int(info.get("split_repaired", 0)))
             longc.append(int(info.get("pixels_long", 0)))
@@ -54,6 +60,30 @@ def main():
         res[n] = {"max_ms": max(times), "min_ms": min(times), "ranks_timed": len(times),
                   "rank_ms": [round(t, 3) for t in times], "split_chunks": info.get("split_chunks", 0),
                   "split_spec": info.get("split_spec", 0), "long_chains": longc, "repaired": repaired}
+        if n > 1:
+            # the root's side of the gather (rt_comm_gather_frame): the other ranks' tiles land in a
+            # staging buffer (here a device copy; over xGMI each peer's tile crosses its own link
+            # into the root's HBM) and k_assemble scatters every tile's stripes into the frame
+            stage = torch.empty(sum(t.numel() for t in tiles[1:]), dtype=torch.float32, device="cuda:0")
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            best = 1e9
+            for _ in range(5):
+                torch.cuda.synchronize()
+                ev0.record()
+                off, views = 0, [tiles[0]]
+                for t in tiles[1:]:
+                    stage[off:off + t.numel()].copy_(t)
+                    views.append(stage[off:off + t.numel()])
+                    off += t.numel()
+                ptdist.assemble_native(views, H, W, args.stripe, frame)
+                ev1.record()
+                torch.cuda.synchronize()
+                best = min(best, ev0.elapsed_time(ev1))
+            link_ms = max(t.numel() * 4 for t in tiles[1:]) / 153e9 * 1e3  # one 153 GB/s xGMI link per peer
+            res[n]["assembly_ms"] = round(best, 4)
+            res[n]["xgmi_link_ms_model"] = round(link_ms, 4)
+            res[n]["max_plus_assembly_ms"] = round(max(times) + best + link_ms, 3)
+        del tiles
     # the costliest pixel (counting launch with per-pixel stats, RT_PIXEL_STATS): queries and traversal
     # steps; in a sample-split tile a pixel's samples run as chunk tasks, whose counts add up per pixel
     # (the seed pass's rounds are reported apart)
@@ -85,6 +115,7 @@ def main():
     for n in (2, 4, 8):
         res[n]["ideal_ms"] = full / n
         res[n]["efficiency_vs_full"] = round(full / n / res[n]["max_ms"], 3)
+        res[n]["speedup_with_assembly"] = round(full / res[n]["max_plus_assembly_ms"], 3)
     print(json.dumps({"config": args.config, "W": W, "H": H, "spp": sr * sr, "tiles": res}))
 
 

@@ -85,7 +85,7 @@ constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
 #define RT_LONG_FINE 1 /* samples per stored seed (and per chunk task) of the subtree-parallel long chains */
 #endif
 #ifndef RT_REPAIR_WIDTH
-#define RT_REPAIR_WIDTH 16u /* lanes per repaired chain: its hit samples in runs of 15 */
+#define RT_REPAIR_WIDTH 64u /* lanes per repaired chain: its hit samples in runs of 63 */
 #endif
 #ifndef RT_REPAIR_SLOTS
 #define RT_REPAIR_SLOTS 4096u /* repaired pixels with per-sample seeds by slot (8.4 MB at 256 spp) */
@@ -526,20 +526,24 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
 {
     const uint32_t draws = 2u + 2u * (uint32_t)c->lights.size();
     const uint64_t key = (uint64_t)a.split_chunks << 40 | (uint64_t)a.split_chunk << 20 | draws;
-    if (!c->d_spec_mul) HIPCHK(c, hipMalloc(&c->d_spec_mul, 2 * 64 * sizeof(uint32_t)));
+    if (!c->d_spec_mul) HIPCHK(c, hipMalloc(&c->d_spec_mul, 4 * 64 * sizeof(uint32_t)));
     if (a.split_chunks > 64) return fail(c, RT_ERR_ARG, "speculated split: more than 64 chunks");
     if (key != c->spec_mul_key) {
-        c->h_spec_mul.assign(2 * 64, 1u);
+        c->h_spec_mul.assign(4 * 64, 1u);
         for (uint32_t ch = 0; ch < a.split_chunks; ++ch) {
             const uint64_t k = (uint64_t)ch * a.split_chunk * draws;
             c->h_spec_mul[2 * ch] = powmod(36969u, k, 36969ull * 65536u - 1u);
             c->h_spec_mul[2 * ch + 1] = powmod(18000u, k, 18000ull * 65536u - 1u);
         }
+        for (uint32_t j = 0; j < 64; ++j) { /* the repair's runs: lane j's sample is j x D draws on */
+            c->h_spec_mul[128 + 2 * j] = powmod(36969u, (uint64_t)j * draws, 36969ull * 65536u - 1u);
+            c->h_spec_mul[128 + 2 * j + 1] = powmod(18000u, (uint64_t)j * draws, 18000ull * 65536u - 1u);
+        }
         /* on the render stream, after the previous frame's chunk tasks and repair pass (which read
            the multipliers: split_render ends with the render stream waiting on the other two); the
            wait keeps the host copy alive until the upload is done (a rare event: the key changes
            with the chunking or the light count) */
-        HIPCHK(c, hipMemcpyAsync(c->d_spec_mul, c->h_spec_mul.data(), 2 * 64 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(c->d_spec_mul, c->h_spec_mul.data(), 4 * 64 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         HIPCHK(c, hipStreamSynchronize(st));
         c->spec_mul_key = key;
     }
@@ -556,6 +560,7 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
     a.split_spec = 1;
     a.split_spec_draws = draws;
     a.split_spec_mul = c->d_spec_mul;
+    a.split_run_mul = c->d_spec_mul + 128;
     a.split_dirty = c->d_split_dirty;
     a.split_repair = c->d_split_repair;
     return RT_OK;
@@ -640,7 +645,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_counter = a.split_counter + 48;
         r.work_counter = a.work_counter + 48;
         r.split_gpw = c->split_gpw;
-        r.split_seed_blocks = 16;
+        r.split_seed_blocks = 16u * RT_REPAIR_WIDTH / 16u; /* up to 4 x 16 chains at once at any width */
         r.split_chunk = a.split_fine;
         r.split_chunks = (a.sample_rate * a.sample_rate + r.split_chunk - 1u) / r.split_chunk;
         r.split_restart = a.split_dirty; /* each chain from its first missed chunk on */

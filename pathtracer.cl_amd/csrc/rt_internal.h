@@ -206,6 +206,7 @@ struct RtTriLaunch {
     uint32_t split_spec;          /* RT_SPLIT_MESH: the mesh pixels' chunk seeds by jump-ahead */
     uint32_t split_spec_draws;    /* random numbers per sample of a speculated pixel */
     const uint32_t *split_spec_mul; /* per chunk c: a_x^(c chunk D) mod m_x, a_y^(c chunk D) mod m_y */
+    const uint32_t *split_run_mul;  /* per lane j < 64: a_x^(j D) mod m_x, a_y^(j D) mod m_y (the repair's runs) */
     uint32_t *split_dirty;        /* per pixel: the first chunk that saw a camera ray miss (~0u: none) */
     uint32_t *split_repair;       /* the marked pixels (yl * W + x) */
     const uint32_t *split_n_dev;  /* RT_SPLIT_BOX: the item count from device memory (NULL: split_n_box) */

@@ -25,6 +25,11 @@
 
 #pragma clang fp contract(off)
 
+#ifndef RT_DIAG_MIX
+#define RT_DIAG_MIX 0 /* diagnostics build (profiles/step_mix.py): counting launches report the stepping
+                         rounds' wave-step mix in the per-pixel-maximum counters */
+#endif
+
 namespace {
 
 constexpr float kInf = __builtin_huge_valf();
@@ -612,8 +617,11 @@ __device__ __forceinline__ void flush_counters(unsigned long long *dst, const un
         const unsigned long long w = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0) atomicAdd(&dst[i], w);
     }
-    if (with_trav) /* per-pixel maxima */
-        for (int i = RT_N_SUM_COUNTERS; i < RT_N_COUNTERS; ++i) atomicMax(&dst[i], v[i]);
+    if (with_trav) /* per-pixel maxima (RT_DIAG_MIX builds: the wave-step mix, summed) */
+        for (int i = RT_N_SUM_COUNTERS; i < RT_N_COUNTERS; ++i) {
+            if (RT_DIAG_MIX) atomicAdd(&dst[i], v[i]);
+            else atomicMax(&dst[i], v[i]);
+        }
 }
 
 /* raytracer.cl:81-85: normalize(view + right*a + up*b), float4 lanes incl. w,
@@ -1536,11 +1544,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                    against the pixel's candidate list; the chain takes the run up to its first miss */
                 const uint32_t D = a.split_spec_draws, rem = spp - sample;
                 const uint32_t runmax = rem < (uint32_t)(G - 1) ? rem : (uint32_t)(G - 1);
-                Seed sl = seed;
-                for (uint32_t i = 0; i < (uint32_t)sub * D; ++i) { /* frand's state steps (rng.h:24-42) */
-                    sl.x = 36969u * (sl.x & 65535u) + (sl.x >> 16);
-                    sl.y = 18000u * (sl.y & 65535u) + (sl.y >> 16);
-                }
+                /* frand's state stepped sub x D draws on (rng.h:24-42): one multiplication by the
+                   jump multiplier of the lane (mwc_jump) */
+                Seed sl;
+                sl.x = mwc_jump<36969u>(seed.x, (uint32_t)sub * D, a.split_run_mul[2 * sub]);
+                sl.y = mwc_jump<18000u>(seed.y, (uint32_t)sub * D, a.split_run_mul[2 * sub + 1]);
                 bool hit = false;
                 if ((uint32_t)sub < runmax) {
                     const uint32_t s = sample + (uint32_t)sub;
@@ -1559,8 +1567,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                         hit = h && !(tt < RT_SMALL_F) && tt <= kInf; /* the closest-hit acceptance */
                     }
                 }
-                const uint32_t hm = (uint32_t)((__ballot(hit) & gmask) >> gbase);
-                const uint32_t m = (uint32_t)__builtin_ctz(~hm); /* the run's hits before its first miss */
+                /* the run's hits before its first miss (64-bit: a group may be the whole wave; lane
+                   runmax <= G - 1 never hits, so ~hm has a set bit) */
+                const unsigned long long hm = (__ballot(hit) & gmask) >> gbase;
+                uint32_t m = (uint32_t)__builtin_ctzll(~hm);
+                if (m > runmax) { /* a defect: reported (rt_synchronize fails the render), the run taken as ended */
+                    if (lane == gbase) atomicOr(guard, (unsigned long long)RT_GUARD_INDEX);
+                    m = runmax;
+                }
                 if ((uint32_t)sub < m && (sample + (uint32_t)sub) % fine == 0u)
                     reinterpret_cast<uint2 *>(a.split_seed)[(size_t)pslot * nseed + (sample + (uint32_t)sub) / fine] =
                         make_uint2(sl.x, sl.y);
@@ -1969,7 +1983,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         ps[6] = COUNT ? (uint32_t)(pix_c >> 6) : 0u;
                         ps[7] = COUNT ? (uint32_t)pix_it : 0u;
                     }
-                    if (COUNT) {
+                    if (COUNT && !RT_DIAG_MIX) {
                         const unsigned long long dt = wave_clock() - pix_t0;
                         cnt[10] = dt > cnt[10] ? dt : cnt[10];
                         cnt[11] = pix_q > cnt[11] ? pix_q : cnt[11];
@@ -2186,6 +2200,16 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 /* RT_STEP_UNROLL steps per exit check (fewer wave-level ballots and branches) */
 #pragma unroll
                 for (int u = 0; u < RT_STEP_UNROLL; ++u) {
+#if RT_DIAG_MIX
+                    if (COUNT) { /* diagnostics build: wave-steps holding node and leaf lanes / nodes only / leaves only */
+                        const unsigned long long bn = __ballot(running && ts.node >= 0), bl = __ballot(running && ts.node < 0);
+                        if ((threadIdx.x & 63) == 0) {
+                            cnt[10] += (bn && bl) ? 1u : 0u;
+                            cnt[11] += (bn && !bl) ? 1u : 0u;
+                            cnt[12] += (!bn && bl) ? 1u : 0u;
+                        }
+                    }
+#endif
                     if (running) {
                         const bool shadow = (mode == M_SHADOW);
                         TravCounts tc = {0u, 0u, 0u};
@@ -2996,7 +3020,9 @@ int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
     if (e != hipSuccess) return (int)e;
     const dim3 g(a.split_seed_blocks), b(RT_BLOCK);
     if (a.split_which == RT_SPLIT_BOX && a.split_coop >= 8) { /* subtree-parallel */
-        if (a.split_coop == 16 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<16, true>), g, b, 0, st, a);
+        if (a.split_coop == 64 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<64, true>), g, b, 0, st, a);
+        else if (a.split_coop == 32 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<32, true>), g, b, 0, st, a);
+        else if (a.split_coop == 16 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<16, true>), g, b, 0, st, a);
         else if (a.split_coop == 8 && a.split_restart) hipLaunchKernelGGL((k_chain_seeds<8, true>), g, b, 0, st, a);
         else if (a.split_coop == 8) hipLaunchKernelGGL(k_chain_seeds<8>, g, b, 0, st, a);
         else if (a.split_coop == 32) hipLaunchKernelGGL(k_chain_seeds<32>, g, b, 0, st, a);

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--config", default="dragon")
     ap.add_argument("--stripe", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--ns", default="1,2,4,8", help="rank counts to rehearse (1 is always timed: the reference)")
     args = ap.parse_args()
     import torch
     import ptload
@@ -41,7 +42,8 @@ def main():
     res = {}
     ptdist = ptload.submodule("dist")
     frame = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
-    for n in (1, 2, 4, 8):
+    ns = sorted({1} | {int(v) for v in args.ns.replace(":", ",").split(",")})
+    for n in ns:
         times, repaired, longc, tiles = [], [], [], []
         for r in range(n):  # every rank's tile: the slowest sets the N-GPU frame time
             tile = (args.stripe, n, r) if n > 1 else None
@@ -88,7 +90,7 @@ def main():
     # steps; in a sample-split tile a pixel's samples run as chunk tasks, whose counts add up per pixel
     # (the seed pass's rounds are reported apart)
     path = os.path.join(tempfile.gettempdir(), f"tile_stats_{os.getpid()}.bin")
-    for n, r in ((1, 0), (8, 0), (8, 1)):
+    for n, r in ((1, 0), (8, 0), (8, 1)) if 8 in ns else ((1, 0),):
         tile = (args.stripe, n, r) if n > 1 else None
         os.environ["RT_PIXEL_STATS"] = path
         rt.setCounting(True)
@@ -112,11 +114,11 @@ def main():
             e["max_pixel_ms_at_2.4GHz"] = c["pixel_clocks_max"] / 2.4e6
         res.setdefault("pixel", {})[f"{n}:{r}"] = e
     full = res[1]["max_ms"]
-    for n in (2, 4, 8):
+    for n in ns[1:]:
         res[n]["ideal_ms"] = full / n
         res[n]["efficiency_vs_full"] = round(full / n / res[n]["max_ms"], 3)
         res[n]["speedup_with_assembly"] = round(full / res[n]["max_plus_assembly_ms"], 3)
-    print(json.dumps({"config": args.config, "W": W, "H": H, "spp": sr * sr, "tiles": res}))
+    print(json.dumps({"config": args.config, "W": W, "H": H, "spp": sr * sr, "stripe": args.stripe, "tiles": res}))
 
 
 if __name__ == "__main__":

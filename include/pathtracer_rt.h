@@ -222,6 +222,8 @@ typedef struct rt_render_info {
                                   seeds (no seed pass for them; pixels near a silhouette run as long chains) */
     uint32_t split_repaired;   /* read after completion: speculated pixels whose camera rays missed the
                                   mesh after all, re-rendered by the repair pass (seed pass + chunks) */
+    uint32_t split_hit_depth;  /* 1: the long chains' chunk tasks answered their box segments' closest-hit
+                                  queries from the seed pass's per-sample mesh-hit depths (no traversal) */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
 /* The long chains of the last sample-split render (pixels_long of them: tile-local y * W + x, the

@@ -127,6 +127,7 @@ class RtRenderInfo(ctypes.Structure):
         ("split_guard", ctypes.c_uint32),
         ("split_spec", ctypes.c_uint32),
         ("split_repaired", ctypes.c_uint32),
+        ("split_hit_depth", ctypes.c_uint32),
     ]
 
 

@@ -171,6 +171,13 @@ struct rt_ctx {
     uint32_t *d_repair_seed = nullptr; /* the repaired pixels' seeds by slot (the first RT_REPAIR_SLOTS of them) */
     size_t repair_seed_bytes = 0;
     uint32_t repair_slots = RT_REPAIR_SLOTS; /* RT_REPAIR_SLOTS (env, test knob): repaired pixels with per-sample seeds */
+#ifndef RT_HIT_DEPTH
+#define RT_HIT_DEPTH 1
+#endif
+    /* RT_HIT_DEPTH (env, A/B knob): the slotted long chains' seed pass records each sample's mesh-hit
+       depth after the seeds (split_hit_depth), and their chunk tasks skip the box segments' traversals */
+    uint32_t hit_depth = RT_HIT_DEPTH;
+    bool last_hit_depth = false; /* the last sample-split render used split_hit_depth */
     size_t split_box_cap = 0;
     uint32_t n_split_box = 0;
     int split_box_grid = 0;           /* the box pixels' seed-pass grid of the render being launched */
@@ -566,6 +573,18 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
     return RT_OK;
 }
 
+/* The long chains' mesh-hit depths (split_hit_depth): their subtree-parallel seed pass answers, for
+   every segment of every sample, whether its closest-hit query accepts a triangle — the same answer
+   the chunk task's traversal would give (the seeds depend on it) — and stores the depth of the one
+   that does (a path ends at its mesh hit, rtcommon.h:411-421); a chunk task then answers the box
+   segments above it without a traversal.  One sample per task (the depth is read at the take), and
+   depths in a byte.  Not for the repair pass: its chains are mesh pixels, whose paths meet the mesh
+   at the camera ray. */
+bool hit_depth_on(const rt_ctx *c, const RtTriLaunch &t)
+{
+    return c->hit_depth && t.split_coop >= 8 && !t.split_restart && t.split_chunk == 1u && t.max_depth < 255u;
+}
+
 /* A sample-split render: the box pixels' seed pass, their chunks and their in-order sums on
    stream2, beside the mesh pixels' seed pass (none when speculated) and chunks on the render
    stream (the box pixels' chains are the long ones: they overlap the rest of the frame instead
@@ -595,7 +614,9 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
             b.split_chunk = RT_LONG_FINE;
             b.split_chunks = (spp + RT_LONG_FINE - 1u) / RT_LONG_FINE;
             b.split_nseed = b.split_chunks + 1u;
-            const size_t bytes = (size_t)n_box * b.split_nseed * 8u;
+            const size_t seed_bytes = (size_t)n_box * b.split_nseed * 8u;
+            const bool hd = hit_depth_on(c, b);
+            const size_t bytes = seed_bytes + (hd ? (size_t)n_box * spp : 0u);
             if (c->long_seed_bytes < bytes) {
                 free_dev(c->d_long_seed);
                 c->d_long_seed = nullptr;
@@ -605,6 +626,8 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
             }
             b.split_seed = c->d_long_seed;
             b.split_seed_slot = 1;
+            b.split_hit_depth = hd ? reinterpret_cast<uint8_t *>(c->d_long_seed) + seed_bytes : nullptr;
+            c->last_hit_depth = hd;
         }
         const int chunk_grid = (int)std::min<uint64_t>((uint64_t)blocks, ((uint64_t)n_box * b.split_chunks + RT_BLOCK - 1) / RT_BLOCK);
         int e = rt_launch_split_seeds(b, c->stream2);
@@ -854,6 +877,7 @@ try {
     }
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     c->repair_slots = std::max(1u, env_u32("RT_REPAIR_SLOTS", RT_REPAIR_SLOTS)); /* test knob: the path beyond them */
+    c->hit_depth = env_u32("RT_HIT_DEPTH", RT_HIT_DEPTH) != 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -1485,6 +1509,7 @@ try {
         }
         if (!e && a.split_chunks) {
             a.n_recs = (uint32_t)std::min<size_t>(c->tris_cap, 0xffffffffu); /* the list area included */
+            c->last_hit_depth = false;
             e = split_render(c, a, blocks, st);
         }
         else if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
@@ -1502,6 +1527,7 @@ try {
         c->info.split_chunks = a.split_chunks;
         c->info.split_coop = a.split_chunks && a.split_n_box ? a.split_coop : 0u;
         c->info.split_spec = a.split_chunks ? a.split_spec : 0u;
+        c->info.split_hit_depth = a.split_chunks && c->last_hit_depth ? 1u : 0u;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
         c->info_list_pending = lists;

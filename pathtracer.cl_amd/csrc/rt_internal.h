@@ -218,6 +218,12 @@ struct RtTriLaunch {
     uint32_t split_seed_slot; /* RT_SPLIT_BOX: split_seed indexed by the item (the chain's slot in its list, minus
                                  split_item_base: its own buffer, a seed per split_fine samples), not by pixel */
     uint32_t split_item_base, split_item_cap; /* RT_SPLIT_BOX: the items split_box[base ...], at most cap (0: all) */
+    /* RT_SPLIT_BOX, slotted seeds, one sample per task: per slot and sample (slot x spp + sample) the
+       depth of the segment whose closest-hit query meets the mesh, 0xff for a path that meets only
+       the box — written by the subtree-parallel seed pass, which answers that very question for
+       every segment; the chunk tasks answer the closest-hit queries above it (box segments: no
+       triangle accepted) without a traversal.  NULL: every query traverses. */
+    uint8_t *split_hit_depth;
 };
 enum { RT_SPLIT_ALL = 0, RT_SPLIT_MESH = 1, RT_SPLIT_BOX = 2 };
 /* k_split_finish parts: every pixel; a list's pixels (split_box: the long chains, the repaired); the mesh

@@ -1531,6 +1531,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                     }
                 }
                 if (sample_done) {
+                    if (!RUNS && a.split_hit_depth && lane == gbase) /* (not the repair pass: NULL there) */
+                        a.split_hit_depth[(size_t)pslot * spp + sample] = ghit ? (uint8_t)depth : (uint8_t)0xffu;
                     ++sample;
                     next = true;
                 }
@@ -1772,6 +1774,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     /* the pixel's class from the probe: -1 mesh pixel; a box pixel (long sample chain): -2, or
        its slot >= 0 among the long chains of a sample-split render */
     int pclass = -1;
+    /* SPLIT over long chains with split_hit_depth: the depth of the sample's mesh hit (the closest
+       queries above it meet only the box); 0 otherwise */
+    int hit_depth = 0;
     bool fin = false;     /* the lane's query completed: ts.best / ts.best_t hold its result */
     TravState ts;
     ts.node = 0;
@@ -1791,7 +1796,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
 
     for (;;) {
-        const unsigned long long t_d0 = COUNT ? wave_clock() : 0ull;
+        const unsigned long long t_d0 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
         for (;;) {
         if (fin) {
@@ -1927,6 +1932,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 }
             }
             if (SPLIT && sample_done) { /* the sample's radiance, summed in order by k_split_finish */
+                hit_depth = 0; /* read per task: its first sample's */
                 float *dst = a.split_col + ((size_t)sample * (a.W * a.Hl) + (yl * a.W + x)) * 3u;
                 dst[0] = col_x;
                 dst[1] = col_y;
@@ -1978,10 +1984,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         ps[2] = COUNT ? (uint32_t)pix_q : 0u;
                         ps[3] = COUNT ? (uint32_t)pix_steps : 0u;
-                        ps[4] = COUNT ? (uint32_t)(pix_d >> 6) : 0u;
-                        ps[5] = COUNT ? (uint32_t)(pix_ab >> 6) : 0u;
-                        ps[6] = COUNT ? (uint32_t)(pix_c >> 6) : 0u;
-                        ps[7] = COUNT ? (uint32_t)pix_it : 0u;
+                        ps[4] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_d >> 6) : 0u;
+                        ps[5] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_ab >> 6) : 0u;
+                        ps[6] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_c >> 6) : 0u;
+                        ps[7] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)pix_it : 0u;
                     }
                     if (COUNT && !RT_DIAG_MIX) {
                         const unsigned long long dt = wave_clock() - pix_t0;
@@ -1999,7 +2005,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         const float cw_q = qd.x * hn.x + qd.y * hn.y + qd.z * hn.z;
         const bool issued = mode == M_SHADOW && !fin && !running;
         const bool need_trav = stmax > RT_SMALL_F && cw_q > 0;
-        const bool redo = issued && !need_trav;
+        /* likewise a long chain's box segment (split_hit_depth): no triangle accepted */
+        const bool known_miss = SPLIT && mode == M_CLOSEST && !fin && !running && (int)depth < hit_depth;
+        const bool redo = (issued && !need_trav) || known_miss;
         if (!__any(redo)) break;
         if (redo) {
             ts.best = -1;
@@ -2008,9 +2016,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         }
         }
 
-        const unsigned long long t_d1 = COUNT ? wave_clock() : 0ull;
-        if (COUNT) {
-            cnt[RT_CNT_SHADE] += t_d1 - t_d0;
+        const unsigned long long t_d1 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
+        if (COUNT) cnt[RT_CNT_SHADE] += t_d1 - t_d0;
+        if (COUNT || RT_PLAIN_PIXEL_STATS) { /* (the plain launch's phase clocks: RT_PLAIN_PIXEL_STATS builds) */
             pix_d += t_d1 - t_d0;
             ++pix_it;
         }
@@ -2076,6 +2084,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                     if (SPLIT && take) {
                         sample = chunk * a.split_chunk;
+                        if (a.split_hit_depth) hit_depth = a.split_hit_depth[(size_t)sbase * spp + sample];
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
                         mode = M_NEWSAMPLE;
                         if (COUNT) pix_q = pix_steps = 0;
@@ -2089,8 +2098,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         if (COUNT) {
                             pix_t0 = wave_clock();
                             pix_q = pix_steps = 0;
-                            pix_d = pix_ab = pix_c = pix_it = 0;
                         }
+                        if (COUNT || RT_PLAIN_PIXEL_STATS) pix_d = pix_ab = pix_c = pix_it = 0;
                         ACC_SET(0, 0.0f);
                         ACC_SET(1, 0.0f);
                         ACC_SET(2, 0.0f);
@@ -2156,7 +2165,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                    term is dropped whatever the visibility (rtcommon.h:93-95 tests
                    cosWi > 0 after the visibility test; the ray is const there, and
                    both draws were already made).  Same pixel, same seeds. */
-                if (shadow && (!(qt > RT_SMALL_F) || !(qd.x * hn.x + qd.y * hn.y + qd.z * hn.z > 0))) {
+                if ((shadow && (!(qt > RT_SMALL_F) || !(qd.x * hn.x + qd.y * hn.y + qd.z * hn.z > 0))) ||
+                    (SPLIT && !shadow && (int)depth < hit_depth)) { /* a long chain's box segment */
                     ts.best = -1;
                     fin = true;
                     ++cnt[RT_CNT_SKIPPED];
@@ -2180,8 +2190,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                 }
             }
-            const unsigned long long t_c0 = COUNT ? wave_clock() : 0ull;
-            if (COUNT) pix_ab += t_c0 - t_d1;
+            const unsigned long long t_c0 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
+            if (COUNT || RT_PLAIN_PIXEL_STATS) pix_ab += t_c0 - t_d1;
             /* a wave holding box pixels (the long serial chains that set the frame time)
                leaves the stepping rounds after fewer completed queries: less idling on the
                critical path, at the price of more (less full) shading passes */
@@ -2233,9 +2243,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 /* a box pixel's query completed: its chain (the frame's critical path) moves on */
                 if (a.box_exit && (fin_lanes & costly_lanes)) break;
             }
-            if (COUNT) {
+            if (COUNT || RT_PLAIN_PIXEL_STATS) {
                 const unsigned long long dc = wave_clock() - t_c0;
-                cnt[6] += dc;
+                if (COUNT) cnt[6] += dc;
                 pix_c += dc;
             }
         } else if (pending) {

@@ -76,17 +76,31 @@ def main():
         t = f * end
         res["pixels_running_at_pct_of_span"][f] = int(((start <= t) & (fin > t)).sum())
     res["started_pct"] = {p: float(np.percentile(start, p)) for p in (50, 90, 99, 100)}
+    # loop iterations and phase clocks: the plain launch's in a RT_PLAIN_PIXEL_STATS build, else the
+    # counting launch's
+    ph = s if s[..., 4:8].any() else sc_
+    res["phase_source"] = "plain" if ph is s and s is not sc_ else "counting"
     # the 20 last finishers
     idx = np.argsort(fin.ravel())[-20:]
     res["last"] = [{"x": int(i % W), "y": int(i // W), "start": round(float(start.ravel()[i]), 2),
                     "finish": round(float(fin.ravel()[i]), 2), "queries": int(q.ravel()[i]),
-                    "steps": int(steps.ravel()[i])} for i in idx]
+                    "steps": int(steps.ravel()[i]),
+                    # counting launch: loop iterations and wave clocks (x 64) in the path advance (D),
+                    # the refill + camera ray (A/B) and the stepping rounds (C) while the pixel ran
+                    "iters": int(ph[..., 7].ravel()[i]), "d_kclk": int(ph[..., 4].ravel()[i]) * 64 // 1000,
+                    "ab_kclk": int(ph[..., 5].ravel()[i]) * 64 // 1000,
+                    "c_kclk": int(ph[..., 6].ravel()[i]) * 64 // 1000} for i in idx]
     # costly pixels: many queries
     heavy = q > 2 * np.median(q)
     res["heavy_pixels"] = int(heavy.sum())
     res["heavy_start_pct"] = {p: float(np.percentile(start[heavy], p)) for p in (50, 90, 100)}
     res["heavy_dur_pct"] = {p: float(np.percentile(dur[heavy], p)) for p in (10, 50, 90, 100)}
     res["light_dur_pct"] = {p: float(np.percentile(dur[~heavy], p)) for p in (10, 50, 90, 100)}
+    it = ph[..., 7]
+    res["iters_pct"] = {p: float(np.percentile(it, p)) for p in (50, 90, 99, 100)}
+    res["heavy_iters_pct"] = {p: float(np.percentile(it[heavy], p)) for p in (50, 90, 100)}
+    tot = ph[..., 4:7].sum(axis=(0, 1)).astype(np.float64)
+    res["phase_share"] = {"D": tot[0] / tot.sum(), "AB": tot[1] / tot.sum(), "C": tot[2] / tot.sum()}
     txt = json.dumps(res, indent=1)
     print(txt)
     if argv:

@@ -170,9 +170,9 @@ def test_dragon_8way_tile_sr16_whole_tile_vs_bvh_oracle(tracer, pt, oracle, drag
     """One whole 8-way row-stripe tile (stripe 8, rank 3 of 8: BASELINE configs[4]'s sharding)
     of the headline frame at its own sampleRate 16 (256 spp): the sample-split path — speculated
     mesh pixels' chunks, the long chains' 8-lane subtree-parallel seed pass and single-sample
-    chunks on the second stream, the repair pass of the speculated pixels whose camera rays
-    missed, the in-order sums per part — against the oracle on every pixel and seed slot of the
-    tile."""
+    chunks on the second stream (their box segments answered from the seed pass's mesh-hit
+    depths), the repair pass of the speculated pixels whose camera rays missed, the in-order sums
+    per part — against the oracle on every pixel and seed slot of the tile."""
     d = dragon
     tile = (8, 8, 3)
     rows = _tile_rows(d["H"], tile)
@@ -183,6 +183,7 @@ def test_dragon_8way_tile_sr16_whole_tile_vs_bvh_oracle(tracer, pt, oracle, drag
     assert info["split_chunks"] == 16 and info["split_coop"] == 8 and info["split_spec"] == 1, info
     assert info["split_guard"] == 0 and info["pixels_long"] >= 1000, info
     assert info["split_repaired"] > 0, info  # the repair pass ran on this tile
+    assert info["split_hit_depth"] == 1, info  # the long chains' box segments answered from the seed pass
     got_seeds = rt.getSeeds()
     rt.close()
     pix = (rows[:, None] * d["W"] + np.arange(d["W"])[None, :]).reshape(-1).astype(np.uint32)

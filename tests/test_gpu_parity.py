@@ -1133,6 +1133,9 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr, width):
         assert info["split_chunks"] == (spp + csz - 1) // csz
         # the long chains ran on their own stream with `width` lanes per chain
         assert info["pixels_long"] > 0 and info["split_coop"] == width and info["split_guard"] == 0, info
+        # subtree-parallel long chains: their chunk tasks answer the box segments from the seed
+        # pass's per-sample mesh-hit depths (no traversal for them)
+        assert info["split_hit_depth"] == (1 if width >= 8 else 0), info
         # the mesh pixels' chunk seeds jumped ahead from their frame seeds (no seed pass for them)
         assert info["split_spec"] == 1, info
         assert len(rt.longChains()) == info["pixels_long"]

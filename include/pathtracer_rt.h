@@ -224,6 +224,8 @@ typedef struct rt_render_info {
                                   mesh after all, re-rendered by the repair pass (seed pass + chunks) */
     uint32_t split_hit_depth;  /* 1: the long chains' chunk tasks answered their box segments' closest-hit
                                   queries from the seed pass's per-sample mesh-hit depths (no traversal) */
+    uint32_t schedule_measured; /* 1: the queue's tiles were ordered by the view's previous frame's measured
+                                   per-pixel costs (its wave iterations), not by the cost probe */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
 /* The long chains of the last sample-split render (pixels_long of them: tile-local y * W + x, the

@@ -128,6 +128,7 @@ class RtRenderInfo(ctypes.Structure):
         ("split_spec", ctypes.c_uint32),
         ("split_repaired", ctypes.c_uint32),
         ("split_hit_depth", ctypes.c_uint32),
+        ("schedule_measured", ctypes.c_uint32),
     ]
 
 

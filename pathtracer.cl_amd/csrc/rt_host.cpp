@@ -199,6 +199,16 @@ struct rt_ctx {
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
     bool schedule_rebuilt = false; /* the last triangle render recomputed the schedule */
+#ifndef RT_MEASURED_LPT
+#define RT_MEASURED_LPT 1
+#endif
+    /* measured-cost schedule (RT_MEASURED_LPT, env A/B knob): a view's first whole-pixel frame
+       records each pixel's wave iterations (pixel_iter), its next frame re-sorts the tiles by them */
+    int measured_lpt = RT_MEASURED_LPT;
+    uint32_t *d_pixel_iter = nullptr;
+    size_t pixel_iter_px = 0;
+    bool iter_recorded = false;  /* this view's costs are in d_pixel_iter */
+    bool order_measured = false; /* d_order is sorted by them */
     rt_render_info info = {};      /* rt_last_render_info */
     bool info_list_pending = false; /* info.list_records / list_pixels_tree still to be read */
     size_t info_list_px = 0;        /* pixels of the render the pending list counts belong to */
@@ -738,8 +748,19 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
     const uint32_t n_t = ((W + 7) / 8) * ((hl + 7) / 8);
     c->schedule_rebuilt = false;
-    if (key == c->order_key) return RT_OK;
+    if (key == c->order_key) {
+        if (c->iter_recorded && !c->order_measured && c->d_order) {
+            /* the view's second frame: its tiles by the first frame's measured costs (the probe's
+               few rays miss where the samples' shadow rays are long: dragon frame) */
+            const int e = rt_sched_order_measured(c->sched, c->d_pixel_iter, W, hl, c->d_order, st);
+            if (e) return hip_fail(c, (hipError_t)e, "measured tile order");
+            c->order_measured = true;
+        }
+        return RT_OK;
+    }
     c->order_key.clear();
+    c->iter_recorded = false;
+    c->order_measured = false;
     c->n_split_box = 0;
     if (trav_kind(c) != RT_TRAV_BVH4Q || a.nodes != reinterpret_cast<const float *>(c->d_nodes4q)) {
         /* the probe walks the compressed tree with its spill layout: other traversal kinds
@@ -869,6 +890,7 @@ try {
     if (const char *v = getenv("RT_SPLIT_MB")) c->split_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
+    if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);
@@ -907,6 +929,7 @@ try {
     free_dev(c->d_flags);
     free_dev(c->d_class);
     free_dev(c->d_split_seed);
+    free_dev(c->d_pixel_iter);
     free_dev(c->d_long_seed);
     free_dev(c->d_repair_seed);
     free_dev(c->d_split_col);
@@ -1390,6 +1413,26 @@ try {
                                               blocks_split - box_blocks));
             }
         }
+        /* whole pixels of many samples (long tasks, a few dequeues per microsecond): queue takes of
+           exactly the items the idle lanes need, so no wave holds the queue's last tiles back
+           (RT_TAKE_EXACT=0/1: an A/B knob) */
+        a.take_exact = !a.split_chunks && c->sample_rate * c->sample_rate >= 16u ? 1u : 0u;
+        if (const char *v = getenv("RT_TAKE_EXACT")) a.take_exact = atoi(v) != 0 && !a.split_chunks ? 1u : 0u;
+        /* a whole-pixel frame under the probe's order records its pixels' costs for the next frame */
+        a.pixel_iter = nullptr;
+        bool record_iter = false;
+        if (a.tile_order && !a.split_chunks && c->measured_lpt && !c->order_measured && c->sample_rate > 0) {
+            const size_t npx_i = (size_t)W * hl;
+            if (c->pixel_iter_px < npx_i) {
+                free_dev(c->d_pixel_iter);
+                c->d_pixel_iter = nullptr;
+                c->pixel_iter_px = 0;
+                HIPCHK(c, hipMalloc(&c->d_pixel_iter, 2 * npx_i * sizeof(uint32_t)));
+                c->pixel_iter_px = npx_i;
+            }
+            a.pixel_iter = c->d_pixel_iter;
+            record_iter = true;
+        }
         const double sched_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
         if (getenv("RT_DEBUG_LAUNCH")) /* diagnostics: the launch shape */
             fprintf(stderr,
@@ -1513,6 +1556,7 @@ try {
             e = split_render(c, a, blocks, st);
         }
         else if (!e) e = rt_launch_tris(a, trav, c->counting, blocks, st);
+        if (!e && record_iter) c->iter_recorded = true;
         c->last_long = a.split_chunks ? a.split_n_box : 0u;
         HIPCHK(c, hipEventRecord(c->ev1, st));
         c->info = rt_render_info{};
@@ -1528,6 +1572,7 @@ try {
         c->info.split_coop = a.split_chunks && a.split_n_box ? a.split_coop : 0u;
         c->info.split_spec = a.split_chunks ? a.split_spec : 0u;
         c->info.split_hit_depth = a.split_chunks && c->last_hit_depth ? 1u : 0u;
+        c->info.schedule_measured = a.tile_order && c->order_measured ? 1u : 0u;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
         c->info_list_pending = lists;

@@ -560,7 +560,10 @@ __device__ __forceinline__ float uniform_f(float v)
    refill.  A single head word saturates at about 88 dequeues per microsecond
    (MI355X_MICROARCH.md, dequeue), which the many short tasks of a sample-split launch exceed.
    Wave-uniform: call with every lane active; bnext / bend start equal; batch >= the takers
-   per wave (k <= batch). */
+   per wave (k <= batch).  batch 0: exactly the items the idle lanes need, none held back — for
+   queues of long tasks (many-sample whole pixels), where a batch held by a wave whose lanes are
+   busy starts its last items late: the dragon frame's last tile started ~9 ms after the queue
+   ran dry (profiles/r05r), and at ~20 dequeues per microsecond one atomic per refill is cheap. */
 constexpr uint32_t kBatch = 64;
 
 __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long long idle, uint32_t &bnext,
@@ -571,15 +574,16 @@ __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long 
     const uint32_t avail = bend - bnext;
     const uint32_t from_b = k < avail ? k : avail;
     uint32_t nb = 0;
+    const uint32_t take = batch ? batch : k - from_b;
     if (k > from_b) {
         const int leader = __ffsll((long long)idle) - 1;
-        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(counter, batch);
+        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(counter, take);
         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader));
     }
     const uint32_t item = rank < from_b ? bnext + rank : nb + (rank - from_b);
     if (k > from_b) {
         bnext = nb + (k - from_b);
-        bend = nb + batch;
+        bend = nb + take;
     } else {
         bnext += k;
     }
@@ -1794,8 +1798,12 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     unsigned long long pix_d = 0, pix_ab = 0, pix_c = 0, pix_it = 0;
     uint32_t pix_rt0 = 0; /* pixel start (s_memrealtime), RT_PIXEL_STATS diagnostics */
     uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
+    /* the wave's loop iterations (wave-uniform): a whole pixel's take and finish iterations go to
+       pixel_iter, the measured cost the view's next schedule sorts by (rt_sched_order_measured) */
+    uint32_t it_wave = 0;
 
     for (;;) {
+        ++it_wave;
         const unsigned long long t_d0 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
         for (;;) {
@@ -1804,7 +1812,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
             bool want_shadow = false, seg_done = false, sample_done = false;
             if (mode == M_CLOSEST) {
                 ++cnt[0];
-                if (COUNT) ++pix_q;
+                if (COUNT || RT_PLAIN_PIXEL_STATS) ++pix_q;
                 bool surface = true;
                 if (ts.best >= 0) {
                     const float qt = ts.best_t;
@@ -1852,7 +1860,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 }
             } else {
                 ++cnt[1];
-                if (COUNT) ++pix_q;
+                if (COUNT || RT_PLAIN_PIXEL_STATS) ++pix_q;
                 if (ts.best < 0) { /* unoccluded: rtcommon.h:93-101 */
                     const float cw = qd.x * hn.x + qd.y * hn.y + qd.z * hn.z;
                     if (cw > 0) {
@@ -1976,14 +1984,15 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
+                    if (a.pixel_iter) a.pixel_iter[a.W * a.Hl + yl * a.W + x] = it_wave;
                     mode = M_IDLE;
                     pclass = -1;
                     if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
                         uint32_t *ps = a.pixel_stats + 8 * ((size_t)yl * a.W + x);
                         ps[0] = pix_rt0;
                         ps[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                        ps[2] = COUNT ? (uint32_t)pix_q : 0u;
-                        ps[3] = COUNT ? (uint32_t)pix_steps : 0u;
+                        ps[2] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)pix_q : 0u;
+                        ps[3] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)pix_steps : 0u;
                         ps[4] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_d >> 6) : 0u;
                         ps[5] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_ab >> 6) : 0u;
                         ps[6] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_c >> 6) : 0u;
@@ -2026,7 +2035,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 64 items; bunny class 1024^2 at 1 spp 0.95 -> 0.55 ms, the dragon frame +-0.5 %) ---- */
         const unsigned long long idle = __ballot(mode == M_IDLE);
         if (idle) {
-            const uint32_t item = batch_take(a.work_counter, idle, bnext, bend);
+            const uint32_t item = batch_take(a.work_counter, idle, bnext, bend, a.take_exact ? 0u : kBatch);
             if (mode == M_IDLE) {
                 if (item >= n_tasks) {
                     mode = M_DONE;
@@ -2093,13 +2102,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
+                        if (a.pixel_iter) a.pixel_iter[yl * a.W + x] = it_wave;
                         if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats)
                             pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                        if (COUNT) {
-                            pix_t0 = wave_clock();
-                            pix_q = pix_steps = 0;
-                        }
-                        if (COUNT || RT_PLAIN_PIXEL_STATS) pix_d = pix_ab = pix_c = pix_it = 0;
+                        if (COUNT) pix_t0 = wave_clock();
+                        if (COUNT || RT_PLAIN_PIXEL_STATS) pix_q = pix_steps = pix_d = pix_ab = pix_c = pix_it = 0;
                         ACC_SET(0, 0.0f);
                         ACC_SET(1, 0.0f);
                         ACC_SET(2, 0.0f);
@@ -2233,6 +2240,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                             cnt[3] += tc.tests;
                             cnt[4] += tc.leaves;
                             pix_steps += tc.nodes + tc.leaves;
+                        } else if (RT_PLAIN_PIXEL_STATS) {
+                            ++pix_steps; /* (plain stats builds: trav_step calls) */
                         }
                     }
                     if (COUNT) ++cnt[5];

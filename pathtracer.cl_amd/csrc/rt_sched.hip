@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "rt_internal.h"
 
@@ -86,6 +87,36 @@ __global__ __launch_bounds__(256) void k_tile_cost(const uint32_t *__restrict__ 
         }
     }
     keys[t] = (float)((1.0 - kLptMax) * sum / 64.0 + kLptMax * mx);
+    idx[t] = t;
+}
+
+/* The same key from a rendered frame: a pixel's cost is the number of its wave's loop iterations
+   it was in flight (take to finish) — its queries, plus the stepping rounds its longer queries
+   span — which, unlike the probe's few rays, sees every sample's light and bounce directions (the
+   probe's shadow rays aim at the light centres) */
+__global__ __launch_bounds__(256) void k_tile_cost_measured(const uint32_t *__restrict__ iters, uint32_t W,
+                                                            uint32_t hl, float wmax, float *__restrict__ keys,
+                                                            uint32_t *__restrict__ idx)
+{
+    const uint32_t tx = (W + 7u) / 8u, n_t = tx * ((hl + 7u) / 8u);
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= n_t) return;
+    const size_t npx = (size_t)W * hl;
+    const uint32_t x0 = (t % tx) * 8u, y0 = (t / tx) * 8u;
+    double sum = 0.0, mx = 0.0;
+    for (uint32_t dy = 0; dy < 8u; ++dy) {
+        const uint32_t y = y0 + dy;
+        if (y >= hl) break;
+        for (uint32_t dx = 0; dx < 8u; ++dx) {
+            const uint32_t x = x0 + dx;
+            if (x >= W) break;
+            const size_t p = (size_t)y * W + x;
+            const double pc = (double)(iters[npx + p] - iters[p]) + 1.0;
+            sum += pc;
+            mx = mx > pc ? mx : pc;
+        }
+    }
+    keys[t] = (float)((1.0 - wmax) * sum / 64.0 + wmax * mx);
     idx[t] = t;
 }
 
@@ -203,6 +234,27 @@ int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_
     hipLaunchKernelGGL(k_tile_cost, dim3((n_t + 255u) / 256u), dim3(256), 0, st, flags, W, hl, pn2, n_lights,
                        max_depth, s.sums, s.keys, s.idx);
     if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    size_t bytes = s.tmp_bytes;
+    e = hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, bytes, s.keys, s.keys_sorted, s.idx, order, (int)n_t, 0,
+                                                     (int)(sizeof(float) * 8), st);
+    return (int)e;
+}
+
+int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W, uint32_t hl, uint32_t *order,
+                            void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+    const uint32_t n_t = ((W + 7u) / 8u) * ((hl + 7u) / 8u);
+    if (!n_t) return 0;
+    int r = reserve(s, n_t, W * hl);
+    if (r) return r;
+    /* the tile key's weight of its costliest pixel (RT_LPT_MAX: an A/B knob, default the probe key's) */
+    float wmax = (float)kLptMax;
+    if (const char *v = getenv("RT_LPT_MAX")) wmax = (float)atof(v);
+    hipLaunchKernelGGL(k_tile_cost_measured, dim3((n_t + 255u) / 256u), dim3(256), 0, st, iters, W, hl, wmax, s.keys,
+                       s.idx);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
     size_t bytes = s.tmp_bytes;
     e = hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, bytes, s.keys, s.keys_sorted, s.idx, order, (int)n_t, 0,
                                                      (int)(sizeof(float) * 8), st);

@@ -12,8 +12,8 @@ seconds each.
 
   * BASELINE configs[0]: the sphere scene at 512x512, 1 spp (main.cpp:123-127), from the
     context's own seeds (the padded 512x512 layout, RayTracerCL.cpp:229-232), three frames;
-  * configs[2]: the bunny-class mesh at 1024x1024, 1 spp, two frames (the second with the
-    camera-ray candidate lists of the unchanged view);
+  * configs[2]: the bunny-class mesh at 1024x1024, 1 spp, three frames (the later ones with the
+    camera-ray candidate lists of the unchanged view and its measured-cost schedule);
   * configs[3]: the dragon-class frame, 1920x1080, at sampleRate 4 (whole-pixel tasks);
   * one 8-way row-stripe tile of configs[3] at its own sampleRate 16 (256 spp): the sample-split
     path with its long chains, speculated mesh pixels and the repair pass;
@@ -117,8 +117,9 @@ def test_sphere_config1_512_vs_oracle(tracer, pt, oracle):
 
 def test_bunny_config_whole_frame_vs_bvh_oracle(tracer, pt, oracle):
     """BASELINE configs[2]: the bunny-class mesh (69,451 triangles) at 1024x1024, 1 spp, from the
-    context's own seeds: every pixel and seed slot of two progressive frames (the second reuses
-    the view's schedule and builds its candidate lists) equal to the oracle's."""
+    context's own seeds: every pixel and seed slot of three progressive frames (the second reuses
+    the view's schedule, re-sorted by the first frame's measured per-pixel costs, and builds its
+    candidate lists) equal to the oracle's."""
     sc = pt.scenes
     W = H = 1024
     Wp, Hp = sc.padded_dims(W, H)
@@ -136,10 +137,11 @@ def test_bunny_config_whole_frame_vs_bvh_oracle(tracer, pt, oracle):
     sd = sc.default_seeds(Wp, Hp)
     got = np.zeros(W * H * 4, np.float32)
     exp = np.zeros_like(got)
-    for p in range(2):
+    for p in range(3):
         rt.rayTrace(got, W, H, p, kernel=2)
         info = rt.renderInfo()
-        assert info["lists"] == (1 if p == 1 else 0), info
+        assert info["lists"] == (1 if p >= 1 else 0), info
+        assert info["schedule_measured"] == (1 if p >= 1 else 0), info
         c_or = oracle.render_tris(exp, cam, S, W, H, Wp, Hp, 1, 6, p, sd, verts, idx, bvh=bvh)
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
         cnt = rt.counters()

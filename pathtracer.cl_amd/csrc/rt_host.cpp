@@ -200,15 +200,17 @@ struct rt_ctx {
     bool schedule = true;
     bool schedule_rebuilt = false; /* the last triangle render recomputed the schedule */
 #ifndef RT_MEASURED_LPT
-#define RT_MEASURED_LPT 1
+#define RT_MEASURED_LPT 2
 #endif
-    /* measured-cost schedule (RT_MEASURED_LPT, env A/B knob): a view's first whole-pixel frame
-       records each pixel's wave iterations (pixel_iter), its next frame re-sorts the tiles by them */
+    /* measured-cost schedule (RT_MEASURED_LPT, env A/B knob: 0 off, 1 whole-pixel frames, 2 those
+       and sample-split tiles): a view's first frame records each pixel's wave iterations
+       (pixel_iter; a split tile's mesh chunk tasks), its next frame re-sorts the tiles by them */
     int measured_lpt = RT_MEASURED_LPT;
     uint32_t *d_pixel_iter = nullptr;
     size_t pixel_iter_px = 0;
     bool iter_recorded = false;  /* this view's costs are in d_pixel_iter */
     bool order_measured = false; /* d_order is sorted by them */
+    uint32_t iter_nch = 1;       /* chunk tasks per pixel of the recorded frame (1: whole pixels) */
     rt_render_info info = {};      /* rt_last_render_info */
     bool info_list_pending = false; /* info.list_records / list_pixels_tree still to be read */
     size_t info_list_px = 0;        /* pixels of the render the pending list counts belong to */
@@ -606,6 +608,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     if (n_box) {
         RtTriLaunch b = a;
         b.split_which = RT_SPLIT_BOX;
+        b.pixel_iter = nullptr; /* the measured costs: the mesh pixels' chunk tasks only */
         b.split_counter = a.split_counter + 32;
         b.work_counter = a.work_counter + 32;
         b.spill = a.spill + (size_t)std::max<int>(blocks, (int)a.split_seed_blocks) * RT_BLOCK * a.spill_cap;
@@ -671,6 +674,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
            tasks are single samples; any beyond take the per-pixel seeds */
         RtTriLaunch r = a;
         r.split_spec = 0;
+        r.pixel_iter = nullptr;
         r.split_which = RT_SPLIT_BOX;
         r.split_box = a.split_repair;
         r.split_n_box = 0;
@@ -752,7 +756,7 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         if (c->iter_recorded && !c->order_measured && c->d_order) {
             /* the view's second frame: its tiles by the first frame's measured costs (the probe's
                few rays miss where the samples' shadow rays are long: dragon frame) */
-            const int e = rt_sched_order_measured(c->sched, c->d_pixel_iter, W, hl, c->d_order, st);
+            const int e = rt_sched_order_measured(c->sched, c->d_pixel_iter, W, hl, c->iter_nch, c->d_order, st);
             if (e) return hip_fail(c, (hipError_t)e, "measured tile order");
             c->order_measured = true;
         }
@@ -890,7 +894,7 @@ try {
     if (const char *v = getenv("RT_SPLIT_MB")) c->split_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
-    if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v) != 0 ? 1 : 0;
+    if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);
@@ -1418,19 +1422,24 @@ try {
            (RT_TAKE_EXACT=0/1: an A/B knob) */
         a.take_exact = !a.split_chunks && c->sample_rate * c->sample_rate >= 16u ? 1u : 0u;
         if (const char *v = getenv("RT_TAKE_EXACT")) a.take_exact = atoi(v) != 0 && !a.split_chunks ? 1u : 0u;
-        /* a whole-pixel frame under the probe's order records its pixels' costs for the next frame */
+        /* a frame under the probe's order records its pixels' costs for the next frame (a sample-split
+           frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;
         bool record_iter = false;
-        if (a.tile_order && !a.split_chunks && c->measured_lpt && !c->order_measured && c->sample_rate > 0) {
-            const size_t npx_i = (size_t)W * hl;
-            if (c->pixel_iter_px < npx_i) {
+        if (a.tile_order && c->measured_lpt && !c->order_measured && c->sample_rate > 0 &&
+            (!a.split_chunks || c->measured_lpt > 1)) {
+            const uint32_t nch = a.split_chunks ? a.split_chunks : 1u;
+            const size_t n_i = (size_t)W * hl * nch;
+            if (c->pixel_iter_px < n_i) {
                 free_dev(c->d_pixel_iter);
                 c->d_pixel_iter = nullptr;
                 c->pixel_iter_px = 0;
-                HIPCHK(c, hipMalloc(&c->d_pixel_iter, 2 * npx_i * sizeof(uint32_t)));
-                c->pixel_iter_px = npx_i;
+                HIPCHK(c, hipMalloc(&c->d_pixel_iter, 2 * n_i * sizeof(uint32_t)));
+                c->pixel_iter_px = n_i;
             }
+            if (a.split_chunks) HIPCHK(c, hipMemsetAsync(c->d_pixel_iter, 0, 2 * n_i * sizeof(uint32_t), st));
             a.pixel_iter = c->d_pixel_iter;
+            c->iter_nch = nch;
             record_iter = true;
         }
         const double sched_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();

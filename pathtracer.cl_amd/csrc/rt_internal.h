@@ -218,8 +218,10 @@ struct RtTriLaunch {
     uint32_t split_seed_slot; /* RT_SPLIT_BOX: split_seed indexed by the item (the chain's slot in its list, minus
                                  split_item_base: its own buffer, a seed per split_fine samples), not by pixel */
     uint32_t split_item_base, split_item_cap; /* RT_SPLIT_BOX: the items split_box[base ...], at most cap (0: all) */
-    /* whole-pixel launches: per pixel the wave's loop iteration at its take ([p]) and at its finish
-       ([W x Hl + p]) — the measured cost a view's next schedule is sorted by (NULL: not recorded) */
+    /* per pixel the wave's loop iteration at its take ([p]) and at its finish ([W x Hl + p]) — the
+       measured cost a view's next schedule is sorted by; a sample-split launch's mesh chunk tasks:
+       per pixel and chunk, [p x split_chunks + c] and [W x Hl x split_chunks + ...] (NULL: not
+       recorded) */
     uint32_t *pixel_iter;
     uint32_t take_exact; /* k_tris: queue takes of exactly the idle lanes' items, no wave-private batch */
     /* RT_SPLIT_BOX, slotted seeds, one sample per task: per slot and sample (slot x spp + sample) the
@@ -300,9 +302,9 @@ int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_
                    uint32_t max_depth, uint32_t *order, void *stream);
 /* The LPT order again, from a rendered frame's measured costs instead of the probe: per pixel the
    wave iterations it was in flight (iters[p]: the iteration at its take, iters[npx + p]: at its
-   finish; k_tris records them) */
-int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W, uint32_t hl, uint32_t *order,
-                            void *stream);
+   finish; k_tris records them; nch > 1: per pixel nch chunk tasks, their iterations summed) */
+int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W, uint32_t hl, uint32_t nch,
+                            uint32_t *order, void *stream);
 /* row > 0 (speculated mesh pixels): the tile's width; the neighbours of a pixel whose probe missed
    the mesh are flagged too */
 int rt_sched_box_scan(RtSchedScratch &s, const uint32_t *flags, uint32_t npx, uint32_t pn2, uint32_t step_max,

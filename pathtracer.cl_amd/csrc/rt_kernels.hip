@@ -1947,6 +1947,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 dst[2] = col_z;
                 ++sample;
                 mode = (sample >= spp || sample % a.split_chunk == 0u) ? M_IDLE : M_NEWSAMPLE;
+                if (a.pixel_iter && mode == M_IDLE) /* the chunk task's finish */
+                    a.pixel_iter[(size_t)a.W * a.Hl * a.split_chunks + (size_t)(yl * a.W + x) * a.split_chunks +
+                                 (sample - 1u) / a.split_chunk] = it_wave;
                 if (sample >= spp && !a.split_seed_slot) /* the pixel's final seed, from its last chunk's own draws
                                                             (a slotted long chain's: from its seed pass) */
                     reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + a.split_nseed - 1u] =
@@ -2092,6 +2095,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         seed.y = sd.y;
                     }
                     if (SPLIT && take) {
+                        if (a.pixel_iter) /* a mesh pixel's chunk task: its take (pixel_iter, whole pixels: below) */
+                            a.pixel_iter[(size_t)(yl * a.W + x) * a.split_chunks + chunk] = it_wave;
                         sample = chunk * a.split_chunk;
                         if (a.split_hit_depth) hit_depth = a.split_hit_depth[(size_t)sbase * spp + sample];
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;

@@ -93,15 +93,16 @@ __global__ __launch_bounds__(256) void k_tile_cost(const uint32_t *__restrict__ 
 /* The same key from a rendered frame: a pixel's cost is the number of its wave's loop iterations
    it was in flight (take to finish) — its queries, plus the stepping rounds its longer queries
    span — which, unlike the probe's few rays, sees every sample's light and bounce directions (the
-   probe's shadow rays aim at the light centres) */
+   probe's shadow rays aim at the light centres); a sample-split frame's pixel: the sum over its nch
+   chunk tasks (0 for pixels that ran elsewhere: the long chains) */
 __global__ __launch_bounds__(256) void k_tile_cost_measured(const uint32_t *__restrict__ iters, uint32_t W,
-                                                            uint32_t hl, float wmax, float *__restrict__ keys,
-                                                            uint32_t *__restrict__ idx)
+                                                            uint32_t hl, uint32_t nch, float wmax,
+                                                            float *__restrict__ keys, uint32_t *__restrict__ idx)
 {
     const uint32_t tx = (W + 7u) / 8u, n_t = tx * ((hl + 7u) / 8u);
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= n_t) return;
-    const size_t npx = (size_t)W * hl;
+    const size_t n = (size_t)W * hl * nch;
     const uint32_t x0 = (t % tx) * 8u, y0 = (t / tx) * 8u;
     double sum = 0.0, mx = 0.0;
     for (uint32_t dy = 0; dy < 8u; ++dy) {
@@ -110,8 +111,9 @@ __global__ __launch_bounds__(256) void k_tile_cost_measured(const uint32_t *__re
         for (uint32_t dx = 0; dx < 8u; ++dx) {
             const uint32_t x = x0 + dx;
             if (x >= W) break;
-            const size_t p = (size_t)y * W + x;
-            const double pc = (double)(iters[npx + p] - iters[p]) + 1.0;
+            const size_t p = ((size_t)y * W + x) * nch;
+            double pc = 1.0;
+            for (uint32_t k = 0; k < nch; ++k) pc += (double)(iters[n + p + k] - iters[p + k]);
             sum += pc;
             mx = mx > pc ? mx : pc;
         }
@@ -240,8 +242,8 @@ int rt_sched_order(RtSchedScratch &s, const uint32_t *flags, uint32_t W, uint32_
     return (int)e;
 }
 
-int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W, uint32_t hl, uint32_t *order,
-                            void *stream)
+int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W, uint32_t hl, uint32_t nch,
+                            uint32_t *order, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
     const uint32_t n_t = ((W + 7u) / 8u) * ((hl + 7u) / 8u);
@@ -251,8 +253,8 @@ int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W
     /* the tile key's weight of its costliest pixel (RT_LPT_MAX: an A/B knob, default the probe key's) */
     float wmax = (float)kLptMax;
     if (const char *v = getenv("RT_LPT_MAX")) wmax = (float)atof(v);
-    hipLaunchKernelGGL(k_tile_cost_measured, dim3((n_t + 255u) / 256u), dim3(256), 0, st, iters, W, hl, wmax, s.keys,
-                       s.idx);
+    hipLaunchKernelGGL(k_tile_cost_measured, dim3((n_t + 255u) / 256u), dim3(256), 0, st, iters, W, hl, nch, wmax,
+                       s.keys, s.idx);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     size_t bytes = s.tmp_bytes;

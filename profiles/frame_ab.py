@@ -4,7 +4,7 @@ kernel time of --frames frames of the same view (the first --skip dropped: sched
 the frames' bits compared across builds.
 
     python profiles/frame_ab.py LABEL=path.so LABEL= LABEL=?K=V ... [--config bunny|dragon|spheres] [--rounds 3] [--frames 20]
-    (LABEL= with an empty path: the in-tree build; ?K=V&K2=V2 after the path: environment of that child)
+    (LABEL= with an empty path: the in-tree build; ?K=V+K2=V2 after the path: environment of that child)
 """
 import argparse
 import hashlib
@@ -71,7 +71,7 @@ def main():
             label, _, path = spec.partition("=")
             path, _, envs = path.partition("?")
             env = dict(os.environ)
-            for kv in filter(None, envs.split("&")):
+            for kv in filter(None, envs.split("+")):
                 k, _, v = kv.partition("=")
                 env[k] = v
             r = subprocess.run([sys.executable, "-u", __file__, "--child", "--lib", path, "--config", args.config,

@@ -4,8 +4,8 @@ round by round so clock drift hits them alike.  Each child renders every rank's 
 --reps) and reports the slowest; the parent prints per-build medians and checks that the builds'
 tiles are bit-identical.
 
-    python profiles/tile_ab.py LABEL=path.so LABEL= ... [--n 8] [--rounds 3] [--reps 2] [--frame]
-    (LABEL= with an empty path: the in-tree build)
+    python profiles/tile_ab.py LABEL=path.so LABEL= LABEL=?K=V ... [--n 8] [--rounds 3] [--reps 2] [--frame]
+    (LABEL= with an empty path: the in-tree build; ?K=V+K2=V2 after the path: that child's environment)
 """
 import argparse
 import hashlib
@@ -83,8 +83,10 @@ def main():
         order = args.libs if rnd % 2 == 0 else list(reversed(args.libs))
         for spec in order:
             label, _, path = spec.partition("=")
+            path, _, envs = path.partition("?")  # LABEL=path?K=V+K2=V2: that child's environment too
             cmd = [sys.executable, "-u", __file__, "--child", "--lib", path, "--n", str(args.n), "--reps",
-                   str(args.reps)] + (["--frame"] if args.frame else []) + sum((["--env", e] for e in args.env), [])
+                   str(args.reps)] + (["--frame"] if args.frame else []) + sum(
+                       (["--env", e] for e in args.env + [kv for kv in envs.split("+") if kv]), [])
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:
                 print(r.stderr[-2000:], file=sys.stderr)

@@ -209,7 +209,8 @@ struct rt_ctx {
     uint32_t *d_pixel_iter = nullptr;
     size_t pixel_iter_px = 0;
     bool iter_recorded = false;  /* this view's costs are in d_pixel_iter */
-    bool order_measured = false; /* d_order is sorted by them */
+    uint32_t order_measured = 0; /* d_order is sorted by them: how many times (re-sorts of this view) */
+    uint32_t measured_sorts = 1; /* re-sorts per view (RT_MEASURED_SORTS: A/B knob) */
     uint32_t iter_nch = 1;       /* chunk tasks per pixel of the recorded frame (1: whole pixels) */
     rt_render_info info = {};      /* rt_last_render_info */
     bool info_list_pending = false; /* info.list_records / list_pixels_tree still to be read */
@@ -753,18 +754,19 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     const uint32_t n_t = ((W + 7) / 8) * ((hl + 7) / 8);
     c->schedule_rebuilt = false;
     if (key == c->order_key) {
-        if (c->iter_recorded && !c->order_measured && c->d_order) {
+        if (c->iter_recorded && c->order_measured < c->measured_sorts && c->d_order) {
             /* the view's second frame: its tiles by the first frame's measured costs (the probe's
                few rays miss where the samples' shadow rays are long: dragon frame) */
             const int e = rt_sched_order_measured(c->sched, c->d_pixel_iter, W, hl, c->iter_nch, c->d_order, st);
             if (e) return hip_fail(c, (hipError_t)e, "measured tile order");
-            c->order_measured = true;
+            ++c->order_measured;
+            c->iter_recorded = false;
         }
         return RT_OK;
     }
     c->order_key.clear();
     c->iter_recorded = false;
-    c->order_measured = false;
+    c->order_measured = 0;
     c->n_split_box = 0;
     if (trav_kind(c) != RT_TRAV_BVH4Q || a.nodes != reinterpret_cast<const float *>(c->d_nodes4q)) {
         /* the probe walks the compressed tree with its spill layout: other traversal kinds
@@ -895,6 +897,7 @@ try {
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
+    c->measured_sorts = std::max(1u, env_u32("RT_MEASURED_SORTS", 1));
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);
@@ -1426,7 +1429,7 @@ try {
            frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;
         bool record_iter = false;
-        if (a.tile_order && c->measured_lpt && !c->order_measured && c->sample_rate > 0 &&
+        if (a.tile_order && c->measured_lpt && c->order_measured < c->measured_sorts && c->sample_rate > 0 &&
             (!a.split_chunks || c->measured_lpt > 1)) {
             const uint32_t nch = a.split_chunks ? a.split_chunks : 1u;
             const size_t n_i = (size_t)W * hl * nch;

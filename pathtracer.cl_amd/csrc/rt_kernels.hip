@@ -1702,6 +1702,9 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         the iteration (the reference loop, wave-uniform).
    SPLIT: a queue item is one chunk of a pixel's samples, started from the seed the seed pass
    (k_split_seeds) stored for it; each sample's radiance is stored for k_split_finish. */
+#ifndef RT_LPT_STEPS
+#define RT_LPT_STEPS 0 /* A/B: pixel_iter records a pixel's traversal steps instead of its iterations in flight */
+#endif
 template <int TRAV, bool COUNT, bool SPLIT = false>
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
@@ -1949,7 +1952,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 mode = (sample >= spp || sample % a.split_chunk == 0u) ? M_IDLE : M_NEWSAMPLE;
                 if (a.pixel_iter && mode == M_IDLE) /* the chunk task's finish */
                     a.pixel_iter[(size_t)a.W * a.Hl * a.split_chunks + (size_t)(yl * a.W + x) * a.split_chunks +
-                                 (sample - 1u) / a.split_chunk] = it_wave;
+                                 (sample - 1u) / a.split_chunk] = RT_LPT_STEPS ? (uint32_t)pix_steps : it_wave;
                 if (sample >= spp && !a.split_seed_slot) /* the pixel's final seed, from its last chunk's own draws
                                                             (a slotted long chain's: from its seed pass) */
                     reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + a.split_nseed - 1u] =
@@ -1987,7 +1990,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
-                    if (a.pixel_iter) a.pixel_iter[a.W * a.Hl + yl * a.W + x] = it_wave;
+                    if (a.pixel_iter) a.pixel_iter[a.W * a.Hl + yl * a.W + x] = RT_LPT_STEPS ? (uint32_t)pix_steps : it_wave;
                     mode = M_IDLE;
                     pclass = -1;
                     if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
@@ -2096,22 +2099,22 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                     if (SPLIT && take) {
                         if (a.pixel_iter) /* a mesh pixel's chunk task: its take (pixel_iter, whole pixels: below) */
-                            a.pixel_iter[(size_t)(yl * a.W + x) * a.split_chunks + chunk] = it_wave;
+                            a.pixel_iter[(size_t)(yl * a.W + x) * a.split_chunks + chunk] = RT_LPT_STEPS ? 0u : it_wave;
                         sample = chunk * a.split_chunk;
                         if (a.split_hit_depth) hit_depth = a.split_hit_depth[(size_t)sbase * spp + sample];
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
                         mode = M_NEWSAMPLE;
-                        if (COUNT) pix_q = pix_steps = 0;
+                        if (COUNT || RT_LPT_STEPS) pix_q = pix_steps = 0;
                     } else if (take) {
                         const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
-                        if (a.pixel_iter) a.pixel_iter[yl * a.W + x] = it_wave;
+                        if (a.pixel_iter) a.pixel_iter[yl * a.W + x] = RT_LPT_STEPS ? 0u : it_wave;
                         if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats)
                             pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         if (COUNT) pix_t0 = wave_clock();
-                        if (COUNT || RT_PLAIN_PIXEL_STATS) pix_q = pix_steps = pix_d = pix_ab = pix_c = pix_it = 0;
+                        if (COUNT || RT_PLAIN_PIXEL_STATS || RT_LPT_STEPS) pix_q = pix_steps = pix_d = pix_ab = pix_c = pix_it = 0;
                         ACC_SET(0, 0.0f);
                         ACC_SET(1, 0.0f);
                         ACC_SET(2, 0.0f);
@@ -2245,8 +2248,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                             cnt[3] += tc.tests;
                             cnt[4] += tc.leaves;
                             pix_steps += tc.nodes + tc.leaves;
-                        } else if (RT_PLAIN_PIXEL_STATS) {
-                            ++pix_steps; /* (plain stats builds: trav_step calls) */
+                        } else if (RT_PLAIN_PIXEL_STATS || RT_LPT_STEPS) {
+                            ++pix_steps; /* (plain stats builds, RT_LPT_STEPS: trav_step calls) */
                         }
                     }
                     if (COUNT) ++cnt[5];

@@ -81,11 +81,18 @@ uint32_t probe_n(uint32_t sample_rate) { return sample_rate >= 2 ? kProbeN : 1u;
 #define RT_FETCH_K 24
 #endif
 constexpr size_t kCounterBytes = RT_COUNTER_WORDS * sizeof(unsigned long long);
+/* the queue cursors after the counters: the main launch's RT_QHEADS heads RT_QSTRIDE words apart (mq_take),
+   then the long chains' and the repairs' one-word cursors on lines of their own */
+constexpr size_t kWorkWords = (size_t)RT_QSTRIDE * RT_QHEADS + 64;
+constexpr uint32_t kWorkBox = RT_QSTRIDE * RT_QHEADS, kWorkRepair = RT_QSTRIDE * RT_QHEADS + 32;
 #ifndef RT_LONG_FINE
 #define RT_LONG_FINE 1 /* samples per stored seed (and per chunk task) of the subtree-parallel long chains */
 #endif
 #ifndef RT_REPAIR_WIDTH
 #define RT_REPAIR_WIDTH 64u /* lanes per repaired chain: its hit samples in runs of 63 */
+#endif
+#ifndef RT_QUEUE_BATCH
+#define RT_QUEUE_BATCH 64
 #endif
 #ifndef RT_REPAIR_SLOTS
 #define RT_REPAIR_SLOTS 4096u /* repaired pixels with per-sample seeds by slot (8.4 MB at 256 spp) */
@@ -209,8 +216,8 @@ struct rt_ctx {
     uint32_t *d_pixel_iter = nullptr;
     size_t pixel_iter_px = 0;
     bool iter_recorded = false;  /* this view's costs are in d_pixel_iter */
-    uint32_t order_measured = 0; /* d_order is sorted by them: how many times (re-sorts of this view) */
-    uint32_t measured_sorts = 1; /* re-sorts per view (RT_MEASURED_SORTS: A/B knob) */
+    bool order_measured = false; /* d_order is sorted by them (once per view: re-sorting again from
+                                    the re-sorted frame's costs measured slower, profiles/r05aa) */
     uint32_t iter_nch = 1;       /* chunk tasks per pixel of the recorded frame (1: whole pixels) */
     rt_render_info info = {};      /* rt_last_render_info */
     bool info_list_pending = false; /* info.list_records / list_pixels_tree still to be read */
@@ -611,7 +618,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         b.split_which = RT_SPLIT_BOX;
         b.pixel_iter = nullptr; /* the measured costs: the mesh pixels' chunk tasks only */
         b.split_counter = a.split_counter + 32;
-        b.work_counter = a.work_counter + 32;
+        b.work_counter = a.work_counter + kWorkBox;
         b.spill = a.spill + (size_t)std::max<int>(blocks, (int)a.split_seed_blocks) * RT_BLOCK * a.spill_cap;
         b.split_gpw = c->split_gpw;
         b.split_seed_blocks = (uint32_t)std::max(1, c->split_box_grid);
@@ -681,7 +688,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_n_box = 0;
         r.split_n_dev = reinterpret_cast<const uint32_t *>(a.counters + RT_CNT_REPAIR);
         r.split_counter = a.split_counter + 48;
-        r.work_counter = a.work_counter + 48;
+        r.work_counter = a.work_counter + kWorkRepair;
         r.split_gpw = c->split_gpw;
         r.split_seed_blocks = 16u * RT_REPAIR_WIDTH / 16u; /* up to 4 x 16 chains at once at any width */
         r.split_chunk = a.split_fine;
@@ -754,19 +761,18 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     const uint32_t n_t = ((W + 7) / 8) * ((hl + 7) / 8);
     c->schedule_rebuilt = false;
     if (key == c->order_key) {
-        if (c->iter_recorded && c->order_measured < c->measured_sorts && c->d_order) {
+        if (c->iter_recorded && !c->order_measured && c->d_order) {
             /* the view's second frame: its tiles by the first frame's measured costs (the probe's
                few rays miss where the samples' shadow rays are long: dragon frame) */
             const int e = rt_sched_order_measured(c->sched, c->d_pixel_iter, W, hl, c->iter_nch, c->d_order, st);
             if (e) return hip_fail(c, (hipError_t)e, "measured tile order");
-            ++c->order_measured;
-            c->iter_recorded = false;
+            c->order_measured = true;
         }
         return RT_OK;
     }
     c->order_key.clear();
     c->iter_recorded = false;
-    c->order_measured = 0;
+    c->order_measured = false;
     c->n_split_box = 0;
     if (trav_kind(c) != RT_TRAV_BVH4Q || a.nodes != reinterpret_cast<const float *>(c->d_nodes4q)) {
         /* the probe walks the compressed tree with its spill layout: other traversal kinds
@@ -897,7 +903,6 @@ try {
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
-    c->measured_sorts = std::max(1u, env_u32("RT_MEASURED_SORTS", 1));
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);
@@ -911,7 +916,7 @@ try {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evm) != hipSuccess ||
-        hipMalloc(&c->d_counters, kCounterBytes + 64 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_counters, kCounterBytes + kWorkWords * sizeof(uint32_t)) != hipSuccess ||
         hipHostMalloc(&c->h_counters, kCounterBytes + sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_HIP;
@@ -1283,7 +1288,7 @@ try {
         if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
     }
     /* the counters, the guard word and the queue cursors: one memset */
-    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + 64 * sizeof(uint32_t), st));
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;
     int e = 0;
@@ -1425,11 +1430,16 @@ try {
            (RT_TAKE_EXACT=0/1: an A/B knob) */
         a.take_exact = !a.split_chunks && c->sample_rate * c->sample_rate >= 16u ? 1u : 0u;
         if (const char *v = getenv("RT_TAKE_EXACT")) a.take_exact = atoi(v) != 0 && !a.split_chunks ? 1u : 0u;
+        /* short whole-pixel frames take from the multi-head queue (mq_take) in batches of
+           RT_QUEUE_BATCH items (0: one head; bunny class 0.519 -> 0.473 ms, profiles/r05ac); the
+           split tiles' chunk tasks keep one head (their tiles' chunk layers spread over the heads
+           measured 15.6 -> 16.3 ms) */
+        a.queue_batch = a.take_exact || a.split_chunks ? 0u : std::min(64u, env_u32("RT_QUEUE_BATCH", RT_QUEUE_BATCH));
         /* a frame under the probe's order records its pixels' costs for the next frame (a sample-split
            frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;
         bool record_iter = false;
-        if (a.tile_order && c->measured_lpt && c->order_measured < c->measured_sorts && c->sample_rate > 0 &&
+        if (a.tile_order && c->measured_lpt && !c->order_measured && c->sample_rate > 0 &&
             (!a.split_chunks || c->measured_lpt > 1)) {
             const uint32_t nch = a.split_chunks ? a.split_chunks : 1u;
             const size_t n_i = (size_t)W * hl * nch;

@@ -130,6 +130,12 @@ int rt_build_bvh_gpu(const float *verts, uint32_t n_verts, const int32_t *idx, u
 bool rt_validate_mesh(const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris, std::string &err);
 
 /* ---- kernel launchers (rt_kernels.hip) ---- */
+#ifndef RT_QHEADS
+#define RT_QHEADS 8 /* heads of the multi-head pixel queue (k_tris mq_take) */
+#endif
+#ifndef RT_QSTRIDE
+#define RT_QSTRIDE 1024 /* words between the heads (4 KB: apart in the memory channels the device-scope atomics go to) */
+#endif
 struct RtTriLaunch {
     float *out;
     uint32_t *seeds;
@@ -224,6 +230,8 @@ struct RtTriLaunch {
        recorded) */
     uint32_t *pixel_iter;
     uint32_t take_exact; /* k_tris: queue takes of exactly the idle lanes' items, no wave-private batch */
+    uint32_t queue_batch; /* k_tris: items per take from the multi-head queue (mq_take; work_counter then points
+                             at RT_QHEADS heads RT_QSTRIDE words apart); 0: one head (batch_take) */
     /* RT_SPLIT_BOX, slotted seeds, one sample per task: per slot and sample (slot x spp + sample) the
        depth of the segment whose closest-hit query meets the mesh, 0xff for a path that meets only
        the box — written by the subtree-parallel seed pass, which answers that very question for

@@ -590,6 +590,50 @@ __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long 
     return item;
 }
 
+/* Multi-head queue (RT_QHEADS heads, RT_QSTRIDE words apart): a launch's items are 64-item groups
+   (an 8 x 8 tile, or one chunk layer of a tile); head h owns the groups g = h, h + RT_QHEADS, ...
+   (in queue order), and a wave takes `batch` items of a head at a time, starting at the head of
+   its block (blockIdx.x mod RT_QHEADS) and moving on to the next head when one is drained.  More
+   heads take more dequeues per microsecond than one (a single head word saturates near 88), so
+   the batches can be small enough that no wave holds back many of the queue's last items while
+   its lanes are busy.  The wave's state is one word `qs`: the head of its batch [bnext, bend)
+   (local indices, bits 0-3), the head it takes from next (bits 4-7), and how many heads in a row
+   it found drained (bits 8-11: RT_QHEADS of them, the queue is empty).  At most one atomic per
+   take; a lane whose take found a drained head stays idle and takes again in the next iteration.
+   Returns the lane's item or ~0u.  Wave-uniform, like batch_take. */
+__device__ __forceinline__ uint32_t mq_take(uint32_t *heads, uint32_t n_tasks, unsigned long long idle, uint32_t &bnext,
+                                            uint32_t &bend, uint32_t &qs, uint32_t batch)
+{
+    constexpr uint32_t Q = RT_QHEADS;
+    const uint32_t k = (uint32_t)__popcll(idle);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+    const uint32_t avail = bend - bnext;
+    const uint32_t from_b = k < avail ? k : avail;
+    const uint32_t bq = qs & 15u, hq = (qs >> 4) & 15u;
+    /* local index l of head q -> queue item: group (l / 64) x Q + q, offset l mod 64 */
+    uint32_t item = rank < from_b ? (((bnext + rank) >> 6) * Q + bq) * 64u + ((bnext + rank) & 63u) : ~0u;
+    bnext += from_b;
+    if (k > from_b && (qs >> 8) < Q) {
+        const int leader = __ffsll((long long)idle) - 1;
+        uint32_t nb = 0;
+        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(heads + RT_QSTRIDE * hq, batch);
+        nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader));
+        const uint32_t n_groups = n_tasks >> 6;
+        const uint32_t n_local = (n_groups > hq ? (n_groups - hq + Q - 1u) / Q : 0u) * 64u;
+        if (nb < n_local) {
+            const uint32_t r = rank - from_b;
+            bend = nb + batch < n_local ? nb + batch : n_local;
+            if (rank >= from_b && nb + r < bend) item = (((nb + r) >> 6) * Q + hq) * 64u + ((nb + r) & 63u);
+            const uint32_t need = k - from_b;
+            bnext = nb + (need < bend - nb ? need : bend - nb);
+            qs = hq | hq << 4; /* the batch's head, the same head next, no drained heads */
+        } else { /* drained: the next head, one more drained in a row */
+            qs = (qs & 15u) | ((hq + 1u) % Q) << 4 | ((qs >> 8) + 1u) << 8;
+        }
+    }
+    return item;
+}
+
 /* RT_SPLIT_BOX launches: the number of items of split_box[split_item_base ...] this launch takes
    (the list's length from the device when split_n_dev is set), at most split_item_cap */
 __device__ __forceinline__ uint32_t box_items(const RtTriLaunch &a)
@@ -1703,9 +1747,12 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
    SPLIT: a queue item is one chunk of a pixel's samples, started from the seed the seed pass
    (k_split_seeds) stored for it; each sample's radiance is stored for k_split_finish. */
 #ifndef RT_LPT_STEPS
-#define RT_LPT_STEPS 0 /* A/B: pixel_iter records a pixel's traversal steps instead of its iterations in flight */
+#define RT_LPT_STEPS 1 /* pixel_iter records a pixel's traversal steps (0: its wave iterations in flight) */
 #endif
-template <int TRAV, bool COUNT, bool SPLIT = false>
+#ifndef RT_LPT_QW
+#define RT_LPT_QW 0 /* A/B: the recorded cost's weight of a completed query, in steps */
+#endif
+template <int TRAV, bool COUNT, bool SPLIT = false, bool MQ = false> /* MQ: the multi-head queue (mq_take) */
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
     constexpr bool RESUME = TRAV == RT_TRAV_BVH4 || TRAV == RT_TRAV_BVH4Q;
@@ -1801,6 +1848,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     unsigned long long pix_d = 0, pix_ab = 0, pix_c = 0, pix_it = 0;
     uint32_t pix_rt0 = 0; /* pixel start (s_memrealtime), RT_PIXEL_STATS diagnostics */
     uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
+    /* the multi-head queue (mq_take: launches of 64-item groups with batched takes) */
+    const bool multi_q = MQ; /* (launched so only with queue_batch > 0, never for exact takes or long chains) */
+    uint32_t qs = (blockIdx.x % RT_QHEADS) << 4;
     /* the wave's loop iterations (wave-uniform): a whole pixel's take and finish iterations go to
        pixel_iter, the measured cost the view's next schedule sorts by (rt_sched_order_measured) */
     uint32_t it_wave = 0;
@@ -1813,6 +1863,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         if (fin) {
             fin = false;
             bool want_shadow = false, seg_done = false, sample_done = false;
+            if (RT_LPT_STEPS && RT_LPT_QW) pix_steps += RT_LPT_QW;
             if (mode == M_CLOSEST) {
                 ++cnt[0];
                 if (COUNT || RT_PLAIN_PIXEL_STATS) ++pix_q;
@@ -2041,9 +2092,12 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 64 items; bunny class 1024^2 at 1 spp 0.95 -> 0.55 ms, the dragon frame +-0.5 %) ---- */
         const unsigned long long idle = __ballot(mode == M_IDLE);
         if (idle) {
-            const uint32_t item = batch_take(a.work_counter, idle, bnext, bend, a.take_exact ? 0u : kBatch);
+            const uint32_t item = multi_q ? mq_take(a.work_counter, n_tasks, idle, bnext, bend, qs, a.queue_batch)
+                                          : batch_take(a.work_counter, idle, bnext, bend, a.take_exact ? 0u : kBatch);
             if (mode == M_IDLE) {
-                if (item >= n_tasks) {
+                if (multi_q && item == ~0u) {
+                    if ((qs >> 8) >= RT_QHEADS) mode = M_DONE; /* else: idle, takes again next iteration */
+                } else if (item >= n_tasks) {
                     mode = M_DONE;
                 } else {
                     /* 8 x 8 pixel tiles, row-major over the (local) frame; SPLIT over tiles: a
@@ -3022,15 +3076,20 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
 {
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)grid_blocks), block(RT_BLOCK);
+    /* the multi-head queue: its own instantiations (its take costs the others registers) */
+    const bool mq = a.queue_batch && !a.take_exact && trav == RT_TRAV_BVH4Q && a.split_which != RT_SPLIT_BOX;
 #define RT_LAUNCH_TRIS(T, S)                                                                                           \
     do {                                                                                                               \
-        if (count) hipLaunchKernelGGL((k_tris<T, true, S>), grid, block, 0, st, a);                                    \
+        if (mq && count) hipLaunchKernelGGL((k_tris<RT_TRAV_BVH4Q, true, S, true>), grid, block, 0, st, a);            \
+        else if (mq) hipLaunchKernelGGL((k_tris<RT_TRAV_BVH4Q, false, S, true>), grid, block, 0, st, a);               \
+        else if (count) hipLaunchKernelGGL((k_tris<T, true, S>), grid, block, 0, st, a);                               \
         else hipLaunchKernelGGL((k_tris<T, false, S>), grid, block, 0, st, a);                                         \
     } while (0)
     /* the sample-split form only where it is used (its code costs a full frame 1 %) */
     if (trav == RT_TRAV_BVH4Q && a.split_chunks) {
-        /* the chunk tasks (queue cursor a.work_counter, reset here) */
-        const hipError_t e = hipMemsetAsync(a.work_counter, 0, sizeof(uint32_t), st);
+        /* the chunk tasks (queue cursor a.work_counter — or the multi-head queue's heads — reset here) */
+        const size_t words = mq ? (size_t)RT_QSTRIDE * RT_QHEADS : 1u;
+        const hipError_t e = hipMemsetAsync(a.work_counter, 0, words * sizeof(uint32_t), st);
         if (e != hipSuccess) return (int)e;
         RT_LAUNCH_TRIS(RT_TRAV_BVH4Q, true);
     } else if (trav == RT_TRAV_LINEAR) RT_LAUNCH_TRIS(RT_TRAV_LINEAR, false);

@@ -343,8 +343,8 @@ def main():
     print(f"warmup kernel ms: {[round(x, 2) for x in warm_ms]}", file=sys.stderr)
 
     kernel_ms, split_ms = [], []
-    # One GPU, whole frames: the K frames are enqueued back to back on one stream (the library's
-    # rt_render_async) and the host never waits between them, so a short frame's launch and host
+    # One GPU, whole frames: the K frames are enqueued back to back on the library's stream
+    # (rt_render_async) and the host never waits between them, so a short frame's launch and host
     # work overlap the previous frame's kernels (bunny class: ~40 us of a 0.5-ms frame); each
     # frame is the same full render, its seeds carried on the device from the one before. The
     # per-frame kernel times for the roofline come from a synchronous pass after the timed one.
@@ -352,7 +352,6 @@ def main():
     rays_frame_fixed = None
     if pipelined:
         rays_frame_fixed = step()  # one more warm frame; its count is every frame's (same view)
-        s_frames = torch.cuda.Stream(device=f"cuda:{device}")
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -361,7 +360,7 @@ def main():
     for _ in range(args.steps):
         if pipelined:
             pnum = frame_no[0] if progressive else 0
-            rt.rayTrace(out, W, H, pnum, kernel=kernel, tile=tile, stream=s_frames.cuda_stream, sync=False)
+            rt.rayTrace(out, W, H, pnum, kernel=kernel, tile=tile, sync=False)  # the library's own stream
             frame_no[0] += 1
             rays += rays_frame_fixed
         else:

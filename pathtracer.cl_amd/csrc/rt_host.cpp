@@ -219,6 +219,8 @@ struct rt_ctx {
     bool order_measured = false; /* d_order is sorted by them (once per view: re-sorting again from
                                     the re-sorted frame's costs measured slower, profiles/r05aa) */
     uint32_t iter_nch = 1;       /* chunk tasks per pixel of the recorded frame (1: whole pixels) */
+    float mesh_lo[3] = {0, 0, 0}, mesh_hi[3] = {0, 0, 0}; /* the mesh's padded bounds (mesh_bounds) */
+    bool mesh_bounds_ok = false;
     rt_render_info info = {};      /* rt_last_render_info */
     bool info_list_pending = false; /* info.list_records / list_pixels_tree still to be read */
     size_t info_list_px = 0;        /* pixels of the render the pending list counts belong to */
@@ -1000,11 +1002,43 @@ try {
     return RT_OK;
 } RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
+/* The mesh's bounds, padded: the box of the vertices the triangles use, grown by 1e-3 of its
+   extent + 1e-4 — every point of every triangle (and every point the kernel's triangle test can
+   accept: its error is orders of magnitude below the pad) lies at least the pad inside, so a ray
+   segment that misses the padded box meets no triangle (k_tris answers such box-path queries
+   without a traversal). False when the vertices are not finite (validation reports it). */
+static bool mesh_bounds(const float *verts, const int32_t *idx, uint32_t n_tris, float lo[3], float hi[3])
+{
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = INFINITY;
+        hi[k] = -INFINITY;
+    }
+    for (uint64_t i = 0; i < 3ull * n_tris; ++i) {
+        const float *v = verts + 3ull * (uint32_t)idx[i];
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], v[k]);
+            hi[k] = std::max(hi[k], v[k]);
+        }
+    }
+    float ext = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+        if (!std::isfinite(lo[k]) || !std::isfinite(hi[k])) return false;
+        ext = std::max(ext, hi[k] - lo[k]);
+    }
+    const float pad = 1e-3f * ext + 1e-4f;
+    for (int k = 0; k < 3; ++k) {
+        lo[k] -= pad;
+        hi[k] += pad;
+    }
+    return true;
+}
+
 int rt_set_mesh(rt_ctx *c, const float *verts, uint32_t n_verts, const int32_t *idx, uint32_t n_tris)
 try {
     if (!c || !verts || !idx || !n_verts || !n_tris) return fail(c, RT_ERR_ARG, "empty mesh");
     HIPCHK(c, hipSetDevice(c->device));
     std::string err;
+    c->mesh_bounds_ok = false;
     if (c->builder == RT_BUILD_GPU) {
         if (!rt_validate_mesh(verts, n_verts, idx, n_tris, err)) return fail(c, RT_ERR_ARG, err);
         free_dev(c->d_nodes4);
@@ -1033,6 +1067,7 @@ try {
         c->bvh.build_seconds = g.build_seconds;
         c->bvh.n_hit = n_tris; /* the GPU build keeps every triangle */
         c->mesh_builder = RT_BUILD_GPU;
+        c->mesh_bounds_ok = mesh_bounds(verts, idx, n_tris, c->mesh_lo, c->mesh_hi);
         return RT_OK;
     }
     RtBvh b;
@@ -1066,6 +1101,7 @@ try {
     c->bvh.stack4 = b.stack4;
     c->bvh.build_seconds = b.build_seconds;
     c->bvh.n_hit = b.n_hit;
+    c->mesh_bounds_ok = mesh_bounds(verts, idx, n_tris, c->mesh_lo, c->mesh_hi);
     return RT_OK;
 } RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
 
@@ -1329,8 +1365,9 @@ try {
            3 of the 5 blocks per CU: its time is then its costliest pixels' serial paths, which step
            faster on less crowded SIMDs (bunny class 0.54 -> 0.46 ms at 768 of 1280 blocks; the
            dragon frame at 1024 blocks 96.7 -> 101.2 ms: profiles/r04l, r04m) */
-        if ((uint64_t)W * hl * c->sample_rate * c->sample_rate < kShortFrameSamplesPerLane * (uint64_t)blocks * RT_BLOCK)
-            blocks = std::max(1, blocks * kShortFrameBlocksPerCU / RT_TRIS_WAVES);
+        const bool short_frame =
+            (uint64_t)W * hl * c->sample_rate * c->sample_rate < kShortFrameSamplesPerLane * (uint64_t)blocks * RT_BLOCK;
+        if (short_frame) blocks = std::max(1, blocks * kShortFrameBlocksPerCU / RT_TRIS_WAVES);
         if (const uint32_t gb = env_u32("RTMI_GRID_BLOCKS", 0)) blocks = std::min(blocks, (int)gb);
         if (trav == RT_TRAV_BVH4Q) {
             r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
@@ -1430,6 +1467,15 @@ try {
            (RT_TAKE_EXACT=0/1: an A/B knob) */
         a.take_exact = !a.split_chunks && c->sample_rate * c->sample_rate >= 16u ? 1u : 0u;
         if (const char *v = getenv("RT_TAKE_EXACT")) a.take_exact = atoi(v) != 0 && !a.split_chunks ? 1u : 0u;
+        /* short frames: box-path queries whose segment misses the mesh's padded bounds are answered
+           without a traversal (bunny class 0.469 -> 0.457 ms; the dragon frame measured 87.1 -> 88.4
+           ms with it, profiles/r05ah: off there). RT_MESH_BOUNDS=0/1 forces it off / on */
+        a.mesh_bounds = c->mesh_bounds_ok && short_frame ? 1u : 0u;
+        if (const char *v = getenv("RT_MESH_BOUNDS")) a.mesh_bounds = c->mesh_bounds_ok && atoi(v) != 0 ? 1u : 0u;
+        for (int k = 0; k < 3; ++k) {
+            a.mesh_lo[k] = c->mesh_lo[k];
+            a.mesh_hi[k] = c->mesh_hi[k];
+        }
         /* short whole-pixel frames take from the multi-head queue (mq_take) in batches of
            RT_QUEUE_BATCH items (0: one head; bunny class 0.519 -> 0.473 ms, profiles/r05ac); the
            split tiles' chunk tasks keep one head (their tiles' chunk layers spread over the heads

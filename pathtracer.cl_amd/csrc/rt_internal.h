@@ -230,6 +230,11 @@ struct RtTriLaunch {
        recorded) */
     uint32_t *pixel_iter;
     uint32_t take_exact; /* k_tris: queue takes of exactly the idle lanes' items, no wave-private batch */
+    /* the mesh's bounds padded by 1e-3 of its extent (rt_host.cpp mesh_bounds): a box-path query
+       (a bounce off the box or a shadow ray leaving it) whose segment misses them meets no
+       triangle and is answered in the path advance, without a traversal (0: not used) */
+    uint32_t mesh_bounds;
+    float mesh_lo[3], mesh_hi[3];
     uint32_t queue_batch; /* k_tris: items per take from the multi-head queue (mq_take; work_counter then points
                              at RT_QHEADS heads RT_QSTRIDE words apart); 0: one head (batch_take) */
     /* RT_SPLIT_BOX, slotted seeds, one sample per task: per slot and sample (slot x spp + sample) the

@@ -1232,6 +1232,24 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
    there; a fresh seed at or above M gets there within 2 steps, M itself is a fixed point), so
    k draws are one multiplication by A^k mod M (`mul`, from the host); a^-1 = 2^16 mod M undoes
    the canonicalising steps.  Small k: the steps themselves. */
+/* Does the segment o + t d, tmin <= t <= tmax, miss the box [lo, hi]?  Slab test with the hardware
+   reciprocal; the box is the mesh's bounds padded far beyond the test's rounding (mesh_bounds), so
+   a segment reported missing meets no triangle.  A zero direction component on a slab plane gives
+   0 x inf = NaN, which min/max drop (a ray in that plane lies outside the triangles' padded box
+   anyway). */
+__device__ __forceinline__ bool segment_misses_box(V3 o, V3 d, float tmin, float tmax, const float *lo, const float *hi)
+{
+    const float ix = __builtin_amdgcn_rcpf(d.x), iy = __builtin_amdgcn_rcpf(d.y), iz = __builtin_amdgcn_rcpf(d.z);
+    const float x1 = (lo[0] - o.x) * ix, x2 = (hi[0] - o.x) * ix;
+    const float y1 = (lo[1] - o.y) * iy, y2 = (hi[1] - o.y) * iy;
+    const float z1 = (lo[2] - o.z) * iz, z2 = (hi[2] - o.z) * iz;
+    const float tn = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x1, x2), __builtin_fminf(y1, y2)),
+                                     __builtin_fmaxf(__builtin_fminf(z1, z2), tmin));
+    const float tf = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x1, x2), __builtin_fmaxf(y1, y2)),
+                                     __builtin_fminf(__builtin_fmaxf(z1, z2), tmax));
+    return tn > tf;
+}
+
 template <uint32_t A>
 __device__ __forceinline__ uint32_t mwc_jump(uint32_t x, uint32_t k, uint32_t mul)
 {
@@ -1752,6 +1770,11 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
 #ifndef RT_LPT_QW
 #define RT_LPT_QW 0 /* A/B: the recorded cost's weight of a completed query, in steps */
 #endif
+#ifndef RT_OFF_MESH_REDO
+#define RT_OFF_MESH_REDO 1 /* path-advance passes that may answer an off-mesh box-path query in place (0 / 1 / all:
+                              bunny class 0.484 / 0.457 / 0.594 ms, profiles/r05ag-r05ah); later ones at the
+                              stepping round's start, without a step */
+#endif
 template <int TRAV, bool COUNT, bool SPLIT = false, bool MQ = false> /* MQ: the multi-head queue (mq_take) */
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
@@ -1859,7 +1882,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         ++it_wave;
         const unsigned long long t_d0 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
-        for (;;) {
+        for (int redo_pass = 0;; ++redo_pass) {
         if (fin) {
             fin = false;
             bool want_shadow = false, seg_done = false, sample_done = false;
@@ -2073,7 +2096,13 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         const bool need_trav = stmax > RT_SMALL_F && cw_q > 0;
         /* likewise a long chain's box segment (split_hit_depth): no triangle accepted */
         const bool known_miss = SPLIT && mode == M_CLOSEST && !fin && !running && (int)depth < hit_depth;
-        const bool redo = (issued && !need_trav) || known_miss;
+        /* and a box-path query (a bounce off the box, or a shadow ray leaving it) whose segment misses
+           the mesh's padded bounds: no triangle accepted, whatever the traversal would visit */
+        bool off_mesh = false;
+        if (redo_pass < RT_OFF_MESH_REDO && a.mesh_bounds && !tri_hit && !fin && !running &&
+            ((mode == M_SHADOW && need_trav) || (mode == M_CLOSEST && depth > 0)))
+            off_mesh = segment_misses_box(qo, qd, RT_SMALL_F, mode == M_SHADOW ? stmax : kInf, a.mesh_lo, a.mesh_hi);
+        const bool redo = (issued && !need_trav) || known_miss || off_mesh;
         if (!__any(redo)) break;
         if (redo) {
             ts.best = -1;
@@ -2235,7 +2264,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                    cosWi > 0 after the visibility test; the ray is const there, and
                    both draws were already made).  Same pixel, same seeds. */
                 if ((shadow && (!(qt > RT_SMALL_F) || !(qd.x * hn.x + qd.y * hn.y + qd.z * hn.z > 0))) ||
-                    (SPLIT && !shadow && (int)depth < hit_depth)) { /* a long chain's box segment */
+                    (SPLIT && !shadow && (int)depth < hit_depth) || /* a long chain's box segment */
+                    (a.mesh_bounds && !tri_hit && (shadow || depth > 0) &&
+                     segment_misses_box(qo, qd, RT_SMALL_F, qt, a.mesh_lo, a.mesh_hi))) { /* off the mesh */
                     ts.best = -1;
                     fin = true;
                     ++cnt[RT_CNT_SKIPPED];

@@ -818,7 +818,9 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     /* speculated mesh pixels: the silhouettes' neighbours run as long chains (RT_SPLIT_SPEC=2: every
        probe-hit pixel speculated — a test knob that makes repairs happen) */
     const uint32_t spec_row = split && c->split_spec == 1 ? W : 0u;
-    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? 96u * pn2 : 0u, spec_row, st);
+    /* RT_LONG_STEPS (A/B knob): the probe steps per ray above which a mesh pixel runs as a long chain (96; 0: none) */
+    const uint32_t long_steps = env_u32("RT_LONG_STEPS", 96);
+    e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? long_steps * pn2 : 0u, spec_row, st);
     if (e) return hip_fail(c, (hipError_t)e, "box-pixel scan");
     uint32_t n_box = 0;
     if (split) { /* every long chain gets a slot: their seed pass and chunks run on a stream of their own */
@@ -1367,7 +1369,8 @@ try {
            dragon frame at 1024 blocks 96.7 -> 101.2 ms: profiles/r04l, r04m) */
         const bool short_frame =
             (uint64_t)W * hl * c->sample_rate * c->sample_rate < kShortFrameSamplesPerLane * (uint64_t)blocks * RT_BLOCK;
-        if (short_frame) blocks = std::max(1, blocks * kShortFrameBlocksPerCU / RT_TRIS_WAVES);
+        if (short_frame) /* RT_SHORT_BLOCKS (A/B knob): blocks per CU of a short frame */
+            blocks = std::max(1, blocks * (int)env_u32("RT_SHORT_BLOCKS", kShortFrameBlocksPerCU) / RT_TRIS_WAVES);
         if (const uint32_t gb = env_u32("RTMI_GRID_BLOCKS", 0)) blocks = std::min(blocks, (int)gb);
         if (trav == RT_TRAV_BVH4Q) {
             r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
@@ -1485,7 +1488,9 @@ try {
            frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;
         bool record_iter = false;
-        if (a.tile_order && c->measured_lpt && !c->order_measured && c->sample_rate > 0 &&
+        /* (frames of >= 16 samples per pixel: a 1-spp pixel's cost is one random path, and the bunny
+           class measured 0.436 -> 0.459 ms re-sorted by it, profiles/r05aj) */
+        if (a.tile_order && c->measured_lpt && !c->order_measured && c->sample_rate * c->sample_rate >= 16u &&
             (!a.split_chunks || c->measured_lpt > 1)) {
             const uint32_t nch = a.split_chunks ? a.split_chunks : 1u;
             const size_t n_i = (size_t)W * hl * nch;

@@ -252,8 +252,10 @@ struct rt_ctx {
 
     /* scratch */
     uint32_t *d_work = nullptr;                 /* queue cursors: inside the d_counters allocation, after the counters */
-    unsigned long long *d_counters = nullptr;   /* RT_COUNTER_WORDS counters + guard, then the 64 cursor words */
+    unsigned long long *d_counters = nullptr;   /* RT_COUNTER_WORDS counters + guard, then the kWorkWords cursor words */
     unsigned long long *h_counters = nullptr;   /* pinned: the counters (+ the list area's fill) copied back on the render's stream */
+    unsigned long long *h_counters_dev = nullptr; /* its device address (mapped): k_counters_out writes it */
+    bool counters_zeroed = false;                 /* the last render ended with k_counters_out: no fill needed */
     hipStream_t sync_stream = nullptr;          /* the stream of the last render (rt_synchronize waits on it) */
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
@@ -927,6 +929,11 @@ try {
     }
     memset(c->h_counters, 0, kCounterBytes + sizeof(unsigned long long)); /* no stale guard before any render */
     c->d_work = reinterpret_cast<uint32_t *>(c->d_counters + RT_COUNTER_WORDS);
+    /* the pinned copy's device address: a render hands its counters back with k_counters_out
+       (RT_COUNTERS_KERNEL=0: the copy-engine transfer instead) */
+    void *hd = nullptr;
+    if (env_u32("RT_COUNTERS_KERNEL", 1) && hipHostGetDevicePointer(&hd, c->h_counters, 0) == hipSuccess)
+        c->h_counters_dev = static_cast<unsigned long long *>(hd);
     *out = c;
     return RT_OK;
 } RT_CATCH(nullptr)
@@ -1325,8 +1332,10 @@ try {
         dout = c->d_stage;
         if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
     }
-    /* the counters, the guard word and the queue cursors: one memset */
-    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
+    /* the counters, the guard word and the queue cursors: one memset (none when the last render's
+       k_counters_out left them zeroed) */
+    if (!c->counters_zeroed) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
+    c->counters_zeroed = false;
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;
     int e = 0;
@@ -1689,7 +1698,15 @@ try {
     if (e) return hip_fail(c, (hipError_t)e, "kernel launch");
     /* the counters (and a new list build's fill) come back on the render's stream, so that
        rt_synchronize is one stream wait (no blocking copy after it) */
-    HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, st));
+    if (c->h_counters_dev && !c->info.lists_rebuilt) {
+        /* counters to the host and zeroed for the next render, in one kernel */
+        const int ek = rt_launch_counters_out(c->d_counters, c->h_counters_dev, (uint32_t)RT_COUNTER_WORDS,
+                                              (uint32_t)((kCounterBytes + kWorkWords * sizeof(uint32_t)) / 8u), st);
+        if (ek) return hip_fail(c, (hipError_t)ek, "counter hand-back");
+        c->counters_zeroed = true;
+    } else {
+        HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, st));
+    }
     if (c->info.lists_rebuilt)
         HIPCHK(c, hipMemcpyAsync(c->h_counters + RT_COUNTER_WORDS, c->d_list_alloc, sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, st));
@@ -1913,6 +1930,7 @@ try {
                     break;
                 }
             }
+        c->counters_zeroed = false; /* this trace leaves its counts there */
         if (c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), c->stream);
         if (e == hipSuccess) {
             const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,

@@ -3130,6 +3130,28 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
     return (int)hipGetLastError();
 }
 
+/* The end of a render: its counters (n_cnt words) written straight into the host's pinned, mapped
+   copy, and the counters and queue cursors (n_zero words from `dev`, the counters first) zeroed for
+   the next render — one small kernel on the render's stream instead of a copy-engine transfer
+   plus a fill at the next render's start. */
+__global__ __launch_bounds__(256) void k_counters_out(unsigned long long *__restrict__ dev,
+                                                      unsigned long long *__restrict__ host, uint32_t n_cnt,
+                                                      uint32_t n_zero)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n_cnt) host[i] = dev[i];
+    if (i < n_zero) dev[i] = 0ull;
+}
+
+int rt_launch_counters_out(unsigned long long *dev, unsigned long long *host_mapped, uint32_t n_cnt, uint32_t n_zero,
+                           void *stream)
+{
+    const uint32_t n = n_cnt > n_zero ? n_cnt : n_zero;
+    hipLaunchKernelGGL(k_counters_out, dim3((n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream, dev, host_mapped,
+                       n_cnt, n_zero);
+    return (int)hipGetLastError();
+}
+
 int rt_launch_split_seeds(const RtTriLaunch &a, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;

@@ -13,7 +13,7 @@ seconds each.
   * BASELINE configs[0]: the sphere scene at 512x512, 1 spp (main.cpp:123-127), from the
     context's own seeds (the padded 512x512 layout, RayTracerCL.cpp:229-232), three frames;
   * configs[2]: the bunny-class mesh at 1024x1024, 1 spp, three frames (the later ones with the
-    camera-ray candidate lists of the unchanged view and its measured-cost schedule);
+    camera-ray candidate lists of the unchanged view);
   * configs[3]: the dragon-class frame, 1920x1080, at sampleRate 4 (whole-pixel tasks);
   * one 8-way row-stripe tile of configs[3] at its own sampleRate 16 (256 spp): the sample-split
     path with its long chains, speculated mesh pixels and the repair pass;
@@ -117,8 +117,8 @@ def test_sphere_config1_512_vs_oracle(tracer, pt, oracle):
 
 def test_bunny_config_whole_frame_vs_bvh_oracle(tracer, pt, oracle):
     """BASELINE configs[2]: the bunny-class mesh (69,451 triangles) at 1024x1024, 1 spp, from the
-    context's own seeds: every pixel and seed slot of three progressive frames (the second reuses
-    the view's schedule, re-sorted by the first frame's measured per-pixel costs, and builds its
+    context's own seeds: every pixel and seed slot of three progressive frames (the later ones reuse
+    the view's schedule — a 1-spp frame keeps the probe's order — and the second builds its
     candidate lists) equal to the oracle's."""
     sc = pt.scenes
     W = H = 1024
@@ -141,7 +141,7 @@ def test_bunny_config_whole_frame_vs_bvh_oracle(tracer, pt, oracle):
         rt.rayTrace(got, W, H, p, kernel=2)
         info = rt.renderInfo()
         assert info["lists"] == (1 if p >= 1 else 0), info
-        assert info["schedule_measured"] == (1 if p >= 1 else 0), info
+        assert info["schedule_measured"] == 0, info  # 1 spp: the probe's order throughout
         c_or = oracle.render_tris(exp, cam, S, W, H, Wp, Hp, 1, 6, p, sd, verts, idx, bvh=bvh)
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"frame {p}")
         cnt = rt.counters()
@@ -153,18 +153,23 @@ def test_bunny_config_whole_frame_vs_bvh_oracle(tracer, pt, oracle):
 
 def test_dragon_whole_frame_sr4_vs_bvh_oracle(tracer, pt, dragon, dragon_sr4):
     """BASELINE configs[3]'s frame (dragon class, 871,414 triangles, 1920x1080, maxDepth 6) at
-    sampleRate 4: all 2,073,600 pixels, both seed planes and the ray counts equal to the oracle's."""
+    sampleRate 4: all 2,073,600 pixels, both seed planes and the ray counts equal to the oracle's —
+    rendered under the probe's order, then again from the same seeds under the order re-sorted by
+    the first render's measured per-pixel costs (16 spp, whole pixels: DESIGN §4.4)."""
     d = dragon
     exp, sd, c_or = dragon_sr4
     rt = _tracer(pt, d, 4)
     got = np.zeros(d["W"] * d["H"] * 4, np.float32)
-    rt.rayTrace(got, d["W"], d["H"], 0, kernel=2)
-    info = rt.renderInfo()
-    assert info["lists"] == 1 and info["split_chunks"] == 0, info
-    np.testing.assert_array_equal(bits(got), bits(exp))
-    np.testing.assert_array_equal(rt.getSeeds(), sd)
-    cnt = rt.counters()
-    assert (cnt["rays_closest"], cnt["rays_shadow"]) == c_or
+    for k in range(2):
+        if k:
+            rt.setSeeds(d["Wp"], d["Hp"], d["seeds"])
+        rt.rayTrace(got, d["W"], d["H"], 0, kernel=2)
+        info = rt.renderInfo()
+        assert info["lists"] == 1 and info["split_chunks"] == 0 and info["schedule_measured"] == k, info
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"render {k}")
+        np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg=f"render {k}")
+        cnt = rt.counters()
+        assert (cnt["rays_closest"], cnt["rays_shadow"]) == c_or
     rt.close()
 
 

@@ -2483,11 +2483,14 @@ __device__ V3 trace_path(PathRay &r, const rt_sphere *__restrict__ sph, uint32_t
 }
 
 template <bool SS>
-__global__ __launch_bounds__(RT_BLOCK) void k_spheres(RtSphLaunch a)
+#ifndef RT_SPH_TILE
+#define RT_SPH_TILE 16 /* pixel tile per block, RT_SPH_TILE^2 threads (A/B: 8) */
+#endif
+__global__ __launch_bounds__(RT_SPH_TILE * RT_SPH_TILE) void k_spheres(RtSphLaunch a)
 {
-    /* 16 x 16 pixel tile per block; a wave covers 16 x 4 pixels */
-    const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u);
-    const uint32_t yl = blockIdx.y * 16u + (threadIdx.x >> 4);
+    /* RT_SPH_TILE x RT_SPH_TILE pixel tile per block; a wave covers 64 consecutive pixels of it */
+    const uint32_t x = blockIdx.x * RT_SPH_TILE + (threadIdx.x % RT_SPH_TILE);
+    const uint32_t yl = blockIdx.y * RT_SPH_TILE + (threadIdx.x / RT_SPH_TILE);
     unsigned long long n_closest = 0, n_shadow = 0, n_skipped = 0;
     if (x < a.W && yl < a.Hl) {
         const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
@@ -3188,7 +3191,8 @@ int rt_launch_split_finish(const RtTriLaunch &a, void *stream)
 int rt_launch_spheres(const RtSphLaunch &a, bool single_sample, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid((a.W + 15u) / 16u, (a.Hl + 15u) / 16u), block(RT_BLOCK);
+    constexpr uint32_t T = RT_SPH_TILE;
+    dim3 grid((a.W + T - 1u) / T, (a.Hl + T - 1u) / T), block(T * T);
     if (single_sample) hipLaunchKernelGGL((k_spheres<true>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_spheres<false>), grid, block, 0, st, a);
     return (int)hipGetLastError();

@@ -235,7 +235,7 @@ struct RtTriLaunch {
        triangle and is answered in the path advance, without a traversal (0: not used) */
     uint32_t mesh_bounds;
     float mesh_lo[3], mesh_hi[3];
-    uint32_t queue_batch; /* k_tris: items per take from the multi-head queue (mq_take; work_counter then points
+    uint32_t queue_batch; /* k_tris: items per take from the multi-head queue (mq_take, exact takes when take_exact; work_counter then points
                              at RT_QHEADS heads RT_QSTRIDE words apart); 0: one head (batch_take) */
     /* RT_SPLIT_BOX, slotted seeds, one sample per task: per slot and sample (slot x spp + sample) the
        depth of the segment whose closest-hit query meets the mesh, 0xff for a path that meets only

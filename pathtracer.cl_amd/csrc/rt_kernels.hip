@@ -616,13 +616,14 @@ __device__ __forceinline__ uint32_t mq_take(uint32_t *heads, uint32_t n_tasks, u
     if (k > from_b && (qs >> 8) < Q) {
         const int leader = __ffsll((long long)idle) - 1;
         uint32_t nb = 0;
-        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(heads + RT_QSTRIDE * hq, batch);
+        const uint32_t take = batch ? batch : k - from_b; /* batch 0: exactly the items needed */
+        if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(heads + RT_QSTRIDE * hq, take);
         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader));
         const uint32_t n_groups = n_tasks >> 6;
         const uint32_t n_local = (n_groups > hq ? (n_groups - hq + Q - 1u) / Q : 0u) * 64u;
         if (nb < n_local) {
             const uint32_t r = rank - from_b;
-            bend = nb + batch < n_local ? nb + batch : n_local;
+            bend = nb + take < n_local ? nb + take : n_local;
             if (rank >= from_b && nb + r < bend) item = (((nb + r) >> 6) * Q + hq) * 64u + ((nb + r) & 63u);
             const uint32_t need = k - from_b;
             bnext = nb + (need < bend - nb ? need : bend - nb);
@@ -2121,7 +2122,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 64 items; bunny class 1024^2 at 1 spp 0.95 -> 0.55 ms, the dragon frame +-0.5 %) ---- */
         const unsigned long long idle = __ballot(mode == M_IDLE);
         if (idle) {
-            const uint32_t item = multi_q ? mq_take(a.work_counter, n_tasks, idle, bnext, bend, qs, a.queue_batch)
+            const uint32_t item = multi_q ? mq_take(a.work_counter, n_tasks, idle, bnext, bend, qs,
+                                                    a.take_exact ? 0u : a.queue_batch)
                                           : batch_take(a.work_counter, idle, bnext, bend, a.take_exact ? 0u : kBatch);
             if (mode == M_IDLE) {
                 if (multi_q && item == ~0u) {
@@ -3111,7 +3113,7 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
     hipStream_t st = (hipStream_t)stream;
     dim3 grid((unsigned)grid_blocks), block(RT_BLOCK);
     /* the multi-head queue: its own instantiations (its take costs the others registers) */
-    const bool mq = a.queue_batch && !a.take_exact && trav == RT_TRAV_BVH4Q && a.split_which != RT_SPLIT_BOX;
+    const bool mq = a.queue_batch && trav == RT_TRAV_BVH4Q && a.split_which != RT_SPLIT_BOX;
 #define RT_LAUNCH_TRIS(T, S)                                                                                           \
     do {                                                                                                               \
         if (mq && count) hipLaunchKernelGGL((k_tris<RT_TRAV_BVH4Q, true, S, true>), grid, block, 0, st, a);            \

@@ -1493,9 +1493,10 @@ try {
            split tiles' chunk tasks keep one head (their tiles' chunk layers spread over the heads
            measured 15.6 -> 16.3 ms) */
         a.queue_batch = a.take_exact || a.split_chunks ? 0u : std::min(64u, env_u32("RT_QUEUE_BATCH", RT_QUEUE_BATCH));
-        /* long tasks with exact takes from the multi-head queue (RT_EXACT_HEADS=1, A/B): each head's
-           tiles go to the waves of one XCD's blocks, so a tile's pixels share that XCD's L2 */
-        if (a.take_exact && env_u32("RT_EXACT_HEADS", 0)) a.queue_batch = 64u;
+        /* long tasks take exactly from the multi-head queue too: each head's tiles go to the waves
+           of one XCD's blocks, so a tile's pixels share that XCD's L2 (dragon frame 87.4 -> 86.5 ms,
+           profiles/r05ar; RT_EXACT_HEADS=0: one head) */
+        if (a.take_exact && env_u32("RT_EXACT_HEADS", 1)) a.queue_batch = 64u;
         /* a frame under the probe's order records its pixels' costs for the next frame (a sample-split
            frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;

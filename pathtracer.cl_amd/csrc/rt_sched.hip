@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_tile_cost(const uint32_t *__restrict__ 
    probe's shadow rays aim at the light centres); a sample-split frame's pixel: the sum over its nch
    chunk tasks (0 for pixels that ran elsewhere: the long chains) */
 __global__ __launch_bounds__(256) void k_tile_cost_measured(const uint32_t *__restrict__ iters, uint32_t W,
-                                                            uint32_t hl, uint32_t nch, float wmax, uint32_t buckets,
+                                                            uint32_t hl, uint32_t nch, float wmax,
                                                             float *__restrict__ keys, uint32_t *__restrict__ idx)
 {
     const uint32_t tx = (W + 7u) / 8u, n_t = tx * ((hl + 7u) / 8u);
@@ -118,19 +118,7 @@ __global__ __launch_bounds__(256) void k_tile_cost_measured(const uint32_t *__re
             mx = mx > pc ? mx : pc;
         }
     }
-    const double key = (1.0 - wmax) * sum / 64.0 + wmax * mx;
-    if (buckets) {
-        /* A/B (RT_LPT_BUCKETS=n): keys in n-per-octave buckets, and within a bucket the tiles in
-           Morton order — consecutive queue tiles spatially close, for the L2 */
-        uint32_t m = 0;
-        const uint32_t tx0 = t % tx, ty0 = t / tx;
-        for (int b = 0; b < 8; ++b) m |= ((tx0 >> b) & 1u) << (2 * b) | ((ty0 >> b) & 1u) << (2 * b + 1);
-        const double q = floor(log2(key) * (double)buckets);
-        const double bq = q < 0.0 ? 0.0 : (q > 255.0 ? 255.0 : q);
-        keys[t] = (float)(bq * 65536.0 + (double)(65535u - (m & 65535u)));
-    } else {
-        keys[t] = (float)key;
-    }
+    keys[t] = (float)((1.0 - wmax) * sum / 64.0 + wmax * mx);
     idx[t] = t;
 }
 
@@ -265,10 +253,8 @@ int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W
     /* the tile key's weight of its costliest pixel (RT_LPT_MAX: an A/B knob, default the probe key's) */
     float wmax = (float)kLptMax;
     if (const char *v = getenv("RT_LPT_MAX")) wmax = (float)atof(v);
-    uint32_t buckets = 0;
-    if (const char *v = getenv("RT_LPT_BUCKETS")) buckets = (uint32_t)atoi(v);
     hipLaunchKernelGGL(k_tile_cost_measured, dim3((n_t + 255u) / 256u), dim3(256), 0, st, iters, W, hl, nch, wmax,
-                       buckets, s.keys, s.idx);
+                       s.keys, s.idx);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     size_t bytes = s.tmp_bytes;

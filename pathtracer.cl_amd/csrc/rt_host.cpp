@@ -1489,14 +1489,16 @@ try {
             a.mesh_hi[k] = c->mesh_hi[k];
         }
         /* short whole-pixel frames take from the multi-head queue (mq_take) in batches of
-           RT_QUEUE_BATCH items (0: one head; bunny class 0.519 -> 0.473 ms, profiles/r05ac); the
-           split tiles' chunk tasks keep one head (their tiles' chunk layers spread over the heads
-           measured 15.6 -> 16.3 ms) */
+           RT_QUEUE_BATCH items (0: one head; bunny class 0.519 -> 0.473 ms, profiles/r05ac) */
         a.queue_batch = a.take_exact || a.split_chunks ? 0u : std::min(64u, env_u32("RT_QUEUE_BATCH", RT_QUEUE_BATCH));
         /* long tasks take exactly from the multi-head queue too: each head's tiles go to the waves
            of one XCD's blocks, so a tile's pixels share that XCD's L2 (dragon frame 87.4 -> 86.5 ms,
            profiles/r05ar; RT_EXACT_HEADS=0: one head) */
         if (a.take_exact && env_u32("RT_EXACT_HEADS", 1)) a.queue_batch = 64u;
+        /* a split tile's mesh chunk tasks from the heads too, in batches of RT_SPLIT_HEADS (64; 0: one
+           head), a tile's chunk layers on one head (8-way tile 15.95 -> 15.71 ms, profiles/r05au) */
+        if (a.split_chunks && env_u32("RT_SPLIT_HEADS", 64))
+            a.queue_batch = std::min(64u, env_u32("RT_SPLIT_HEADS", 64));
         /* a frame under the probe's order records its pixels' costs for the next frame (a sample-split
            frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;

@@ -602,7 +602,7 @@ __device__ __forceinline__ uint32_t batch_take(uint32_t *counter, unsigned long 
    take; a lane whose take found a drained head stays idle and takes again in the next iteration.
    Returns the lane's item or ~0u.  Wave-uniform, like batch_take. */
 __device__ __forceinline__ uint32_t mq_take(uint32_t *heads, uint32_t n_tasks, unsigned long long idle, uint32_t &bnext,
-                                            uint32_t &bend, uint32_t &qs, uint32_t batch)
+                                            uint32_t &bend, uint32_t &qs, uint32_t batch, uint32_t span = 64u)
 {
     constexpr uint32_t Q = RT_QHEADS;
     const uint32_t k = (uint32_t)__popcll(idle);
@@ -610,8 +610,10 @@ __device__ __forceinline__ uint32_t mq_take(uint32_t *heads, uint32_t n_tasks, u
     const uint32_t avail = bend - bnext;
     const uint32_t from_b = k < avail ? k : avail;
     const uint32_t bq = qs & 15u, hq = (qs >> 4) & 15u;
-    /* local index l of head q -> queue item: group (l / 64) x Q + q, offset l mod 64 */
-    uint32_t item = rank < from_b ? (((bnext + rank) >> 6) * Q + bq) * 64u + ((bnext + rank) & 63u) : ~0u;
+    /* local index l of head q -> queue item: span-item group (l / span) x Q + q, offset l mod span (span
+       64: a tile; a split launch's 64 x chunks: a tile's chunk layers together) */
+    auto global = [&](uint32_t l, uint32_t q) { return ((l / span) * Q + q) * span + l % span; };
+    uint32_t item = rank < from_b ? global(bnext + rank, bq) : ~0u;
     bnext += from_b;
     if (k > from_b && (qs >> 8) < Q) {
         const int leader = __ffsll((long long)idle) - 1;
@@ -619,12 +621,12 @@ __device__ __forceinline__ uint32_t mq_take(uint32_t *heads, uint32_t n_tasks, u
         const uint32_t take = batch ? batch : k - from_b; /* batch 0: exactly the items needed */
         if ((int)(threadIdx.x & 63) == leader) nb = atomicAdd(heads + RT_QSTRIDE * hq, take);
         nb = __builtin_amdgcn_readfirstlane(__shfl(nb, leader));
-        const uint32_t n_groups = n_tasks >> 6;
-        const uint32_t n_local = (n_groups > hq ? (n_groups - hq + Q - 1u) / Q : 0u) * 64u;
+        const uint32_t n_groups = n_tasks / span;
+        const uint32_t n_local = (n_groups > hq ? (n_groups - hq + Q - 1u) / Q : 0u) * span;
         if (nb < n_local) {
             const uint32_t r = rank - from_b;
             bend = nb + take < n_local ? nb + take : n_local;
-            if (rank >= from_b && nb + r < bend) item = (((nb + r) >> 6) * Q + hq) * 64u + ((nb + r) & 63u);
+            if (rank >= from_b && nb + r < bend) item = global(nb + r, hq);
             const uint32_t need = k - from_b;
             bnext = nb + (need < bend - nb ? need : bend - nb);
             qs = hq | hq << 4; /* the batch's head, the same head next, no drained heads */
@@ -2100,7 +2102,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         /* and a box-path query (a bounce off the box, or a shadow ray leaving it) whose segment misses
            the mesh's padded bounds: no triangle accepted, whatever the traversal would visit */
         bool off_mesh = false;
-        if (redo_pass < RT_OFF_MESH_REDO && a.mesh_bounds && !tri_hit && !fin && !running &&
+        if (!SPLIT && redo_pass < RT_OFF_MESH_REDO && a.mesh_bounds && !tri_hit && !fin && !running &&
             ((mode == M_SHADOW && need_trav) || (mode == M_CLOSEST && depth > 0)))
             off_mesh = segment_misses_box(qo, qd, RT_SMALL_F, mode == M_SHADOW ? stmax : kInf, a.mesh_lo, a.mesh_hi);
         const bool redo = (issued && !need_trav) || known_miss || off_mesh;
@@ -2123,7 +2125,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         const unsigned long long idle = __ballot(mode == M_IDLE);
         if (idle) {
             const uint32_t item = multi_q ? mq_take(a.work_counter, n_tasks, idle, bnext, bend, qs,
-                                                    a.take_exact ? 0u : a.queue_batch)
+                                                    a.take_exact ? 0u : a.queue_batch,
+                                                    SPLIT ? 64u * a.split_chunks : 64u)
                                           : batch_take(a.work_counter, idle, bnext, bend, a.take_exact ? 0u : kBatch);
             if (mode == M_IDLE) {
                 if (multi_q && item == ~0u) {
@@ -2267,7 +2270,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                    both draws were already made).  Same pixel, same seeds. */
                 if ((shadow && (!(qt > RT_SMALL_F) || !(qd.x * hn.x + qd.y * hn.y + qd.z * hn.z > 0))) ||
                     (SPLIT && !shadow && (int)depth < hit_depth) || /* a long chain's box segment */
-                    (a.mesh_bounds && !tri_hit && (shadow || depth > 0) &&
+                    (!SPLIT && a.mesh_bounds && !tri_hit && (shadow || depth > 0) && /* (short frames: never split) */
                      segment_misses_box(qo, qd, RT_SMALL_F, qt, a.mesh_lo, a.mesh_hi))) { /* off the mesh */
                     ts.best = -1;
                     fin = true;

@@ -1334,7 +1334,8 @@ try {
     }
     /* the counters, the guard word and the queue cursors: one memset (none when the last render's
        k_counters_out left them zeroed) */
-    if (!c->counters_zeroed) HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
+    if (!c->counters_zeroed || st != c->sync_stream) /* (another stream: its zeroing is not ordered before us) */
+        HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
     c->counters_zeroed = false;
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;

@@ -87,6 +87,7 @@ def main():
                     "steps": int(steps.ravel()[i]),
                     # counting launch: loop iterations and wave clocks (x 64) in the path advance (D),
                     # the refill + camera ray (A/B) and the stepping rounds (C) while the pixel ran
+                    "plain_q": int(ph[..., 2].ravel()[i]), "plain_steps": int(ph[..., 3].ravel()[i]),
                     "iters": int(ph[..., 7].ravel()[i]), "d_kclk": int(ph[..., 4].ravel()[i]) * 64 // 1000,
                     "ab_kclk": int(ph[..., 5].ravel()[i]) * 64 // 1000,
                     "c_kclk": int(ph[..., 6].ravel()[i]) * 64 // 1000} for i in idx]
@@ -99,6 +100,10 @@ def main():
     it = ph[..., 7]
     res["iters_pct"] = {p: float(np.percentile(it, p)) for p in (50, 90, 99, 100)}
     res["heavy_iters_pct"] = {p: float(np.percentile(it[heavy], p)) for p in (50, 90, 100)}
+    # iterations beyond a pixel's own need (one per query, plus its steps over 6 per stepping round)
+    need = ph[..., 2] + (ph[..., 3] + 5) // 6
+    res["excess_iters_pct"] = {p: float(np.percentile(it - need, p)) for p in (10, 50, 90, 99, 100)}
+    res["excess_iters_heavy_pct"] = {p: float(np.percentile((it - need)[heavy], p)) for p in (10, 50, 90, 99, 100)}
     tot = ph[..., 4:7].sum(axis=(0, 1)).astype(np.float64)
     res["phase_share"] = {"D": tot[0] / tot.sum(), "AB": tot[1] / tot.sum(), "C": tot[2] / tot.sum()}
     txt = json.dumps(res, indent=1)

@@ -167,6 +167,7 @@ struct rt_ctx {
 #ifndef RT_SPLIT_GPW
 #define RT_SPLIT_GPW 0
 #endif
+    uint32_t split_nch = 16;   /* sample-split: chunk tasks per pixel (about; RT_SPLIT_NCH A/B knob, 2-64) */
     uint32_t split_gpw = RT_SPLIT_GPW; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
     float *d_split_col = nullptr;     /* per sample and pixel: its radiance */
@@ -909,6 +910,7 @@ try {
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
+    if (const char *v = getenv("RT_SPLIT_NCH")) c->split_nch = (uint32_t)std::min(64, std::max(2, atoi(v))); /* A/B knob */
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);
@@ -1431,7 +1433,7 @@ try {
                chains' chunks (run after their seed pass, on a nearly idle chip) are 4x shorter:
                8-way tile 22.6 -> 20.x ms */
             const uint32_t spp = c->sample_rate * c->sample_rate;
-            const uint32_t fine = std::max(1u, (spp + 63u) / 64u), csz = fine * std::max(1u, ((spp + 15u) / 16u) / fine);
+            const uint32_t fine = std::max(1u, (spp + 63u) / 64u), csz = fine * std::max(1u, ((spp + c->split_nch - 1u) / c->split_nch) / fine);
             const uint32_t nch = (spp + csz - 1u) / csz, nseed = (spp + fine - 1u) / fine + 1u;
             const size_t npx_s = (size_t)W * hl;
             const size_t seed_bytes = npx_s * nseed * 8u, col_bytes = npx_s * spp * 12u;

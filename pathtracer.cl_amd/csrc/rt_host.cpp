@@ -910,7 +910,7 @@ try {
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
-    if (const char *v = getenv("RT_SPLIT_NCH")) c->split_nch = (uint32_t)std::min(64, std::max(2, atoi(v))); /* A/B knob */
+    if (const char *v = getenv("RT_SPLIT_NCH")) c->split_nch = (uint32_t)std::min(64, std::max(1, atoi(v))); /* A/B knob */
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);

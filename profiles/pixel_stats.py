@@ -4,7 +4,9 @@ steps per pixel), then: the finish
 time distribution, the last pixels to finish and what they are (probe: box or mesh pixel),
 and how the frame's last milliseconds are spent.  GPU box.
 
-    python profiles/pixel_stats.py [out.json] [--config dragon|bunny] [--lib build.so]
+    python profiles/pixel_stats.py [out.json] [--config dragon|bunny] [--lib build.so] [--tile N:R]
+
+`--tile N:R`: rank R's row-stripe tile (stripe 8) of an N-way split of the frame instead.
 
 The plain launch records clocks only in a diagnostics build of the library
 (`bash profiles/build_variant.sh ab/stats.so -DRT_PLAIN_PIXEL_STATS=1`, run with
@@ -37,6 +39,12 @@ def main():
         i = argv.index("--lib")
         os.environ["RTMI_LIB"] = str(Path(argv[i + 1]).resolve())
         del argv[i:i + 2]
+    tile = None
+    if "--tile" in argv:  # rank R's row-stripe tile of N (stripe 8)
+        i = argv.index("--tile")
+        n, r = (int(v) for v in argv[i + 1].split(":"))
+        tile = (8, n, r)
+        del argv[i:i + 2]
     pt = ptload.load()
     sc = pt.scenes
     W, H, sr = (1920, 1080, 16) if cfg == "dragon" else (1024, 1024, 1)
@@ -48,14 +56,17 @@ def main():
     rt.setMaxPathDepth(6)
     rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS[cfg]))
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
-    rt.rayTrace(out, W, H, 0, kernel=2)  # probe + warm
-    rt.rayTrace(out, W, H, 0, kernel=2)
+    if tile:
+        H = len(ptload.submodule("dist").tile_rows(H, *tile))  # the dump holds the tile's rows
+    H_frame = H if not tile else {"dragon": 1080, "bunny": 1024}[cfg]
+    rt.rayTrace(out, W, H_frame, 0, kernel=2, tile=tile)  # probe + warm
+    rt.rayTrace(out, W, H_frame, 0, kernel=2, tile=tile)
     plain_ms = rt.lastKernelMs()
     s = np.fromfile(dump, np.uint32).reshape(H, W, 8).astype(np.int64)  # timing: the plain launch
     if not s[..., 1].any():  # the library records clocks in counting launches only
         s = None
     rt.setCounting(True)
-    rt.rayTrace(out, W, H, 0, kernel=2)
+    rt.rayTrace(out, W, H_frame, 0, kernel=2, tile=tile)
     count_ms = rt.lastKernelMs()
     sc_ = np.fromfile(dump, np.uint32).reshape(H, W, 8).astype(np.int64)  # queries / steps
     if s is None:

@@ -167,7 +167,7 @@ struct rt_ctx {
 #ifndef RT_SPLIT_GPW
 #define RT_SPLIT_GPW 0
 #endif
-    uint32_t split_nch = 16;   /* sample-split: chunk tasks per pixel (about; RT_SPLIT_NCH A/B knob, 2-64) */
+    uint32_t split_nch = 16;   /* sample-split: chunk tasks per pixel (about; RT_SPLIT_NCH A/B knob, 1-64) */
     uint32_t split_gpw = RT_SPLIT_GPW; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
     float *d_split_col = nullptr;     /* per sample and pixel: its radiance */

@@ -528,13 +528,16 @@ int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
 }
 
 /* The long chains' seed-pass grid: one chain per group of `width` lanes, at most a quarter of
-   the full grid (further chains queue behind the first); full_grid 0: unbounded. */
+   the full grid (further chains queue behind the first) — subtree-parallel chains at most three
+   quarters, so the mesh pixels' chunk launch beside it keeps a quarter of the grid (a tile with
+   tens of thousands of chains left it one block: RT_SEED_WIDTH=8 on the 2-way tile ran for
+   seconds, profiles/r05bc; 77 ms with the cap, r05bf); full_grid 0: unbounded. */
 int split_box_blocks(const rt_ctx *c, uint32_t width, int full_grid)
 {
     const uint32_t per_wave = c->split_gpw ? c->split_gpw : 64u / std::max(1u, width == RT_SEED_COOP4 ? 4u : width);
     int n = (int)((c->n_split_box + per_wave * 4u - 1u) / (per_wave * 4u));
-    /* subtree-parallel chains (width >= 8) all run at once: each is the critical path */
-    if (full_grid > 0) n = std::min(n, std::max(1, width >= 8 ? full_grid : full_grid / RT_BOX_GRID_DIV));
+    /* subtree-parallel chains (width >= 8) all run at once where they fit: each is the critical path */
+    if (full_grid > 0) n = std::min(n, std::max(1, width >= 8 ? full_grid * 3 / 4 : full_grid / RT_BOX_GRID_DIV));
     return n;
 }
 

@@ -167,6 +167,7 @@ struct rt_ctx {
 #ifndef RT_SPLIT_GPW
 #define RT_SPLIT_GPW 0
 #endif
+    bool repair_wide = true;   /* the repair pass in the runs form whatever the long chains' (RT_REPAIR_WIDE A/B knob) */
     uint32_t split_nch = 16;   /* sample-split: chunk tasks per pixel (about; RT_SPLIT_NCH A/B knob, 1-64) */
     uint32_t split_gpw = RT_SPLIT_GPW; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
@@ -704,7 +705,9 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_restart = a.split_dirty; /* each chain from its first missed chunk on */
         r.split_restart_chunk = a.split_chunk;
         r.finish_part = RT_FIN_LIST;
-        if (a.split_coop >= 8) {
+        /* the runs form also where the long chains take the cooperative pass (the 4-way tile: the
+           repair 2.7 -> 2.1 ms at the end of the mesh pixels' stream, the tile 28.83 -> 28.39 ms, profiles/r05bg, r05bh) */
+        if (a.split_coop >= 8 || c->repair_wide) {
             const uint32_t spp = a.sample_rate * a.sample_rate;
             r.split_coop = RT_REPAIR_WIDTH; /* runs of width - 1 hit samples (k_chain_seeds<width, true>) */
             RtTriLaunch s = r;
@@ -913,6 +916,7 @@ try {
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
     if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
+    if (const char *v = getenv("RT_REPAIR_WIDE")) c->repair_wide = atoi(v) != 0; /* A/B knob */
     if (const char *v = getenv("RT_SPLIT_NCH")) c->split_nch = (uint32_t)std::min(64, std::max(1, atoi(v))); /* A/B knob */
     if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
     if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */

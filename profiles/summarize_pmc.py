@@ -62,7 +62,7 @@ def main():
     tag = sys.argv[1]
     src = Path(sys.argv[2]) if len(sys.argv) > 2 else ROOT / "gpurun_out" / f"prof_{tag}"
     workload = sys.argv[3] if len(sys.argv) > 3 else None
-    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_tris<4, false, false, false>"
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_tris<4, false, false, true>"
     files = sorted(glob.glob(f"{src}/pmc_*/run_counter_collection.csv")) + sorted(
         glob.glob(f"{src}/pmcx_*/run_counter_collection.csv"))
     c = counters(files, kernel)

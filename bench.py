@@ -349,9 +349,10 @@ def main():
     # frame is the same full render, its seeds carried on the device from the one before. The
     # per-frame kernel times for the roofline come from a synchronous pass after the timed one.
     pipelined = world == 1 and halo is None and comm is None and not frames_per_rank
-    rays_frame_fixed = None
+    rays_warm = None  # the last warm frame's count (same view), reported beside the measured mean
     if pipelined:
-        rays_frame_fixed = step()  # one more warm frame; its count is every frame's (same view)
+        rays_warm = step()
+        rt.counterTotals(reset=True)  # the timed frames' own counts accumulate on the device from here
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -362,7 +363,6 @@ def main():
             pnum = frame_no[0] if progressive else 0
             rt.rayTrace(out, W, H, pnum, kernel=kernel, tile=tile, sync=False)  # the library's own stream
             frame_no[0] += 1
-            rays += rays_frame_fixed
         else:
             rays += step()
             kernel_ms.append(rt.lastKernelMs())
@@ -371,8 +371,16 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    counted = None
     if pipelined:
         rt.synchronize()  # the render's own completion checks (guard words) for the last frame
+        # every timed frame's own queries, summed on the device by the counter hand-back kernel
+        # (raises if a defect guard fired in any of them)
+        tot = rt.counterTotals(reset=True)
+        if tot["renders"] != args.steps:
+            raise RuntimeError(f"counter totals cover {tot['renders']} renders, {args.steps} were timed")
+        rays = tot["rays_closest"] + tot["rays_shadow"]
+        counted = {"rays_skipped": tot["rays_skipped"], "renders": tot["renders"]}
         for _ in range(min(args.steps, 5)):  # untimed: each frame's kernel time (HIP events)
             step()
             kernel_ms.append(rt.lastKernelMs())
@@ -434,6 +442,8 @@ def main():
 
     frame_rays = cnt_frame["rays_closest"] + cnt_frame["rays_shadow"]
     traversed_share = (frame_rays - cnt_frame["rays_skipped"]) / max(frame_rays, 1)
+    if counted is not None:  # the timed frames' own share (one GPU, pipelined frames)
+        traversed_share = (rays - counted["rays_skipped"]) / max(rays, 1)
     line = {
         "metric": (METRIC_WEAK if frames_per_rank else METRIC) if cfg == "dragon" else CONFIG_METRIC.get(
             cfg, f"Mrays/sec + frames/sec, {cfg}"),
@@ -451,9 +461,12 @@ def main():
         # launch share; DESIGN.md §5: shadow rays answered without one are still rays)
         "mrays_traversed_per_sec": round(mrays * traversed_share, 2),
         "value_traversed": round(mrays * traversed_share, 2),
-        "value_rule": ("value counts the reference's queries (closest-hit + shadow, equal to the oracle's counts); "
+        "value_rule": ("value counts the reference's queries (closest-hit + shadow, equal to the oracle's counts) "
+                       "of the timed frames themselves, summed on the device (rt_counter_totals); "
                        "value_traversed leaves out the shadow rays answered without a traversal (tmax <= tmin, or "
                        "cos(wi) <= 0, whose term rtcommon.h:93-95 drops after the visibility test)"),
+        "rays_counted": ("device totals over the timed frames" if counted is not None
+                         else "per frame, read after each timed step"),
         "higher_is_better": True,
         "scaling": "weak" if frames_per_rank else "strong",
         "vs_baseline": None,
@@ -468,6 +481,8 @@ def main():
                                        if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl"
                                        else " + gloo gather") if world > 1 else "")),
                    "rays_per_frame": int(rays / steps / (world if frames_per_rank else 1)),
+                   # one untimed warm frame of the same view (seeds carried on, so each frame's count differs)
+                   "rays_warm_frame": int(rays_warm) if rays_warm is not None else None,
                    # rays = the reference's queries (oracle-equal counts); shadow rays whose answer
                    # cannot change the pixel are answered without a traversal
                    "rays_traversed_per_frame": int(cnt_frame["rays_closest"] + cnt_frame["rays_shadow"]

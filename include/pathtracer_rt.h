@@ -188,6 +188,13 @@ uint32_t rt_tile_rows(uint32_t height, const rt_tile *tile);
 /* ---- instrumentation ---- */
 int rt_get_counters(const rt_ctx *ctx, rt_counters *out); /* of the last completed render (or counting rt_trace_rays call) */
 int rt_set_counting(rt_ctx *ctx, int enable);             /* count nodes/tris in the next renders */
+/* Running totals over every render since the context was created or the totals were last reset
+   (renders enqueued back to back with rt_render_async overwrite each other's rt_get_counters;
+   their totals are kept on the device): waits for the context's renders, then sums of the summed
+   counters, maxima of the per-pixel maxima (pixels_long: 0), *renders = renders counted.
+   reset != 0 zeroes the totals after reading them.  RT_ERR_STATE if a sample-split defect guard
+   fired in any of those renders (rt_synchronize reports only the last one's). */
+int rt_counter_totals(rt_ctx *ctx, rt_counters *sum, uint64_t *renders, int reset);
 /* Device time of the last render's kernel (HIP events on the launch stream), ms. */
 int rt_last_kernel_ms(const rt_ctx *ctx, float *ms);
 /* The same time split at the start of the main path kernel: the camera-ray candidate-list

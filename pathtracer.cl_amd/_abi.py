@@ -165,6 +165,7 @@ SIGNATURES = {
     "rt_read": (_i32, [_vp, _vp, _sz]),
     "rt_get_counters": (_i32, [_vp, ctypes.POINTER(RtCounters)]),
     "rt_set_counting": (_i32, [_vp, _i32]),
+    "rt_counter_totals": (_i32, [_vp, ctypes.POINTER(RtCounters), ctypes.POINTER(ctypes.c_uint64), _i32]),
     "rt_last_kernel_ms": (_i32, [_vp, ctypes.POINTER(_f32)]),
     "rt_last_kernel_split_ms": (_i32, [_vp, ctypes.POINTER(_f32), ctypes.POINTER(_f32)]),
     "rt_last_render_info": (_i32, [_vp, ctypes.POINTER(RtRenderInfo)]),

@@ -258,7 +258,10 @@ struct rt_ctx {
     unsigned long long *h_counters = nullptr;   /* pinned: the counters (+ the list area's fill) copied back on the render's stream */
     unsigned long long *h_counters_dev = nullptr; /* its device address (mapped): k_counters_out writes it */
     bool counters_zeroed = false;                 /* the last render ended with k_counters_out: no fill needed */
+    unsigned long long *d_totals = nullptr;     /* running totals over renders (k_counters_out; rt_counter_totals) */
     hipStream_t sync_stream = nullptr;          /* the stream of the last render (rt_synchronize waits on it) */
+    hipEvent_t ev_done = nullptr;               /* recorded after the last render's counter hand-back: a render on
+                                                   another stream waits for it (its counters and queue cursors) */
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
     rt_counters last = {};
@@ -699,7 +702,8 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_counter = a.split_counter + 48;
         r.work_counter = a.work_counter + kWorkRepair;
         r.split_gpw = c->split_gpw;
-        r.split_seed_blocks = 16u * RT_REPAIR_WIDTH / 16u; /* up to 4 x 16 chains at once at any width */
+        r.split_seed_blocks = 16u * RT_REPAIR_WIDTH / 16u; /* RT_REPAIR_WIDTH blocks of 4 waves, one chain per wave
+                                                                at width 64: up to 256 chains at once */
         r.split_chunk = a.split_fine;
         r.split_chunks = (a.sample_rate * a.sample_rate + r.split_chunk - 1u) / r.split_chunk;
         r.split_restart = a.split_dirty; /* each chain from its first missed chunk on */
@@ -931,6 +935,9 @@ try {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->evm) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming) != hipSuccess ||
+        hipMalloc(&c->d_totals, (RT_COUNTER_WORDS + 1) * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_totals, 0, (RT_COUNTER_WORDS + 1) * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_counters, kCounterBytes + kWorkWords * sizeof(uint32_t)) != hipSuccess ||
         hipHostMalloc(&c->h_counters, kCounterBytes + sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         rt_destroy(c);
@@ -985,6 +992,8 @@ try {
     rt_sched_free(c->sched);
     free_dev(c->d_seeds);
     free_dev(c->d_counters); /* d_work lives in it */
+    free_dev(c->d_totals);
+    if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     free_dev(c->d_stage);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1341,9 +1350,12 @@ try {
         dout = c->d_stage;
         if (prog > 0) HIPCHK(c, hipMemcpyAsync(dout, out, out_bytes, hipMemcpyHostToDevice, st));
     }
+    /* a render on another stream than the last one's: ordered after that render's counter hand-back
+       (which reads and zeroes the counters and queue cursors this render uses) */
+    if (c->sync_stream && st != c->sync_stream) HIPCHK(c, hipStreamWaitEvent(st, c->ev_done, 0));
     /* the counters, the guard word and the queue cursors: one memset (none when the last render's
        k_counters_out left them zeroed) */
-    if (!c->counters_zeroed || st != c->sync_stream) /* (another stream: its zeroing is not ordered before us) */
+    if (!c->counters_zeroed)
         HIPCHK(c, hipMemsetAsync(c->d_counters, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
     c->counters_zeroed = false;
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
@@ -1715,17 +1727,20 @@ try {
     /* the counters (and a new list build's fill) come back on the render's stream, so that
        rt_synchronize is one stream wait (no blocking copy after it) */
     if (c->h_counters_dev && !c->info.lists_rebuilt) {
-        /* counters to the host and zeroed for the next render, in one kernel */
-        const int ek = rt_launch_counters_out(c->d_counters, c->h_counters_dev, (uint32_t)RT_COUNTER_WORDS,
+        /* counters to the host, added to the running totals and zeroed for the next render, in one kernel */
+        const int ek = rt_launch_counters_out(c->d_counters, c->h_counters_dev, c->d_totals, (uint32_t)RT_COUNTER_WORDS,
                                               (uint32_t)((kCounterBytes + kWorkWords * sizeof(uint32_t)) / 8u), st);
         if (ek) return hip_fail(c, (hipError_t)ek, "counter hand-back");
         c->counters_zeroed = true;
     } else {
+        const int ek = rt_launch_counters_out(c->d_counters, nullptr, c->d_totals, (uint32_t)RT_COUNTER_WORDS, 0u, st);
+        if (ek) return hip_fail(c, (hipError_t)ek, "counter totals");
         HIPCHK(c, hipMemcpyAsync(c->h_counters, c->d_counters, kCounterBytes, hipMemcpyDeviceToHost, st));
     }
     if (c->info.lists_rebuilt)
         HIPCHK(c, hipMemcpyAsync(c->h_counters + RT_COUNTER_WORDS, c->d_list_alloc, sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipEventRecord(c->ev_done, st));
     c->sync_stream = st;
     c->have_timing = true;
     c->last_out = dout;
@@ -1768,6 +1783,41 @@ try {
         snprintf(msg, sizeof(msg),
                  "sample-split seed pass: a defect guard fired (flags 0x%x: 1 record index, 2 group stack, 4 round "
                  "bound); the frame is invalid (RT_SPLIT=0 renders whole pixels)",
+                 (unsigned)h[RT_CNT_GUARD]);
+        return fail(c, RT_ERR_STATE, msg);
+    }
+    return RT_OK;
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
+
+int rt_counter_totals(rt_ctx *c, rt_counters *sum, uint64_t *renders, int reset)
+try {
+    if (!c || !sum) return RT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->sync_stream && c->sync_stream != c->stream) HIPCHK(c, hipStreamSynchronize(c->sync_stream));
+    unsigned long long h[RT_COUNTER_WORDS + 1];
+    HIPCHK(c, hipMemcpy(h, c->d_totals, sizeof(h), hipMemcpyDeviceToHost));
+    if (reset) HIPCHK(c, hipMemset(c->d_totals, 0, sizeof(h)));
+    *sum = rt_counters{};
+    sum->rays_closest = h[0];
+    sum->rays_shadow = h[1];
+    sum->nodes_visited = h[2];
+    sum->tris_tested = h[3];
+    sum->leaves_visited = h[4];
+    sum->lane_slots = h[5];
+    sum->clocks_traversal = h[6] / 64;
+    sum->clocks_total = h[7] / 64;
+    sum->rays_skipped = h[RT_CNT_SKIPPED];
+    sum->clocks_shade = h[RT_CNT_SHADE] / 64;
+    sum->pixel_clocks_max = h[10];
+    sum->pixel_rays_max = h[11];
+    sum->pixel_steps_max = h[12];
+    if (renders) *renders = h[RT_COUNTER_WORDS];
+    if (h[RT_CNT_GUARD]) {
+        char msg[160];
+        snprintf(msg, sizeof(msg),
+                 "rt_counter_totals: a sample-split seed pass defect guard fired in one of the renders (flags 0x%x); "
+                 "those frames are invalid",
                  (unsigned)h[RT_CNT_GUARD]);
         return fail(c, RT_ERR_STATE, msg);
     }
@@ -1947,7 +1997,8 @@ try {
                 }
             }
         c->counters_zeroed = false; /* this trace leaves its counts there */
-        if (c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), c->stream);
+        if (c->sync_stream && c->sync_stream != c->stream) e = hipStreamWaitEvent(c->stream, c->ev_done, 0);
+        if (e == hipSuccess && c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), c->stream);
         if (e == hipSuccess) {
             const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,
                                                 cap, d_idx, d_t, c->counting ? c->d_counters : nullptr, c->stream);

@@ -285,8 +285,8 @@ enum { RT_TRAV_LINEAR = 0, RT_TRAV_BVH4 = 2, RT_TRAV_BVH4Q = 4 };
 int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, void *stream);
 /* a render's counters into the host's mapped pinned copy, then the counters and queue cursors
    zeroed for the next render (n_zero 64-bit words from dev) */
-int rt_launch_counters_out(unsigned long long *dev, unsigned long long *host_mapped, uint32_t n_cnt, uint32_t n_zero,
-                           void *stream);
+int rt_launch_counters_out(unsigned long long *dev, unsigned long long *host_mapped, unsigned long long *totals,
+                           uint32_t n_cnt, uint32_t n_zero, void *stream);
 /* Sample-split renders: the seed pass (grid a.split_seed_blocks, cursor a.split_counter reset
    first) and the in-order sums; rt_launch_tris runs the chunk tasks (a.split_chunks > 0). */
 int rt_launch_split_seeds(const RtTriLaunch &a, void *stream);

@@ -1875,7 +1875,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     uint32_t pix_rt0 = 0; /* pixel start (s_memrealtime), RT_PIXEL_STATS diagnostics */
     uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
     /* the multi-head queue (mq_take: launches of 64-item groups with batched takes) */
-    const bool multi_q = MQ; /* (launched so only with queue_batch > 0, never for exact takes or long chains) */
+    const bool multi_q = MQ; /* multi-head queue: short frames' batched takes, long tasks' exact takes (batch 0)
+                                and a split tile's mesh chunk tasks; never for RT_SPLIT_BOX launches */
     uint32_t qs = (blockIdx.x % RT_QHEADS) << 4;
     /* the wave's loop iterations (wave-uniform): a whole pixel's take and finish iterations go to
        pixel_iter, the measured cost the view's next schedule sorts by (rt_sched_order_measured) */
@@ -3141,22 +3142,36 @@ int rt_launch_tris(const RtTriLaunch &a, int trav, bool count, int grid_blocks, 
 /* The end of a render: its counters (n_cnt words) written straight into the host's pinned, mapped
    copy, and the counters and queue cursors (n_zero words from `dev`, the counters first) zeroed for
    the next render — one small kernel on the render's stream instead of a copy-engine transfer
-   plus a fill at the next render's start. */
+   plus a fill at the next render's start.  `totals` (RT_COUNTER_WORDS + 1 words, device) keeps the
+   context's running totals over renders, whose counters are otherwise overwritten render by
+   render when renders are enqueued back to back (rt_counter_totals): sums for the summed counters
+   and the repair count, maxima for the per-pixel maxima, the OR of the guard words, and the
+   number of renders in the last word.  host == nullptr: totals only (the copy-engine path). */
 __global__ __launch_bounds__(256) void k_counters_out(unsigned long long *__restrict__ dev,
-                                                      unsigned long long *__restrict__ host, uint32_t n_cnt,
+                                                      unsigned long long *__restrict__ host,
+                                                      unsigned long long *__restrict__ totals, uint32_t n_cnt,
                                                       uint32_t n_zero)
 {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i < n_cnt) host[i] = dev[i];
+    if (i < n_cnt) {
+        const unsigned long long v = dev[i];
+        if (host) host[i] = v;
+        if (totals) {
+            if (i < RT_N_SUM_COUNTERS || i == RT_CNT_REPAIR) totals[i] += v;
+            else if (i == RT_CNT_GUARD) totals[i] |= v;
+            else totals[i] = totals[i] > v ? totals[i] : v;
+        }
+    }
+    if (totals && i == 0) totals[RT_COUNTER_WORDS] += 1ull;
     if (i < n_zero) dev[i] = 0ull;
 }
 
-int rt_launch_counters_out(unsigned long long *dev, unsigned long long *host_mapped, uint32_t n_cnt, uint32_t n_zero,
-                           void *stream)
+int rt_launch_counters_out(unsigned long long *dev, unsigned long long *host_mapped, unsigned long long *totals,
+                           uint32_t n_cnt, uint32_t n_zero, void *stream)
 {
     const uint32_t n = n_cnt > n_zero ? n_cnt : n_zero;
     hipLaunchKernelGGL(k_counters_out, dim3((n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream, dev, host_mapped,
-                       n_cnt, n_zero);
+                       totals, n_cnt, n_zero);
     return (int)hipGetLastError();
 }
 

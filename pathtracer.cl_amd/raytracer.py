@@ -243,6 +243,18 @@ class RayTracer:
         self._check(self._lib.rt_get_counters(self._h, ctypes.byref(c)), "rt_get_counters")
         return {f: getattr(c, f) for f, _ in _abi.RtCounters._fields_}
 
+    def counterTotals(self, reset: bool = True) -> dict:
+        """rt_counter_totals: the counters summed over every render since the last reset (waits for
+        the renders; frames enqueued back to back each add their own counts), with `renders` = how
+        many renders they cover.  Raises if a defect guard fired in any of them."""
+        c = _abi.RtCounters()
+        n = ctypes.c_uint64(0)
+        self._check(self._lib.rt_counter_totals(self._h, ctypes.byref(c), ctypes.byref(n), int(bool(reset))),
+                    "rt_counter_totals")
+        d = {f: getattr(c, f) for f, _ in _abi.RtCounters._fields_}
+        d["renders"] = n.value
+        return d
+
     def lastKernelMs(self) -> float:
         ms = ctypes.c_float()
         self._check(self._lib.rt_last_kernel_ms(self._h, ctypes.byref(ms)), "rt_last_kernel_ms")

@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--sample-rate", type=int, default=None)
     ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--partition", default="balanced", choices=["balanced", "interleaved"],
+                    help="N > 1 strong scaling: the row stripes dealt to ranks by their probed cost (rt_partition_stripes, "
+                         "LPT; the default) or round-robin")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="N > 1: strong (default) = one frame split into row-stripe tiles across ranks, gathered "
                          "to rank 0 over RCCL; weak = one full frame per rank (turntable views 3 degrees apart), "
@@ -228,8 +231,13 @@ def main():
         mesh_info["gen_seconds"] = round(t1 - t0, 3)
 
     n_ranks = 1 if frames_per_rank else world  # ranks sharing one frame
-    tile = (args.stripe, n_ranks, rank) if n_ranks > 1 else None
-    rows = ptdist.max_tile_rows(H, args.stripe, n_ranks) if n_ranks > 1 else H
+    # the stripes' owners: by probed cost (every rank computes the same map from the same view) for
+    # triangle frames, round-robin for the progressive sphere frames (their seed-row halo)
+    owner = None
+    if n_ranks > 1 and args.partition == "balanced" and kernel == pt.RayTracer.KERNEL_TRIS:
+        owner = rt.partitionStripes(W, H, args.stripe, n_ranks)
+    tile = (args.stripe, n_ranks, rank, owner) if n_ranks > 1 else None
+    rows = ptdist.max_tile_rows(H, args.stripe, n_ranks, owner) if n_ranks > 1 else H
     out = torch.zeros(rows * W * 4, dtype=torch.float32, device=f"cuda:{device}")
 
     Wp, Hp = sc.padded_dims(W, H)
@@ -257,6 +265,7 @@ def main():
         err = None
         try:
             comm = ptdist.NativeComm.from_torch(device)
+            comm.set_partition(args.partition == "balanced")
         except Exception as e:  # noqa: BLE001 - reported in the line
             err = f"{type(e).__name__}: {e}"
         ok = torch.tensor([0 if err else 1], dtype=torch.int64, device=f"cuda:{device}")
@@ -284,7 +293,7 @@ def main():
         frame_no[0] += 1
         c = rt.counters()
         if n_ranks > 1:
-            ptdist.gather_frame(out, H, W, args.stripe)
+            ptdist.gather_frame(out, H, W, args.stripe, owner=owner)
         elif frames_per_rank:
             ptdist.gather_frames(out)
         return c["rays_closest"] + c["rays_shadow"]
@@ -403,7 +412,7 @@ def main():
     sharded = None
     if n_ranks > 1:
         sharded = verify_sharded(rt, pt, sc, ptdist, comm, dist, W, H, Wp, Hp, kernel, args.stripe, n_ranks, rank,
-                                 device, out, frame_full if comm is not None else None)
+                                 device, out, frame_full if comm is not None else None, owner)
 
     if rank != 0:
         if comm is not None:
@@ -421,7 +430,7 @@ def main():
     k_ms = float(np.mean([m for _, m in split_ms]))
     rays_cnt = cnt["rays_closest"] + cnt["rays_shadow"]
     workload = workload_name(cfg, n_tris, W, H, sr, args.traversal, args.builder)
-    pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0)) if n_ranks > 1 else H)
+    pix = W * (len(ptdist.tile_rows(H, args.stripe, n_ranks, 0, owner)) if n_ranks > 1 else H)
     roofline = roofline_block(pt, kernel, cnt, args.traversal, pix, k_ms, workload, n_ranks, chain, rays_cnt,
                               frame_ms, pre_ms)
 
@@ -475,7 +484,7 @@ def main():
         "config": {"workload": workload,
                    "W": W, "H": H, "spp": sr * sr, "n_tris": n_tris,
                    "parallelism": ((f"frames x{world} (one turntable view per rank)" if frames_per_rank
-                                    else f"row-stripes({args.stripe})x{world}")
+                                    else f"row-stripes({args.stripe}, {args.partition if owner is not None or comm else 'interleaved'})x{world}")
                                    + ((" + librtmi rt_comm (RCCL send/recv gather)" if comm is not None
                                        else " + rccl gather (torch.distributed)"
                                        if os.environ.get("BENCH_DIST_BACKEND", "nccl") == "nccl"
@@ -550,7 +559,7 @@ def interactive_cost(rt, step, cam_setup, azimuth, device, dist):
 
 
 def verify_sharded(rt, pt, sc, ptdist, comm, dist, W, H, Wp, Hp, kernel, stripe, n_ranks, rank, device, out,
-                   frame_full):
+                   frame_full, owner=None):
     """The N > 1 line checks itself (collective; untimed, after the timed steps): every rank
     takes the same seed planes (the glibc rand() stream from its start), renders its stripes and
     the frame is gathered through the same path as the timed step (rt_comm_render, or the
@@ -566,9 +575,10 @@ def verify_sharded(rt, pt, sc, ptdist, comm, dist, W, H, Wp, Hp, kernel, stripe,
         comm.render(rt, frame_full, W, H, 0, kernel, stripe=stripe)
         gathered = frame_full.cpu().numpy().reshape(-1) if rank == 0 else None
         ranks = comm.count()
+        owner = comm.last_partition()
     else:
-        rt.rayTrace(out, W, H, 0, kernel=kernel, tile=(stripe, n_ranks, rank))
-        g = ptdist.gather_frame(out, H, W, stripe)
+        rt.rayTrace(out, W, H, 0, kernel=kernel, tile=(stripe, n_ranks, rank, owner))
+        g = ptdist.gather_frame(out, H, W, stripe, owner=owner)
         gathered = g.cpu().numpy().reshape(-1) if rank == 0 else None
         ranks = dist.get_world_size()
     seeds = torch.from_numpy(rt.getSeeds().view(np.int32).copy())
@@ -586,11 +596,14 @@ def verify_sharded(rt, pt, sc, ptdist, comm, dist, W, H, Wp, Hp, kernel, stripe,
     plane = Wp * Hp
     for r in range(n_ranks):
         got = bucket[r].cpu().numpy().view(np.uint32)
-        rows = ptdist.tile_rows(H, stripe, n_ranks, r)
+        rows = ptdist.tile_rows(H, stripe, n_ranks, r, owner)
         sl = (rows[:, None] * Wp + np.arange(W)[None, :]).reshape(-1)
         seeds_ok &= bool(np.array_equal(got[sl], single[sl]) and np.array_equal(got[plane + sl], single[plane + sl]))
     return {"gathered_bit_exact": bool(np.array_equal(gathered.view(np.uint32), full.view(np.uint32))),
             "gathered_seeds_bit_exact": bool(seeds_ok), "ranks": int(ranks),
+            "partition": ("owner map (rt_partition_stripes: probed stripe costs, LPT), rows per rank "
+                          + str([len(ptdist.tile_rows(H, stripe, n_ranks, r, owner)) for r in range(n_ranks)])
+                          if owner is not None else "interleaved stripes"),
             "gathered_check": "frame from the initial glibc rand() seeds gathered through the timed path == "
                               "rank 0's single-GPU render of the same seeds (bits), seed rows per rank likewise"}
 

@@ -65,13 +65,17 @@ enum {
 };
 
 /* Row-stripe tile of the frame owned by one rank (multi-GPU sharding).
-   Rows y with (y / stripe_rows) % n_ranks == rank are rendered, compacted in
-   increasing y into `out` (rt_tile_rows() rows of W pixels).  Seeds are always
-   indexed in the global padded frame (raytracer.cl:207-209).  NULL = full frame. */
+   The frame's rows are cut into ceil(H / stripe_rows) stripes; stripe s belongs to rank
+   stripe_owner[s], or, with stripe_owner NULL, to rank s % n_ranks (interleaved).  A rank's
+   rows are rendered compacted in increasing y into `out` (rt_tile_rows() rows of W pixels).
+   Seeds are always indexed in the global padded frame (raytracer.cl:207-209), so any
+   partition renders the same bits.  NULL tile = full frame.  rt_partition_stripes makes a
+   cost-balanced owner map. */
 typedef struct rt_tile {
     uint32_t stripe_rows;
     uint32_t n_ranks;
     uint32_t rank;
+    const uint32_t *stripe_owner; /* NULL, or ceil(H / stripe_rows) owners, each < n_ranks */
 } rt_tile;
 
 /* Ray accounting: one closest-hit query or one any-hit (shadow) query = 1 ray. */
@@ -184,6 +188,18 @@ int rt_synchronize(rt_ctx *ctx);
 int rt_read(rt_ctx *ctx, float *host, size_t n_floats);
 /* Rows of `height` owned by `tile` (NULL: height). */
 uint32_t rt_tile_rows(uint32_t height, const rt_tile *tile);
+/* Cost-balanced partition of a W x H raytrace_tris frame's row stripes over n_ranks for the
+   context's current camera, mesh and lights (the multi-GPU split; the reference renders on one
+   device, RayTracerCL.cpp:217-307).  A probe of the whole frame — one camera ray per pixel
+   through the compressed tree, and its shadow rays — counts per stripe the pixels whose camera
+   ray misses the mesh (box pixels: the long serial chains of a tile) and the
+   probe's traversal steps of the others; the stripes are dealt largest cost first to the least
+   loaded rank (LPT; ties to the lower stripe and rank index).  Deterministic: every rank
+   computes the same map from the same scene.  Cached per view (camera, mesh, lights, frame
+   shape).  owner: ceil(H / stripe_rows) entries.  *recomputed (may be NULL) = 1 when the probe
+   ran, 0 when the cached map was returned. */
+int rt_partition_stripes(rt_ctx *ctx, uint32_t width, uint32_t height, uint32_t stripe_rows, uint32_t n_ranks,
+                         uint32_t *owner, int *recomputed);
 
 /* ---- instrumentation ---- */
 int rt_get_counters(const rt_ctx *ctx, rt_counters *out); /* of the last completed render (or counting rt_trace_rays call) */
@@ -286,22 +302,26 @@ const char *rt_comm_last_error(const rt_comm *comm);
 /* ncclCommCount (rccl.h:378): ranks in the communicator as RCCL sees them. */
 int rt_comm_count(const rt_comm *comm, int *n_ranks);
 /* Frame assembly (collective): every rank passes its compact tile (device pointer,
-   rt_tile_rows(H, {stripe, n_ranks, rank}) rows of W RGBA32F pixels); `root` receives
-   them with grouped ncclSend/ncclRecv (one point-to-point xGMI transfer per sender)
-   and scatters the stripes into `frame_dev` (device, W*H*4 floats; others: ignored). */
+   rt_tile_rows(H, {stripe, n_ranks, rank, stripe_owner}) rows of W RGBA32F pixels); `root`
+   receives them with grouped ncclSend/ncclRecv (one point-to-point xGMI transfer per sender)
+   and scatters the stripes into `frame_dev` (device, W*H*4 floats; others: ignored).
+   stripe_owner: the partition the tiles were rendered with (NULL: interleaved). */
 int rt_comm_gather_frame(rt_comm *comm, const float *tile_dev, float *frame_dev, uint32_t width, uint32_t height,
-                         uint32_t stripe_rows, int root);
+                         uint32_t stripe_rows, const uint32_t *stripe_owner, int root);
 /* Device-side assembly on one GPU: n_ranks compact tiles (device pointers, rank
    order) scattered into frame_dev (the root's step of rt_comm_gather_frame). */
 int rt_assemble_tiles(const float *const *tiles_dev, uint32_t n_ranks, uint32_t width, uint32_t height,
-                      uint32_t stripe_rows, float *frame_dev, int device);
+                      uint32_t stripe_rows, const uint32_t *stripe_owner, float *frame_dev, int device);
 /* Seed-row halo plan (host only).  writer[Hpad]: last rank that wrote each seed row
    (-1: nobody, the initial seeds are identical on every rank).  Before a raytrace
-   frame with row shift `progressive`, lists the moves (src rank, dst rank, seed row)
-   that bring every row a rank reads up to date; then records the frame's writes in
-   writer.  Capacity of the three output arrays: height entries. */
+   frame with row shift `progressive` under the partition (stripe_rows, n_ranks,
+   stripe_owner: NULL = interleaved), lists the moves (src rank, dst rank, seed row) that
+   bring every row a rank reads up to date — including rows whose stripe changed owner since
+   it was written; then records the frame's writes in writer.  Capacity of the three output
+   arrays: height entries. */
 int rt_seed_halo_plan(int32_t *writer, uint32_t height, uint32_t hpad, uint32_t stripe_rows, uint32_t n_ranks,
-                      uint32_t progressive, uint32_t *src, uint32_t *dst, uint32_t *rows, uint32_t *n_moves);
+                      const uint32_t *stripe_owner, uint32_t progressive, uint32_t *src, uint32_t *dst,
+                      uint32_t *rows, uint32_t *n_moves);
 /* One rank's side of a halo plan (host only): the rows `me` sends to each peer and receives
    from each peer, as one packed block per peer in peer order — send_rows holds the blocks to
    peers 0, 1, ... back to back (send_counts[p] rows to peer p), likewise recv_rows /
@@ -318,10 +338,20 @@ int rt_seed_halo_peer_blocks(const uint32_t *src, const uint32_t *dst, const uin
    which after progressive sphere frames another rank may have written last), then
    gathers the frame to `root` (frame_dev: device, W*H*4 floats on root).  Bit-identical
    to rt_render of the whole frame on one GPU.  Call rt_comm_reset_halo after replacing
-   a context's seeds (rt_set_seeds). */
+   a context's seeds (rt_set_seeds).  The stripes are dealt by the communicator's partition
+   (rt_comm_set_partition). */
 int rt_comm_render(rt_comm *comm, rt_ctx *ctx, float *frame_dev, uint32_t width, uint32_t height,
                    uint32_t progression, int kernel, uint32_t stripe_rows, int root);
 int rt_comm_reset_halo(rt_comm *comm);
+/* Partition of rt_comm_render's frames: RT_PARTITION_INTERLEAVED (stripe s to rank
+   s % n_ranks) or RT_PARTITION_BALANCED (the default: raytrace_tris frames by
+   rt_partition_stripes, computed by every rank for each new view and checked against the
+   root's with one broadcast; sphere frames stay interleaved).  A change of owner moves the
+   stripe's seed rows through the halo (rt_seed_halo_plan).  rt_comm_last_partition copies
+   the last frame's owner map (cap entries; *n = its stripes). */
+enum { RT_PARTITION_INTERLEAVED = 0, RT_PARTITION_BALANCED = 1 };
+int rt_comm_set_partition(rt_comm *comm, int mode);
+int rt_comm_last_partition(const rt_comm *comm, uint32_t *owner, uint32_t cap, uint32_t *n);
 
 #ifdef __cplusplus
 }

@@ -81,7 +81,23 @@ CAMERA_FLOATS = 16
 
 
 class RtTile(ctypes.Structure):
-    _fields_ = [("stripe_rows", ctypes.c_uint32), ("n_ranks", ctypes.c_uint32), ("rank", ctypes.c_uint32)]
+    """rt_tile: stripe s of the frame belongs to rank stripe_owner[s] (a uint32 array of
+    ceil(H / stripe_rows) entries), or with stripe_owner NULL to rank s % n_ranks."""
+    _fields_ = [("stripe_rows", ctypes.c_uint32), ("n_ranks", ctypes.c_uint32), ("rank", ctypes.c_uint32),
+                ("stripe_owner", ctypes.c_void_p)]
+
+
+def tile_struct(tile):
+    """RtTile from (stripe, n_ranks, rank) or (stripe, n_ranks, rank, owner), owner a uint32 array
+    (or None); returns (struct, the owner array it points into, to be kept alive)."""
+    if tile is None:
+        return None, None
+    stripe, n, r = (int(v) for v in tile[:3])
+    owner = tile[3] if len(tile) > 3 else None
+    if owner is None:
+        return RtTile(stripe, n, r, None), None
+    o = np.ascontiguousarray(owner, np.uint32)
+    return RtTile(stripe, n, r, o.ctypes.data), o
 
 
 class RtMeshStats(ctypes.Structure):
@@ -162,6 +178,7 @@ SIGNATURES = {
     "rt_render_async": (_i32, [_vp, _vp, _u32, _u32, _u32, _i32, ctypes.POINTER(RtTile), _i32, _vp]),
     "rt_synchronize": (_i32, [_vp]),
     "rt_tile_rows": (_u32, [_u32, ctypes.POINTER(RtTile)]),
+    "rt_partition_stripes": (_i32, [_vp, _u32, _u32, _u32, _u32, _vp, ctypes.POINTER(_i32)]),
     "rt_read": (_i32, [_vp, _vp, _sz]),
     "rt_get_counters": (_i32, [_vp, ctypes.POINTER(RtCounters)]),
     "rt_set_counting": (_i32, [_vp, _i32]),
@@ -185,13 +202,17 @@ SIGNATURES = {
     "rt_comm_destroy": (_i32, [_vp]),
     "rt_comm_last_error": (ctypes.c_char_p, [_vp]),
     "rt_comm_count": (_i32, [_vp, ctypes.POINTER(_i32)]),
-    "rt_comm_gather_frame": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32]),
-    "rt_assemble_tiles": (_i32, [_vp, _u32, _u32, _u32, _u32, _vp, _i32]),
-    "rt_seed_halo_plan": (_i32, [_vp, _u32, _u32, _u32, _u32, _u32, _vp, _vp, _vp, ctypes.POINTER(_u32)]),
+    "rt_comm_gather_frame": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _i32]),
+    "rt_assemble_tiles": (_i32, [_vp, _u32, _u32, _u32, _u32, _vp, _vp, _i32]),
+    "rt_seed_halo_plan": (_i32, [_vp, _u32, _u32, _u32, _u32, _vp, _u32, _vp, _vp, _vp, ctypes.POINTER(_u32)]),
     "rt_seed_halo_peer_blocks": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp]),
     "rt_comm_render": (_i32, [_vp, _vp, _vp, _u32, _u32, _u32, _i32, _u32, _i32]),
     "rt_comm_reset_halo": (_i32, [_vp]),
+    "rt_comm_set_partition": (_i32, [_vp, _i32]),
+    "rt_comm_last_partition": (_i32, [_vp, _vp, _u32, ctypes.POINTER(_u32)]),
 }
+RT_PARTITION_INTERLEAVED = 0
+RT_PARTITION_BALANCED = 1
 RT_COMM_ID_BYTES = 128
 
 _LIB = None

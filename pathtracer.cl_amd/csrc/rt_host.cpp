@@ -230,6 +230,17 @@ struct rt_ctx {
     int mesh_builder = RT_BUILD_HOST; /* builder of the current mesh */
     uint64_t mesh_serial = 0;
     size_t spill_entries = 0;
+    /* owner-map tiles (rt_tile.stripe_owner): the tile's frame stripes in order, on the device, and a
+       serial that changes with them (in the view / schedule keys) */
+    std::vector<uint32_t> stripe_map_h;
+    uint32_t *d_stripe_map = nullptr;
+    size_t stripe_map_cap = 0;
+    uint32_t stripe_map_serial = 0;
+    /* rt_partition_stripes: the last map and what it was computed for */
+    std::vector<uint32_t> part_key, part_owner;
+    uint32_t *d_part_probe = nullptr;
+    unsigned long long *d_part_cost = nullptr;
+    size_t part_probe_px = 0, part_cost_cap = 0;
 
     /* camera state (RayTracer.h:21-29) */
     float view[4][4]; /* viewMatrix, row-major; identity by default (gmtl) */
@@ -766,7 +777,7 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
        the compressed tree is probed: a key without it would hand a BVH4F / linear launch stale
        classes) */
     const uintptr_t np = reinterpret_cast<uintptr_t>(a.nodes);
-    std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, c->max_depth, (uint32_t)c->lights.size(),
+    std::vector<uint32_t> key = {a.W, a.H, hl, a.stripe, a.n_ranks, a.rank, a.map_key, c->max_depth, (uint32_t)c->lights.size(),
                                  (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32), (uint32_t)blocks,
                                  c->sample_rate, (uint32_t)(c->split + 1) | (uint32_t)c->split_spec << 8,
                                  (uint32_t)trav_kind(c), (uint32_t)np,
@@ -993,6 +1004,9 @@ try {
     free_dev(c->d_seeds);
     free_dev(c->d_counters); /* d_work lives in it */
     free_dev(c->d_totals);
+    free_dev(c->d_stripe_map);
+    free_dev(c->d_part_probe);
+    free_dev(c->d_part_cost);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     free_dev(c->d_stage);
@@ -1276,6 +1290,12 @@ uint32_t rt_tile_rows(uint32_t height, const rt_tile *t)
 {
     if (!t || t->n_ranks <= 1) return height;
     if (t->stripe_rows == 0 || t->rank >= t->n_ranks) return 0;
+    if (t->stripe_owner) { /* an owner map: the rank's stripes (only the frame's last can be short) */
+        uint32_t rows = 0;
+        for (uint32_t s = 0, y = 0; y < height; ++s, y += t->stripe_rows)
+            if (t->stripe_owner[s] == t->rank) rows += std::min(t->stripe_rows, height - y);
+        return rows;
+    }
     const uint32_t period = t->stripe_rows * t->n_ranks;
     const uint32_t full = height / period;
     uint32_t rows = full * t->stripe_rows;
@@ -1283,6 +1303,147 @@ uint32_t rt_tile_rows(uint32_t height, const rt_tile *t)
     const uint32_t start = t->rank * t->stripe_rows;
     if (rem > start) rows += std::min(rem - start, t->stripe_rows);
     return rows;
+}
+
+/* A box pixel's serial chain against a mesh pixel of the frame's mean probe steps, in the stripes'
+   cost (rt_partition_stripes).  From the 8-way dragon tiles (profiles/r06b/partition8.npz: rank
+   time against the rank's long chains and traversal steps, least squares): a long chain adds
+   3.5e-4 ms, a whole mesh pixel of the mean steps 6.2e-6 ms — about 55 of them. */
+static constexpr uint64_t kPartitionBoxWeight = 55;
+
+int rt_partition_stripes(rt_ctx *c, uint32_t W, uint32_t H, uint32_t stripe, uint32_t n, uint32_t *owner,
+                         int *recomputed)
+try {
+    if (!c || !owner || stripe == 0 || n == 0) return RT_ERR_ARG;
+    if (recomputed) *recomputed = 0;
+    const uint32_t ns = (H + stripe - 1) / stripe;
+    if (ns == 0) return RT_OK;
+    const int trav = trav_kind(c);
+    if (c->n_tris == 0 || trav != RT_TRAV_BVH4Q || n == 1) { /* nothing to probe (or one rank): interleaved */
+        for (uint32_t s = 0; s < ns; ++s) owner[s] = s % n;
+        return RT_OK;
+    }
+    rt_camera cam;
+    if (c->cam_override) cam = c->cam_explicit;
+    else camera_from_view(c->view, c->fov, W, &cam);
+    std::vector<uint32_t> key = {W, H, stripe, n, (uint32_t)c->mesh_serial, (uint32_t)(c->mesh_serial >> 32),
+                                 (uint32_t)c->lights.size()};
+    {
+        const uint32_t *cb = reinterpret_cast<const uint32_t *>(&cam);
+        key.insert(key.end(), cb, cb + sizeof(rt_camera) / 4);
+        for (const rt_sphere &L : c->lights) {
+            const uint32_t *lb = reinterpret_cast<const uint32_t *>(&L);
+            key.insert(key.end(), lb, lb + sizeof(rt_sphere) / 4);
+        }
+    }
+    if (key == c->part_key && c->part_owner.size() == ns) {
+        std::copy(c->part_owner.begin(), c->part_owner.end(), owner);
+        return RT_OK;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    if (c->sync_stream && c->sync_stream != st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_done, 0));
+    const size_t npx = (size_t)W * H;
+    if (c->part_probe_px < npx) {
+        HIPCHK(c, hipStreamSynchronize(st));
+        free_dev(c->d_part_probe);
+        c->d_part_probe = nullptr;
+        c->part_probe_px = 0;
+        HIPCHK(c, hipMalloc(&c->d_part_probe, npx * sizeof(uint32_t)));
+        c->part_probe_px = npx;
+    }
+    if (c->part_cost_cap < ns) {
+        HIPCHK(c, hipStreamSynchronize(st));
+        free_dev(c->d_part_cost);
+        c->d_part_cost = nullptr;
+        c->part_cost_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_part_cost, (size_t)ns * 2 * sizeof(unsigned long long)));
+        c->part_cost_cap = ns;
+    }
+    /* the probe of the whole frame: one camera ray per pixel (its centre) and its shadow rays */
+    RtTriLaunch a{};
+    a.nodes = trav_nodes(c);
+    a.tris = c->d_tris;
+    a.n_tris = c->n_tris;
+    a.lights = c->d_lights;
+    a.n_lights = (uint32_t)c->lights.size();
+    a.cam = cam;
+    a.W = W;
+    a.H = H;
+    a.Hl = H;
+    a.stripe = 1;
+    a.n_ranks = 1;
+    a.rank = 0;
+    a.stripe_map = nullptr;
+    a.probe_n = 1;
+    int blocks = 0;
+    if (const int r = grid_blocks(c, trav, false, RT_FORM_PLAIN, &blocks)) return r;
+    a.spill_cap = spill_cap(c);
+    if (a.spill_cap) {
+        HIPCHK(c, hipStreamSynchronize(st)); /* (a render in flight may use the spill area) */
+        if (const int r = ensure_spill(c, (size_t)blocks * 2 * RT_BLOCK * a.spill_cap)) return r;
+    }
+    a.spill = c->d_spill;
+    int e = rt_launch_probe_cost(a, blocks, c->d_part_probe, st);
+    if (!e) e = rt_launch_stripe_costs(c->d_part_probe, W, H, stripe, 1u, c->d_part_cost, st);
+    if (e) return hip_fail(c, (hipError_t)e, "partition probe");
+    std::vector<unsigned long long> h((size_t)ns * 2);
+    HIPCHK(c, hipMemcpyAsync(h.data(), c->d_part_cost, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    /* a stripe's cost in probe steps: its mesh pixels' steps + its box pixels at kPartitionBoxWeight
+       mesh pixels of the frame's mean steps each (integers: every rank gets the same map) */
+    uint64_t mesh_px = 0, mesh_steps = 0;
+    for (uint32_t s = 0; s < ns; ++s) {
+        const uint64_t px = (uint64_t)W * std::min(stripe, H - s * stripe);
+        mesh_px += px - h[2 * s];
+        mesh_steps += h[2 * s + 1];
+    }
+    const uint64_t box_cost = kPartitionBoxWeight * (mesh_px ? (mesh_steps + mesh_px / 2) / mesh_px : 1u);
+    std::vector<uint64_t> cost(ns);
+    for (uint32_t s = 0; s < ns; ++s) cost[s] = h[2 * s] * box_cost + h[2 * s + 1] + 1u;
+    /* LPT: costliest stripe first (ties: lower index), to the least loaded rank (ties: lower rank) */
+    std::vector<uint32_t> order(ns);
+    for (uint32_t s = 0; s < ns; ++s) order[s] = s;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
+    std::vector<uint64_t> load(n, 0);
+    for (uint32_t s : order) {
+        uint32_t best = 0;
+        for (uint32_t r = 1; r < n; ++r)
+            if (load[r] < load[best]) best = r;
+        owner[s] = best;
+        load[best] += cost[s];
+    }
+    c->part_key = key;
+    c->part_owner.assign(owner, owner + ns);
+    if (recomputed) *recomputed = 1;
+    return RT_OK;
+} RT_CATCH(c ? &const_cast<rt_ctx *>(c)->err : nullptr)
+
+/* An owner-map tile's frame stripes, in tile order, on the device (RtTriLaunch::stripe_map);
+   re-uploaded (after the stream's earlier renders) only when they change. */
+static int upload_stripe_map(rt_ctx *c, uint32_t H, const rt_tile *t, hipStream_t st)
+{
+    const uint32_t ns = (H + t->stripe_rows - 1) / t->stripe_rows;
+    std::vector<uint32_t> mine;
+    for (uint32_t s = 0; s < ns; ++s) {
+        if (t->stripe_owner[s] >= t->n_ranks) return fail(c, RT_ERR_ARG, "stripe owner out of range");
+        if (t->stripe_owner[s] == t->rank) mine.push_back(s);
+    }
+    if (mine == c->stripe_map_h && c->d_stripe_map) return RT_OK;
+    HIPCHK(c, hipStreamSynchronize(st)); /* earlier renders on this stream read the old map */
+    if (c->sync_stream && c->sync_stream != st) HIPCHK(c, hipStreamSynchronize(c->sync_stream));
+    if (c->stripe_map_cap < std::max<size_t>(mine.size(), 1)) {
+        free_dev(c->d_stripe_map);
+        c->d_stripe_map = nullptr;
+        c->stripe_map_cap = 0;
+        HIPCHK(c, hipMalloc(&c->d_stripe_map, std::max<size_t>(mine.size(), 1) * sizeof(uint32_t)));
+        c->stripe_map_cap = std::max<size_t>(mine.size(), 1);
+    }
+    if (!mine.empty())
+        HIPCHK(c, hipMemcpy(c->d_stripe_map, mine.data(), mine.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->stripe_map_h = std::move(mine);
+    ++c->stripe_map_serial;
+    return RT_OK;
 }
 
 int rt_render_async(rt_ctx *c, float *out, uint32_t W, uint32_t H, uint32_t prog, int kernel, const rt_tile *tile,
@@ -1360,6 +1521,15 @@ try {
     c->counters_zeroed = false;
     const uint32_t stripe = tile ? tile->stripe_rows : 1u, nr = tile ? std::max(tile->n_ranks, 1u) : 1u,
                    rk = tile ? tile->rank : 0u;
+    /* an owner-map tile: its stripes' frame indices on the device (the view and schedule keys
+       carry the map's serial) */
+    const uint32_t *smap = nullptr;
+    if (tile && nr > 1 && tile->stripe_owner) {
+        const int r = upload_stripe_map(c, H, tile, st);
+        if (r != RT_OK) return r;
+        smap = c->d_stripe_map;
+    }
+    const uint32_t map_key = smap ? c->stripe_map_serial : 0u;
     int e = 0;
     if (kernel == RT_KERNEL_TRIS) {
         RtTriLaunch a{};
@@ -1383,6 +1553,8 @@ try {
         a.stripe = stripe;
         a.n_ranks = nr;
         a.rank = rk;
+        a.stripe_map = smap;
+        a.map_key = map_key;
         a.work_counter = c->d_work;
         a.counters = c->d_counters;
         const int trav = trav_kind(c);
@@ -1573,7 +1745,7 @@ try {
         list_cap = std::min<uint64_t>(list_cap, kept < (1ull << 28) ? (1ull << 28) - 8 - kept : 0);
         /* the view the lists (and the schedule) are a function of */
         const uintptr_t np4 = reinterpret_cast<uintptr_t>(c->d_nodes4);
-        std::vector<uint32_t> view = {W, H, hl, stripe, nr, rk, (uint32_t)trav, (uint32_t)c->mesh_serial,
+        std::vector<uint32_t> view = {W, H, hl, stripe, nr, rk, map_key, (uint32_t)trav, (uint32_t)c->mesh_serial,
                                       (uint32_t)(c->mesh_serial >> 32), (uint32_t)np4, (uint32_t)((uint64_t)np4 >> 32)};
         {
             const uint32_t *cb = reinterpret_cast<const uint32_t *>(&c->cam);
@@ -1714,6 +1886,7 @@ try {
         a.stripe = stripe;
         a.n_ranks = nr;
         a.rank = rk;
+        a.stripe_map = smap;
         a.counters = c->d_counters;
         HIPCHK(c, hipEventRecord(c->ev0, st));
         HIPCHK(c, hipEventRecord(c->evm, st));

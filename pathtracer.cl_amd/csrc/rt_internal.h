@@ -148,6 +148,9 @@ struct RtTriLaunch {
     uint32_t W, H, Wpad, Hpad, Hl;
     uint32_t sample_rate, max_depth, progressive;
     uint32_t stripe, n_ranks, rank;
+    const uint32_t *stripe_map; /* tile-local stripe -> the frame's stripe (an owner-map partition,
+                                   rt_tile.stripe_owner); NULL: interleaved, (yl / stripe) * n_ranks + rank */
+    uint32_t map_key;           /* host only: the serial of stripe_map's contents (0: none), in the schedule key */
     uint32_t *work_counter;
     unsigned long long *counters; /* [RT_COUNTER_WORDS]: the counters, then the guard word (RT_CNT_GUARD) */
     int32_t *spill;      /* per-lane stack overflow (4-wide traversal), spill_cap entries per lane */
@@ -275,6 +278,7 @@ struct RtSphLaunch {
     uint32_t W, H, Wpad, Hpad, Hl;
     uint32_t sample_rate, max_depth, progressive;
     uint32_t stripe, n_ranks, rank;
+    const uint32_t *stripe_map; /* as RtTriLaunch::stripe_map */
     unsigned long long *counters;
 };
 
@@ -303,6 +307,11 @@ int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint3
 /* Scheduling probe: per pixel the mesh hits of a grid of probe rays and the traversal steps of
    their queries (rt_kernels.hip). */
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream);
+/* Per stripe of stripe_rows rows of a W x H probe (rt_launch_probe_cost over the whole frame, pn2 rays
+   per pixel): out[2 s] = pixels with a probe ray that missed the mesh, out[2 s + 1] = the probe steps
+   of the others (rt_partition_stripes) */
+int rt_launch_stripe_costs(const uint32_t *probe, uint32_t W, uint32_t H, uint32_t stripe_rows, uint32_t pn2,
+                           unsigned long long *out, void *stream);
 /* The pixel-queue schedule from the probe, on the device (rt_sched.hip): LPT tile order, box
    flags and their exclusive scan, pixel classes with the long chains' slots. */
 struct RtSchedScratch {

@@ -687,10 +687,14 @@ __device__ __forceinline__ V3 camera_dir(const rt_camera &cam, float a, float b)
     return v3(x / len, y / len, z / len);
 }
 
-__device__ __forceinline__ uint32_t global_row(uint32_t yl, uint32_t stripe, uint32_t n_ranks, uint32_t rank)
+/* The frame row of a tile's row yl: the interleaved partition's formula, or the owner map's stripe
+   list (rt_tile.stripe_owner; only a frame's last stripe can be short, and it is its owner's last) */
+template <class L>
+__device__ __forceinline__ uint32_t global_row(const L &a, uint32_t yl)
 {
-    if (n_ranks <= 1) return yl;
-    return ((yl / stripe) * n_ranks + rank) * stripe + (yl % stripe);
+    if (a.stripe_map) return a.stripe_map[yl / a.stripe] * a.stripe + yl % a.stripe;
+    if (a.n_ranks <= 1) return yl;
+    return ((yl / a.stripe) * a.n_ranks + a.rank) * a.stripe + (yl % a.stripe);
 }
 
 /* A pixel's camera-ray candidate list (k_pixel_lists) packed in one word, read when the lane takes
@@ -1029,7 +1033,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         if (take && a.split_which == RT_SPLIT_MESH) take = a.pixel_class[(size_t)yl * a.W + x] == -1;
                     }
                     if (take) {
-                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                        const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
                         lpack = list_pack(a, x, yl, tiles_x);
@@ -1085,7 +1089,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 } else {
                     const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
                     const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
-                    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                    const uint32_t y = global_row(a, yl);
                     const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
                     qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
                     qd = camera_dir(a.cam, fa - hw, fb - hh);
@@ -1534,7 +1538,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                 pslot = a.split_seed_slot ? item : p;
                 x = p % a.W;
                 yl = p / a.W;
-                const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                 seed.x = a.seeds[slot];
                 seed.y = a.seeds[plane + slot];
                 sample = 0;
@@ -1626,7 +1630,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                     Seed sc = sl;
                     const uint32_t sx = s / a.sample_rate, sy = s % a.sample_rate;
                     const float fa = (float)x + strat_rand(sc, (int)sx, (int)a.sample_rate);
-                    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                    const uint32_t y = global_row(a, yl);
                     const float fb = (float)y + strat_rand(sc, (int)sy, (int)a.sample_rate);
                     const V3 o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
                     const V3 dd = camera_dir(a.cam, fa - hw, fb - hh);
@@ -1680,7 +1684,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                     const float qv = num / (float)a.sample_rate;
                     const float ua = __shfl(qv, gbase), ub = __shfl(qv, gbase + 1);
                     const float fa = (float)x + ua;
-                    const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+                    const uint32_t y = global_row(a, yl);
                     const float fb = (float)y + ub;
                     qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
                     qd = group_camera_dir(a.cam, fa - hw, fb - hh, sub, gbase);
@@ -2065,7 +2069,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         }
                         *dst = p;
                     }
-                    const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                    const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
                     if (a.pixel_iter) a.pixel_iter[a.W * a.Hl + yl * a.W + x] = RT_LPT_STEPS ? (uint32_t)pix_steps : it_wave;
@@ -2176,7 +2180,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     if (SPLIT && take && a.split_spec && a.split_which == RT_SPLIT_MESH) {
                         /* a speculated mesh pixel: the chunk's first seed jumped ahead from the
                            frame seed (split_spec_draws numbers per sample before it) */
-                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                        const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                         const uint32_t k = chunk * a.split_chunk * a.split_spec_draws;
                         seed.x = mwc_jump<36969u>(a.seeds[slot], k, a.split_spec_mul[2 * chunk]);
                         seed.y = mwc_jump<18000u>(a.seeds[plane + slot], k, a.split_spec_mul[2 * chunk + 1]);
@@ -2195,7 +2199,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         mode = M_NEWSAMPLE;
                         if (COUNT || RT_LPT_STEPS) pix_q = pix_steps = 0;
                     } else if (take) {
-                        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+                        const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
@@ -2241,7 +2245,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         if (mode == M_NEWSAMPLE) {
             const uint32_t sx = sample / a.sample_rate, sy = sample % a.sample_rate;
             const float fa = (float)x + strat_rand(seed, (int)sx, (int)a.sample_rate);
-            const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+            const uint32_t y = global_row(a, yl);
             const float fb = (float)y + strat_rand(seed, (int)sy, (int)a.sample_rate);
             qo = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
             qd = camera_dir(a.cam, fa - hw, fb - hh);
@@ -2499,7 +2503,7 @@ __global__ __launch_bounds__(RT_SPH_TILE * RT_SPH_TILE) void k_spheres(RtSphLaun
     const uint32_t yl = blockIdx.y * RT_SPH_TILE + (threadIdx.x / RT_SPH_TILE);
     unsigned long long n_closest = 0, n_shadow = 0, n_skipped = 0;
     if (x < a.W && yl < a.Hl) {
-        const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+        const uint32_t y = global_row(a, yl);
         const uint32_t plane = a.Wpad * a.Hpad;
         /* get_seed (raytracer.cl:20-24): rows shifted by `progressive`; raytrace_ss unshifted */
         const uint32_t slot = SS ? (y * a.Wpad + x) : (((y + a.progressive) % a.Hpad) * a.Wpad + x);
@@ -2621,7 +2625,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_probe_cost(RtTriLau
         const uint32_t p = r * stride + blockIdx.x * RT_BLOCK + threadIdx.x;
         const bool valid = p < npx;
         const uint32_t x = valid ? p % a.W : 0u, yl = valid ? p / a.W : 0u;
-        const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+        const uint32_t y = global_row(a, yl);
         const V3 o = v3(a.cam.position.x, a.cam.position.y, a.cam.position.z);
         uint32_t steps = 0, hits = 0;
         const uint32_t pn = a.probe_n;
@@ -2715,7 +2719,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_split_finish(RtTriLaunch a)
         }
         *dst = px;
         const uint32_t x = p % a.W, yl = p / a.W;
-        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+        const uint32_t slot = global_row(a, yl) * a.Wpad + x;
         const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)p * a.split_nseed + a.split_nseed - 1u];
         a.seeds[slot] = sd.x;
         a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
@@ -2771,7 +2775,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_split_finish_list(RtTriLaunch a)
         }
         *dst = px;
         const uint32_t x = p % a.W, yl = p / a.W;
-        const uint32_t slot = global_row(yl, a.stripe, a.n_ranks, a.rank) * a.Wpad + x;
+        const uint32_t slot = global_row(a, yl) * a.Wpad + x;
         const uint2 sd = reinterpret_cast<const uint2 *>(a.split_seed)[(size_t)(a.split_seed_slot ? i : p) * a.split_nseed + a.split_nseed - 1u];
         a.seeds[slot] = sd.x;
         a.seeds[a.Wpad * a.Hpad + slot] = sd.y;
@@ -2942,7 +2946,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
     uint32_t n = 0;
     bool ok = false;
     if (valid) {
-        const uint32_t y = global_row(yl, a.stripe, a.n_ranks, a.rank);
+        const uint32_t y = global_row(a, yl);
         /* a = fa - W/2 with fa in [x, x + 1] (the kernel's float subtraction, exact at these
            magnitudes), likewise b */
         const float ax = (float)x - ((float)a.W) / 2.0f, by = (float)y - ((float)a.H) / 2.0f;
@@ -3282,6 +3286,45 @@ int rt_launch_pixel_lists(const RtTriLaunch &a, const float *nodes4, const uint3
 int rt_launch_probe_cost(const RtTriLaunch &a, int grid_blocks, uint32_t *out, void *stream)
 {
     hipLaunchKernelGGL(k_probe_cost, dim3((unsigned)grid_blocks), dim3(RT_BLOCK), 0, (hipStream_t)stream, a, out);
+    return (int)hipGetLastError();
+}
+
+/* Per stripe of a whole-frame probe (rt_partition_stripes): one block per stripe, its pixels'
+   box flags and mesh-pixel steps summed over the block (integer sums: the same on every GPU). */
+__global__ __launch_bounds__(256) void k_stripe_costs(const uint32_t *__restrict__ probe, uint32_t W, uint32_t H,
+                                                      uint32_t stripe_rows, uint32_t pn2,
+                                                      unsigned long long *__restrict__ out)
+{
+    __shared__ unsigned long long s_box[256], s_steps[256];
+    const uint32_t s = blockIdx.x;
+    const uint32_t y0 = s * stripe_rows, y1 = min(H, y0 + stripe_rows);
+    unsigned long long box = 0, steps = 0;
+    for (uint32_t p = y0 * W + threadIdx.x; p < y1 * W; p += 256u) {
+        const uint32_t w = probe[p];
+        if ((w >> RT_PROBE_HIT_SHIFT) < pn2) ++box;
+        else steps += w & RT_PROBE_STEP_MASK;
+    }
+    s_box[threadIdx.x] = box;
+    s_steps[threadIdx.x] = steps;
+    __syncthreads();
+    for (uint32_t k = 128; k > 0; k >>= 1) {
+        if (threadIdx.x < k) {
+            s_box[threadIdx.x] += s_box[threadIdx.x + k];
+            s_steps[threadIdx.x] += s_steps[threadIdx.x + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[2 * s] = s_box[0];
+        out[2 * s + 1] = s_steps[0];
+    }
+}
+
+int rt_launch_stripe_costs(const uint32_t *probe, uint32_t W, uint32_t H, uint32_t stripe_rows, uint32_t pn2,
+                           unsigned long long *out, void *stream)
+{
+    const uint32_t ns = (H + stripe_rows - 1u) / stripe_rows;
+    hipLaunchKernelGGL(k_stripe_costs, dim3(ns), dim3(256), 0, (hipStream_t)stream, probe, W, H, stripe_rows, pn2, out);
     return (int)hipGetLastError();
 }
 

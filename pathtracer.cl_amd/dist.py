@@ -1,8 +1,11 @@
-"""Multi-GPU frame sharding: one process per GPU, interleaved row stripes, RCCL gather.
+"""Multi-GPU frame sharding: one process per GPU, row stripes, RCCL gather.
 
 Every pixel of raytrace_tris is independent (its own seed slot, its own read-modify-write
 of its output pixel — raytracer.cl:207-242), so a frame splits into row stripes dealt
-round-robin over ranks (load balance: the mesh sits mid-frame).  Each rank keeps a full
+over ranks: round-robin (interleaved), or by an owner map that balances the stripes'
+probed cost (RayTracer.partitionStripes, rt_partition_stripes: the long serial chains of
+the box pixels crowd the top of the dragon frame).  Every function below takes the
+partition as (stripe, n_ranks[, owner]).  Each rank keeps a full
 scene/BVH replica and the full seed planes, renders its rows into a compact local
 framebuffer (rt_tile), and the frame is assembled on the root with ONE collective: a
 gather of the compact tiles over RCCL (torch.distributed backend "nccl" = RCCL on ROCm),
@@ -26,17 +29,37 @@ from __future__ import annotations
 import numpy as np
 
 
-def tile_rows(height: int, stripe: int, n_ranks: int, rank: int) -> np.ndarray:
+def row_owner(height: int, stripe: int, n_ranks: int, owner=None) -> np.ndarray:
+    """Owner rank of every frame row: owner[y // stripe], or (y // stripe) % n_ranks."""
+    s = np.arange(height) // stripe
+    return s % n_ranks if owner is None else np.asarray(owner, np.int64)[s]
+
+
+def tile_rows(height: int, stripe: int, n_ranks: int, rank: int, owner=None) -> np.ndarray:
     """Global row indices owned by `rank`, in the order they are stored (rt_tile_rows)."""
     y = np.arange(height)
-    return y[(y // stripe) % n_ranks == rank]
+    return y[row_owner(height, stripe, n_ranks, owner) == rank]
 
 
-def max_tile_rows(height: int, stripe: int, n_ranks: int) -> int:
-    return max(len(tile_rows(height, stripe, n_ranks, r)) for r in range(n_ranks))
+def max_tile_rows(height: int, stripe: int, n_ranks: int, owner=None) -> int:
+    return max(len(tile_rows(height, stripe, n_ranks, r, owner)) for r in range(n_ranks))
 
 
-def assemble(tiles, height: int, width: int, stripe: int):
+def lpt_owner(costs, n_ranks: int) -> np.ndarray:
+    """The stripes dealt costliest first to the least-loaded rank (ties: the lower stripe index, the
+    lower rank) — the rule rt_partition_stripes applies to its probed costs."""
+    c = np.asarray(costs)
+    order = sorted(range(len(c)), key=lambda s: -c[s])  # stable: ties keep the lower index first
+    load = [0] * n_ranks
+    own = np.zeros(len(c), np.uint32)
+    for s in order:
+        r = min(range(n_ranks), key=lambda k: (load[k], k))
+        own[s] = r
+        load[r] += c[s]
+    return own
+
+
+def assemble(tiles, height: int, width: int, stripe: int, owner=None):
     """Scatter gathered compact tiles (rank order; each [>=rows_r, W, 4]) into a full
     [H, W, 4] frame.  Works on numpy arrays or torch tensors."""
     n = len(tiles)
@@ -48,7 +71,7 @@ def assemble(tiles, height: int, width: int, stripe: int):
 
         full = torch.empty((height, width, 4), dtype=first.dtype, device=first.device)
     for r, t in enumerate(tiles):
-        rows = tile_rows(height, stripe, n, r)
+        rows = tile_rows(height, stripe, n, r, owner)
         if len(rows) == 0:
             continue
         t = t.reshape(-1, width, 4)[: len(rows)]
@@ -61,7 +84,7 @@ def assemble(tiles, height: int, width: int, stripe: int):
     return full
 
 
-def gather_frame(local, height: int, width: int, stripe: int, group=None, root: int = 0):
+def gather_frame(local, height: int, width: int, stripe: int, group=None, root: int = 0, owner=None):
     """Gather every rank's compact tile to `root` with one torch.distributed.gather
     (RCCL over xGMI for CUDA tensors; gloo on CPU).  `local` is the rank's framebuffer
     padded to max_tile_rows rows.  Returns the assembled [H, W, 4] frame on root, else None."""
@@ -72,7 +95,7 @@ def gather_frame(local, height: int, width: int, stripe: int, group=None, root: 
     rank = dist.get_rank(group)
     if local.is_cuda and dist.get_backend(group) == "gloo":  # CPU rehearsal of the RCCL path
         local = local.cpu()
-    rows_max = max_tile_rows(height, stripe, world)
+    rows_max = max_tile_rows(height, stripe, world, owner)
     local = local.reshape(-1)[: rows_max * width * 4]
     if local.numel() != rows_max * width * 4:
         raise ValueError("local framebuffer must hold max_tile_rows rows")
@@ -80,7 +103,7 @@ def gather_frame(local, height: int, width: int, stripe: int, group=None, root: 
     dist.gather(local, gathered, dst=root, group=group)
     if rank != root:
         return None
-    return assemble([g.reshape(rows_max, width, 4) for g in gathered], height, width, stripe)
+    return assemble([g.reshape(rows_max, width, 4) for g in gathered], height, width, stripe, owner)
 
 
 def gather_frames(local, group=None, root: int = 0):
@@ -106,15 +129,18 @@ class SeedHalo:
     wrote it last (or nobody has: the initial seeds are identical everywhere).  Before a
     frame with row shift s, rank j needs rows (y + s) % Hpad for its pixel rows y < H;
     `plan(s)` lists, per (src, dst) rank pair, the rows dst must receive from their last
-    writer src.  `commit(s)` records the frame's writes."""
+    writer src.  `commit(s)` records the frame's writes.  `set_owner` changes the partition:
+    the next plan moves the rows whose stripe changed owner since they were written."""
 
-    def __init__(self, height: int, hpad: int, stripe: int, n_ranks: int):
+    def __init__(self, height: int, hpad: int, stripe: int, n_ranks: int, owner=None):
         if hpad < height:
             raise ValueError("Hpad < H")
         self.height, self.hpad, self.stripe, self.n_ranks = height, hpad, stripe, n_ranks
-        y = np.arange(height)
-        self.row_rank = (y // stripe) % n_ranks
+        self.set_owner(owner)
         self.writer = np.full(hpad, -1, np.int64)
+
+    def set_owner(self, owner=None) -> None:
+        self.row_rank = row_owner(self.height, self.stripe, self.n_ranks, owner)
 
     def _rows(self, shift: int) -> np.ndarray:
         return (np.arange(self.height) + int(shift)) % self.hpad
@@ -158,7 +184,8 @@ def exchange_seed_rows(plan: dict, pack, unpack, n_words_per_row: int, device=No
     return sum(len(r) for r, _ in recvs)
 
 
-def seed_halo_plan_native(writer: np.ndarray, height: int, hpad: int, stripe: int, n_ranks: int, shift: int):
+def seed_halo_plan_native(writer: np.ndarray, height: int, hpad: int, stripe: int, n_ranks: int, shift: int,
+                          owner=None):
     """rt_seed_halo_plan (librtmi, host only): the moves of SeedHalo.plan(shift) as
     (src, dst, row) arrays, then SeedHalo.commit(shift) applied to `writer` in place."""
     from . import _abi
@@ -169,8 +196,9 @@ def seed_halo_plan_native(writer: np.ndarray, height: int, hpad: int, stripe: in
     dst = np.empty(height, np.uint32)
     rows = np.empty(height, np.uint32)
     k = _abi.ctypes.c_uint32(0)
-    st = lib.rt_seed_halo_plan(_abi.ptr(w), height, hpad, stripe, n_ranks, shift, _abi.ptr(src), _abi.ptr(dst),
-                               _abi.ptr(rows), _abi.ctypes.byref(k))
+    o = None if owner is None else np.ascontiguousarray(owner, np.uint32)
+    st = lib.rt_seed_halo_plan(_abi.ptr(w), height, hpad, stripe, n_ranks, _abi.ptr(o), shift, _abi.ptr(src),
+                               _abi.ptr(dst), _abi.ptr(rows), _abi.ctypes.byref(k))
     if st != _abi.RT_OK:
         raise _abi.RtError(st, "rt_seed_halo_plan")
     writer[...] = w
@@ -281,11 +309,30 @@ class NativeComm:
         if st != self._abi.RT_OK:
             raise self._abi.RtError(st, f"{what}: {self._lib.rt_comm_last_error(self._h).decode()}")
 
-    def gather(self, tile, frame, width: int, height: int, stripe: int = 8, root: int = 0) -> None:
+    def gather(self, tile, frame, width: int, height: int, stripe: int = 8, root: int = 0, owner=None) -> None:
         """rt_comm_gather_frame: device tile (this rank's rows) -> device frame on root."""
         p = self._abi.ptr
-        self._check(self._lib.rt_comm_gather_frame(self._h, p(tile), p(frame), width, height, stripe, root),
+        o = None if owner is None else np.ascontiguousarray(owner, np.uint32)
+        self._check(self._lib.rt_comm_gather_frame(self._h, p(tile), p(frame), width, height, stripe, p(o), root),
                     "rt_comm_gather_frame")
+
+    def set_partition(self, balanced: bool) -> None:
+        """rt_comm_set_partition: rt_comm_render's triangle frames by the cost-balanced owner map
+        (rt_partition_stripes, the default) or interleaved stripes."""
+        mode = self._abi.RT_PARTITION_BALANCED if balanced else self._abi.RT_PARTITION_INTERLEAVED
+        self._check(self._lib.rt_comm_set_partition(self._h, mode), "rt_comm_set_partition")
+
+    def last_partition(self):
+        """rt_comm_last_partition: the owner map of the last rt_comm_render frame (None: interleaved)."""
+        n = self._abi.ctypes.c_uint32(0)
+        self._check(self._lib.rt_comm_last_partition(self._h, None, 0, self._abi.ctypes.byref(n)),
+                    "rt_comm_last_partition")
+        if not n.value:
+            return None
+        out = np.empty(n.value, np.uint32)
+        self._check(self._lib.rt_comm_last_partition(self._h, self._abi.ptr(out), n.value, self._abi.ctypes.byref(n)),
+                    "rt_comm_last_partition")
+        return out
 
     def render(self, rt, frame, width: int, height: int, progression: int, kernel: int, stripe: int = 8,
                root: int = 0) -> None:
@@ -315,13 +362,14 @@ class NativeComm:
             pass
 
 
-def assemble_native(tiles, height: int, width: int, stripe: int, frame, device: int = 0) -> None:
+def assemble_native(tiles, height: int, width: int, stripe: int, frame, device: int = 0, owner=None) -> None:
     """rt_assemble_tiles: the root's device-side scatter of compact tiles (device tensors,
     rank order) into `frame` (device, H*W*4 floats)."""
     from . import _abi
 
     arr = (_abi.ctypes.c_void_p * len(tiles))(*[t.data_ptr() for t in tiles])
-    st = _abi.load().rt_assemble_tiles(_abi.ctypes.addressof(arr), len(tiles), width, height, stripe,
+    o = None if owner is None else np.ascontiguousarray(owner, np.uint32)
+    st = _abi.load().rt_assemble_tiles(_abi.ctypes.addressof(arr), len(tiles), width, height, stripe, _abi.ptr(o),
                                        _abi.ptr(frame), device)
     if st != _abi.RT_OK:
         raise _abi.RtError(st, "rt_assemble_tiles")

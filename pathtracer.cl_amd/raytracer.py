@@ -190,8 +190,10 @@ class RayTracer:
 
     # ---- render (RayTracerCL::rayTrace) ---------------------------------------------------
     def rayTrace(self, out, width: int, height: int, progression: int, kernel: int = _abi.RT_KERNEL_SPHERES,
-                 tile: tuple[int, int, int] | None = None, stream=None, sync: bool = True, halo: bool = False) -> None:
+                 tile: tuple | None = None, stream=None, sync: bool = True, halo: bool = False) -> None:
         """Render into `out` (W*H*4 float32 — or tile rows*W*4 — numpy or torch CUDA tensor).
+        tile = (stripe_rows, n_ranks, rank) for interleaved stripes, or (stripe_rows, n_ranks,
+        rank, owner) with a per-stripe owner map (partitionStripes).
         halo=True: the caller keeps this tile's seed rows current (dist.SeedHalo), which
         permits progressive sphere frames on a tile."""
         self._sync_scene()
@@ -206,7 +208,7 @@ class RayTracer:
         else:
             if out.dtype != np.float32 or not out.flags["C_CONTIGUOUS"]:
                 raise ValueError("framebuffer must be a contiguous float32 array")
-        t = _abi.RtTile(*tile) if tile else None
+        t, _keep = _abi.tile_struct(tile)  # (_keep: the owner map the struct points into)
         rows = self._lib.rt_tile_rows(height, ctypes.byref(t) if t else None)
         need = int(width) * int(rows) * 4
         n = out.size if isinstance(out, np.ndarray) else out.numel()
@@ -233,6 +235,17 @@ class RayTracer:
 
     def synchronize(self) -> None:
         self._check(self._lib.rt_synchronize(self._h), "rt_synchronize")
+
+    def partitionStripes(self, width: int, height: int, stripe: int, n_ranks: int) -> np.ndarray:
+        """rt_partition_stripes: the cost-balanced owner of each of the frame's row stripes for the
+        current camera, mesh and lights (a whole-frame probe, LPT over the stripes; cached per view)."""
+        self._sync_scene()
+        ns = (int(height) + int(stripe) - 1) // int(stripe)
+        owner = np.empty(max(ns, 1), np.uint32)
+        made = ctypes.c_int(0)
+        self._check(self._lib.rt_partition_stripes(self._h, int(width), int(height), int(stripe), int(n_ranks),
+                                                   _abi.ptr(owner), ctypes.byref(made)), "rt_partition_stripes")
+        return owner[:ns]
 
     # ---- instrumentation ------------------------------------------------------------------
     def setCounting(self, enable: bool) -> None:

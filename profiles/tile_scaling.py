@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--stripe", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ns", default="1,2,4,8", help="rank counts to rehearse (1 is always timed: the reference)")
+    ap.add_argument("--partition", default="balanced", choices=["balanced", "interleaved"],
+                    help="the stripes' owners: rt_partition_stripes (probed cost, LPT; bench.py's default) or round-robin")
     args = ap.parse_args()
     import torch
     import ptload
@@ -43,11 +45,14 @@ def main():
     ptdist = ptload.submodule("dist")
     frame = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     ns = sorted({1} | {int(v) for v in args.ns.replace(":", ",").split(",")})
+    owners = {}
     for n in ns:
         times, repaired, longc, tiles = [], [], [], []
+        owner = rt.partitionStripes(W, H, args.stripe, n) if (n > 1 and args.partition == "balanced") else None
+        owners[n] = owner
         for r in range(n):  # every rank's tile: the slowest sets the N-GPU frame time
-            tile = (args.stripe, n, r) if n > 1 else None
-            rows = len(ptdist.tile_rows(H, args.stripe, n, r)) if n > 1 else H
+            tile = (args.stripe, n, r, owner) if n > 1 else None
+            rows = len(ptdist.tile_rows(H, args.stripe, n, r, owner)) if n > 1 else H
             buf = torch.zeros(rows * W * 4, dtype=torch.float32, device="cuda:0")
             best = 1e9
             for _ in range(args.reps):
@@ -60,6 +65,8 @@ def main():
             longc.append(int(info.get("pixels_long", 0)))
         info = rt.renderInfo()
         res[n] = {"max_ms": max(times), "min_ms": min(times), "ranks_timed": len(times),
+                  "partition": args.partition if n > 1 else None,
+                  "rows": [len(ptdist.tile_rows(H, args.stripe, n, r, owner)) for r in range(n)] if n > 1 else [H],
                   "rank_ms": [round(t, 3) for t in times], "split_chunks": info.get("split_chunks", 0),
                   "split_spec": info.get("split_spec", 0), "long_chains": longc, "repaired": repaired}
         if n > 1:
@@ -77,7 +84,7 @@ def main():
                     stage[off:off + t.numel()].copy_(t)
                     views.append(stage[off:off + t.numel()])
                     off += t.numel()
-                ptdist.assemble_native(views, H, W, args.stripe, frame)
+                ptdist.assemble_native(views, H, W, args.stripe, frame, owner=owner)
                 ev1.record()
                 torch.cuda.synchronize()
                 best = min(best, ev0.elapsed_time(ev1))
@@ -91,7 +98,7 @@ def main():
     # (the seed pass's rounds are reported apart)
     path = os.path.join(tempfile.gettempdir(), f"tile_stats_{os.getpid()}.bin")
     for n, r in ((1, 0), (8, 0), (8, 1)) if 8 in ns else ((1, 0),):
-        tile = (args.stripe, n, r) if n > 1 else None
+        tile = (args.stripe, n, r, owners.get(n)) if n > 1 else None
         os.environ["RT_PIXEL_STATS"] = path
         rt.setCounting(True)
         rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)
@@ -99,7 +106,8 @@ def main():
         info = rt.renderInfo()
         rt.setCounting(False)
         os.environ.pop("RT_PIXEL_STATS")
-        rows = rt._lib.rt_tile_rows(H, ctypes.byref(pt._abi.RtTile(*tile)) if tile else None)
+        t, _keep = pt._abi.tile_struct(tile)
+        rows = rt._lib.rt_tile_rows(H, ctypes.byref(t) if t else None)
         st = np.fromfile(path, np.uint32).reshape(rows * W, 8).astype(np.int64)
         os.remove(path)
         split = info.get("split_chunks", 0) > 0

@@ -111,6 +111,19 @@ int run_host()
     check(sum == 1080, "tile rows sum");
     t.rank = 5;
     check(rt_tile_rows(1080, &t) == 0, "bad tile rank");
+    { /* an owner map: 1083 rows = 135 full stripes + a 3-row one, dealt 2, 0, 1, 2, 0, 1, ... */
+        std::vector<uint32_t> own(136);
+        for (size_t s = 0; s < own.size(); ++s) own[s] = (uint32_t)((s + 2) % 3);
+        rt_tile m = {8, 3, 0, own.data()};
+        uint32_t rows = 0;
+        for (uint32_t k = 0; k < 3; ++k) {
+            m.rank = k;
+            rows += rt_tile_rows(1083, &m);
+        }
+        check(rows == 1083, "owner-map tile rows sum");
+        m.rank = 2; /* stripe 135 (3 rows) is owner (135 + 2) % 3 = 2's */
+        check(rt_tile_rows(1083, &m) == 45 * 8 + 3, "owner-map short stripe");
+    }
 
     /* synthetic mesh + the host BVH builder (and its input checks) */
     const uint32_t nt = 20000, nv = rt_mesh_vertex_count(nt);
@@ -152,8 +165,11 @@ int run_host()
         std::vector<uint32_t> src(hpad), dst(hpad), rows(hpad);
         for (uint32_t shift = 0; shift < 12; ++shift) {
             uint32_t k = 0;
-            check(rt_seed_halo_plan(writer.data(), H, hpad, stripe, n, shift, src.data(), dst.data(), rows.data(),
-                                    &k) == RT_OK,
+            /* odd shifts under an owner map (stripes dealt in reverse), even ones interleaved */
+            std::vector<uint32_t> own((H + stripe - 1) / stripe);
+            for (size_t s = 0; s < own.size(); ++s) own[s] = n - 1 - (uint32_t)(s % n);
+            check(rt_seed_halo_plan(writer.data(), H, hpad, stripe, n, (shift & 1) ? own.data() : nullptr, shift,
+                                    src.data(), dst.data(), rows.data(), &k) == RT_OK,
                   "halo plan");
             check(k <= hpad, "halo move count");
             for (uint32_t me = 0; me < n; ++me) {

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, H, W, stripe, frame_path, result_path):
+def _worker(rank, world, port, H, W, stripe, frame_path, result_path, owner=None):
     sys.path.insert(0, str(ROOT))
     import torch
     import torch.distributed as dist
@@ -38,19 +38,19 @@ def _worker(rank, world, port, H, W, stripe, frame_path, result_path):
 
     pdist = ptload.submodule("dist")
     full = np.load(frame_path)
-    rows = pdist.tile_rows(H, stripe, world, rank)
-    rmax = pdist.max_tile_rows(H, stripe, world)
+    rows = pdist.tile_rows(H, stripe, world, rank, owner)
+    rmax = pdist.max_tile_rows(H, stripe, world, owner)
     local = torch.zeros(rmax * W * 4, dtype=torch.float32)
     local[: len(rows) * W * 4] = torch.from_numpy(full[rows].reshape(-1))
-    frame = pdist.gather_frame(local, H, W, stripe)
+    frame = pdist.gather_frame(local, H, W, stripe, owner=owner)
     if rank == 0:
         np.save(result_path, frame.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,stripe", [(2, 8), (3, 5)])
-def test_gather_frame_gloo(world, stripe, tmp_path, oracle, pt):
+@pytest.mark.parametrize("world,stripe,balanced", [(2, 8, False), (3, 5, False), (2, 4, True), (3, 3, True)])
+def test_gather_frame_gloo(world, stripe, balanced, tmp_path, oracle, pt):
     sc = pt.scenes
     W, H = 40, 29
     Wp, Hp = sc.padded_dims(W, H)
@@ -62,9 +62,20 @@ def test_gather_frame_gloo(world, stripe, tmp_path, oracle, pt):
     fp = tmp_path / "frame.npy"
     rp = tmp_path / "result.npy"
     np.save(fp, full)
-    mp.spawn(_worker, args=(world, _free_port(), H, W, stripe, str(fp), str(rp)), nprocs=world, join=True)
+    owner = None
+    if balanced:  # an owner map like rt_partition_stripes': LPT over a cost per stripe (here: its brightness)
+        ns = (H + stripe - 1) // stripe
+        cost = [int(full[s * stripe:(s + 1) * stripe].sum() * 1000) for s in range(ns)]
+        owner = pdist_module().lpt_owner(cost, world)
+    mp.spawn(_worker, args=(world, _free_port(), H, W, stripe, str(fp), str(rp), owner), nprocs=world, join=True)
     got = np.load(rp)
     np.testing.assert_array_equal(got.view(np.uint32), full.view(np.uint32))
+
+
+def pdist_module():
+    import ptload
+
+    return ptload.submodule("dist")
 
 
 # ---- seed-row halo for tiled progressive sphere frames (raytracer.cl:20-30) ----------------
@@ -202,6 +213,41 @@ def test_native_halo_plan_equals_python(pt, H, hpad, stripe, n):
         halo.commit(s)
         np.testing.assert_array_equal(writer, halo.writer)
     assert total > 0
+
+
+@pytest.mark.parametrize("H,hpad,stripe,n", [(53, 56, 8, 2), (45, 48, 4, 3), (64, 64, 8, 8), (1080, 1080, 8, 8)])
+def test_halo_moves_rows_whose_stripe_changed_owner(pt, H, hpad, stripe, n):
+    """rt_comm_render under the balanced partition: each view brings its own owner map
+    (rt_partition_stripes), so between triangle frames (unshifted seed rows) a stripe may change
+    owner.  rt_seed_halo_plan must equal SeedHalo.plan under the new map, and after the moves every
+    row a rank reads holds the latest write — the seeds follow their stripes."""
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    ns = (H + stripe - 1) // stripe
+    rng = np.random.default_rng(H + n)
+    maps = [None] + [dist.lpt_owner(rng.integers(1, 100, ns), n) for _ in range(4)] + [None]
+    halo = dist.SeedHalo(H, hpad, stripe, n)
+    writer = np.full(hpad, -1, np.int32)
+    truth = np.arange(hpad, dtype=np.int64) * 3 + 11
+    local = [truth.copy() for _ in range(n)]
+    moved = 0
+    for f, own in enumerate(maps + maps[1:3]):  # (a map used again later)
+        halo.set_owner(own)
+        plan = halo.plan(0)
+        src, dst, rows = dist.seed_halo_plan_native(writer, H, hpad, stripe, n, 0, own)
+        exp = [(a, b, int(r)) for (a, b), rr in plan.items() for r in rr]
+        assert list(zip(src.tolist(), dst.tolist(), rows.tolist())) == exp, f
+        for a, b, r in exp:
+            local[b][r] = local[a][r]
+        moved += len(exp)
+        for y in range(H):
+            k = halo.row_rank[y]
+            assert local[k][y] == truth[y], (f, y)
+            truth[y] = local[k][y] = _write_value(y, f)
+        halo.commit(0)
+        np.testing.assert_array_equal(writer, halo.writer)
+    assert moved > 0
 
 
 # (kernel, progression) sequences of rt_comm_render calls: progressive sphere frames with

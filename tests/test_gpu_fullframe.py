@@ -70,8 +70,10 @@ def _tracer(pt, d, sr):
 
 
 def _tile_rows(H, tile):
-    stripe, n, r = tile
-    return np.arange(H)[(np.arange(H) // stripe) % n == r]
+    stripe, n, r = tile[:3]
+    owner = tile[3] if len(tile) > 3 else None
+    s = np.arange(H) // stripe
+    return np.arange(H)[(s % n if owner is None else np.asarray(owner)[s]) == r]
 
 
 def _check_tile(got, got_seeds, exp, exp_seeds, d, rows):
@@ -199,6 +201,60 @@ def test_dragon_8way_tile_sr16_whole_tile_vs_bvh_oracle(tracer, pt, oracle, drag
     oracle.render_tris(exp, d["cam"], d["S"], d["W"], d["H"], d["Wp"], d["Hp"], 16, 6, 0, sd, d["verts"], d["idx"],
                        pixels=pix, bvh=d["bvh"])
     _check_tile(got, got_seeds, exp, sd, d, rows)
+
+
+def test_dragon_balanced_8way_tile_sr16_whole_tile_vs_bvh_oracle(tracer, pt, oracle, dragon):
+    """The headline frame's 8-way partition by probed stripe cost (rt_partition_stripes: a whole-frame
+    probe, LPT over the 135 stripes — bench.py's default at N > 1): a valid owner map, the same from a
+    fresh context, and the tile of the rank holding the frame's top stripe (where the box pixels'
+    long chains crowd) at sampleRate 16 equal to the oracle on every pixel and seed slot — the
+    tile-local rows map to the frame's rows and seed slots through the owner map
+    (RtTriLaunch::stripe_map)."""
+    d = dragon
+    rt = _tracer(pt, d, 16)
+    owner = rt.partitionStripes(d["W"], d["H"], 8, 8)
+    assert owner.shape == (135,) and owner.max() < 8 and len(set(owner.tolist())) == 8
+    rt2 = _tracer(pt, d, 16)
+    np.testing.assert_array_equal(rt2.partitionStripes(d["W"], d["H"], 8, 8), owner)  # deterministic
+    rt2.close()
+    tile = (8, 8, int(owner[0]), owner)
+    rows = _tile_rows(d["H"], tile)
+    assert 0 in rows and not np.array_equal(rows, _tile_rows(d["H"], (8, 8, int(owner[0]))))
+    got = np.zeros(len(rows) * d["W"] * 4, np.float32)
+    rt.rayTrace(got, d["W"], d["H"], 0, kernel=2, tile=tile)
+    info = rt.renderInfo()
+    assert info["split_chunks"] == 16 and info["split_guard"] == 0 and info["pixels_long"] >= 1000, info
+    got_seeds = rt.getSeeds()
+    rt.close()
+    pix = (rows[:, None] * d["W"] + np.arange(d["W"])[None, :]).reshape(-1).astype(np.uint32)
+    exp = np.zeros(d["W"] * d["H"] * 4, np.float32)
+    sd = d["seeds"].copy()
+    oracle.render_tris(exp, d["cam"], d["S"], d["W"], d["H"], d["Wp"], d["Hp"], 16, 6, 0, sd, d["verts"], d["idx"],
+                       pixels=pix, bvh=d["bvh"])
+    _check_tile(got, got_seeds, exp, sd, d, rows)
+
+
+def test_balanced_partition_evens_out_the_long_chains(pt, dragon):
+    """What the cost-aware partition is for: under interleaved 8-row stripes the 8 ranks'
+    long chains (box pixels, serial sample chains) run from ~7,400 down to ~4,900 — the box pixels
+    crowd the frame's top rows — and the slowest rank follows them.  Under rt_partition_stripes' map
+    every rank's count is within 10 % of the mean."""
+    d = dragon
+    rt = _tracer(pt, d, 16)
+    owner = rt.partitionStripes(d["W"], d["H"], 8, 8)
+    counts = {}
+    for name, own in (("interleaved", None), ("balanced", owner)):
+        c = []
+        for r in range(8):
+            rows = _tile_rows(d["H"], (8, 8, r, own))
+            buf = np.zeros(len(rows) * d["W"] * 4, np.float32)
+            rt.rayTrace(buf, d["W"], d["H"], 0, kernel=2, tile=(8, 8, r, own))
+            c.append(rt.renderInfo()["pixels_long"])
+        counts[name] = np.array(c, np.float64)
+    rt.close()
+    spread = {k: (v.max() - v.min()) / v.mean() for k, v in counts.items()}
+    assert spread["balanced"] < 0.2 and counts["balanced"].max() < 1.1 * counts["balanced"].mean(), counts
+    assert spread["balanced"] < spread["interleaved"], counts
 
 
 def test_split_buffers_regrown_with_repairs_vs_oracle(pt, dragon, dragon_sr4, monkeypatch):

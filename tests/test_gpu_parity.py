@@ -470,6 +470,72 @@ def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt,
             rk.close()
 
 
+def test_owner_map_tiles_assemble_to_full_frame(tracer, pt, oracle):
+    """Tiles under an owner-map partition (rt_tile.stripe_owner): the cost-balanced map of
+    rt_partition_stripes (cached per view: a second call returns it without a probe) and a
+    hand-made one with a rank that owns nothing.  Every rank's tile, on its own context and on one
+    context that switches partitions (the stripe map and the schedule are re-keyed), reassembles
+    bit-exactly — on the host and with rt_assemble_tiles — to the full frame, itself the oracle's,
+    with every rank's seed rows equal to the full frame's."""
+    import torch
+    from importlib import import_module
+
+    dist = import_module("pathtracer_cl_amd.dist")
+    sc = pt.scenes
+    W, H, stripe, sr = 72, 53, 8, 2
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(5000)
+    seeds = sc.default_seeds(Wp, Hp)
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    S = sc.ply_scene()
+
+    def make():
+        rt = pt.RayTracer(0)
+        rt.setSpheres(S)
+        rt.setCamera(cam)
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        return rt
+
+    rt = make()
+    full = np.zeros(W * H * 4, np.float32)
+    rt.rayTrace(full, W, H, 0, kernel=2)
+    full_seeds = rt.getSeeds().reshape(2, Hp, Wp)
+    exp = np.zeros_like(full)
+    oracle.render_tris(exp, cam, S, W, H, Wp, Hp, sr, 6, 0, seeds.copy(), verts, idx)
+    np.testing.assert_array_equal(bits(full), bits(exp))
+    n = 3
+    balanced = rt.partitionStripes(W, H, stripe, n)
+    np.testing.assert_array_equal(rt.partitionStripes(W, H, stripe, n), balanced)
+    assert balanced.shape == (7,) and balanced.max() < n
+    rt.close()
+    switching = make()
+    for owner in (balanced, np.array([1, 1, 0, 1, 0, 0, 1], np.uint32), None):
+        tiles = []
+        for r in range(n):
+            rows = dist.tile_rows(H, stripe, n, r, owner)
+            for rk, fresh in ((make(), True), (switching, False)):
+                rk.setSeeds(Wp, Hp, seeds)
+                t = torch.zeros(max(len(rows), 1) * W * 4, dtype=torch.float32, device="cuda:0")
+                rk.rayTrace(t, W, H, 0, kernel=2, tile=(stripe, n, r, owner))
+                s_ = rk.getSeeds().reshape(2, Hp, Wp)
+                np.testing.assert_array_equal(s_[:, rows], full_seeds[:, rows])
+                got = t.cpu().numpy()[: len(rows) * W * 4]
+                np.testing.assert_array_equal(bits(got), bits(full.reshape(H, W, 4)[rows].reshape(-1)),
+                                              err_msg=f"owner {owner}, rank {r}, fresh {fresh}")
+                if fresh:
+                    rk.close()
+                    tiles.append(t)
+        frame = dist.assemble([t.cpu().numpy().reshape(-1, W, 4) for t in tiles], H, W, stripe, owner)
+        np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full))
+        dev_frame = torch.full((W * H * 4,), -1.0, dtype=torch.float32, device="cuda:0")
+        dist.assemble_native(tiles, H, W, stripe, dev_frame, owner=owner)
+        np.testing.assert_array_equal(bits(dev_frame.cpu().numpy()), bits(full))
+    switching.close()
+
+
 def test_native_comm_assembly_and_single_rank_render(tracer, pt):
     """The native host's sharding path (csrc/rt_comm.hip).  rt_assemble_tiles (the root's
     device-side scatter) rebuilds the full frame from 3 ranks' compact tiles; a 1-rank RCCL

@@ -117,6 +117,45 @@ def test_assemble_roundtrip():
     np.testing.assert_array_equal(dist.assemble(tiles, H, W, stripe), full)
 
 
+@pytest.mark.parametrize("H,stripe,n,seed", [(1080, 8, 8, 0), (1083, 8, 3, 1), (53, 5, 4, 2), (7, 16, 4, 3),
+                                             (64, 8, 5, 4)])
+def test_tile_rows_owner_map(pt, H, stripe, n, seed):
+    """rt_tile with a stripe-owner map (rt_partition_stripes' output form): rt_tile_rows equals
+    dist.tile_rows for every rank — including ranks that own no stripe and a short last stripe —
+    the ranks' rows cover the frame once, and compact tiles assemble back to the frame."""
+    dist = __import__("ptload").submodule("dist")
+    lib = pt.load_library()
+    ns = (H + stripe - 1) // stripe
+    rng = np.random.default_rng(seed)
+    owner = rng.integers(0, max(n - 1, 1), ns).astype(np.uint32)  # rank n - 1 owns nothing
+    seen = []
+    for r in range(n):
+        rows = dist.tile_rows(H, stripe, n, r, owner)
+        t, _keep = pt._abi.tile_struct((stripe, n, r, owner))
+        assert lib.rt_tile_rows(H, ctypes.byref(t)) == len(rows)
+        assert np.all(np.diff(rows) > 0)
+        np.testing.assert_array_equal(dist.row_owner(H, stripe, n, owner)[rows], r)
+        seen.append(rows)
+    np.testing.assert_array_equal(np.sort(np.concatenate(seen)), np.arange(H))
+    W = 3
+    full = rng.random((H, W, 4)).astype(np.float32)
+    tiles = [full[rows] for rows in seen]
+    np.testing.assert_array_equal(dist.assemble(tiles, H, W, stripe, owner), full)
+
+
+def test_lpt_owner_rule():
+    """dist.lpt_owner — the rule rt_partition_stripes applies to its probed stripe costs: costliest
+    stripe first (ties: lower index) to the least-loaded rank (ties: lower rank)."""
+    dist = __import__("ptload").submodule("dist")
+    np.testing.assert_array_equal(dist.lpt_owner([5, 9, 1, 9, 3], 2), [0, 0, 1, 1, 1])
+    np.testing.assert_array_equal(dist.lpt_owner([1, 1, 1, 1], 4), [0, 1, 2, 3])
+    rng = np.random.default_rng(7)
+    c = rng.integers(1, 1000, 135)
+    own = dist.lpt_owner(c, 8)
+    loads = np.bincount(own, weights=c, minlength=8)
+    assert loads.max() - loads.min() <= c.max()  # LPT: within one stripe of each other
+
+
 def test_fails_loudly_without_gpu(pt):
     if gpu_available():
         pytest.skip("a GPU is visible")

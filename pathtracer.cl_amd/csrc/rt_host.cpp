@@ -164,12 +164,7 @@ struct rt_ctx {
     uint32_t seed_width = 0; /* lanes per long chain in the seed pass: 8-64 subtree-parallel (k_chain_seeds), 3 coop_round,
                                 1 one lane, 0 by the launch (seed_width_auto) */
     uint32_t split_probe = 4;
-#ifndef RT_SPLIT_GPW
-#define RT_SPLIT_GPW 0
-#endif
-    bool repair_wide = true;   /* the repair pass in the runs form whatever the long chains' (RT_REPAIR_WIDE A/B knob) */
-    uint32_t split_nch = 16;   /* sample-split: chunk tasks per pixel (about; RT_SPLIT_NCH A/B knob, 1-64) */
-    uint32_t split_gpw = RT_SPLIT_GPW; /* chains per seed-pass wave: 0 = every lane / group (16 / 4 per wave measured no faster) */
+    uint32_t split_nch = 16;   /* sample-split: chunk tasks per pixel, about (8 / 13 / 32 no faster, profiles/r05ba) */
     uint32_t *d_split_seed = nullptr; /* per pixel and chunk: the seed at the chunk's first sample */
     float *d_split_col = nullptr;     /* per sample and pixel: its radiance */
     uint32_t *d_split_counter = nullptr; /* [0]: the seed pass's cursor, [32]: the box pixels' (own line) */
@@ -180,12 +175,6 @@ struct rt_ctx {
     uint32_t *d_repair_seed = nullptr; /* the repaired pixels' seeds by slot (the first RT_REPAIR_SLOTS of them) */
     size_t repair_seed_bytes = 0;
     uint32_t repair_slots = RT_REPAIR_SLOTS; /* RT_REPAIR_SLOTS (env, test knob): repaired pixels with per-sample seeds */
-#ifndef RT_HIT_DEPTH
-#define RT_HIT_DEPTH 1
-#endif
-    /* RT_HIT_DEPTH (env, A/B knob): the slotted long chains' seed pass records each sample's mesh-hit
-       depth after the seeds (split_hit_depth), and their chunk tasks skip the box segments' traversals */
-    uint32_t hit_depth = RT_HIT_DEPTH;
     bool last_hit_depth = false; /* the last sample-split render used split_hit_depth */
     size_t split_box_cap = 0;
     uint32_t n_split_box = 0;
@@ -208,13 +197,9 @@ struct rt_ctx {
     std::vector<uint32_t> order_key; /* what the cached order was computed for */
     bool schedule = true;
     bool schedule_rebuilt = false; /* the last triangle render recomputed the schedule */
-#ifndef RT_MEASURED_LPT
-#define RT_MEASURED_LPT 2
-#endif
-    /* measured-cost schedule (RT_MEASURED_LPT, env A/B knob: 0 off, 1 whole-pixel frames, 2 those
-       and sample-split tiles): a view's first frame records each pixel's wave iterations
-       (pixel_iter; a split tile's mesh chunk tasks), its next frame re-sorts the tiles by them */
-    int measured_lpt = RT_MEASURED_LPT;
+    /* measured-cost schedule (whole-pixel frames and sample-split tiles of >= 16 samples per pixel):
+       a view's first frame records each pixel's traversal steps (pixel_iter; a split tile's mesh chunk
+       tasks), its next frame re-sorts the tiles by them */
     uint32_t *d_pixel_iter = nullptr;
     size_t pixel_iter_px = 0;
     bool iter_recorded = false;  /* this view's costs are in d_pixel_iter */
@@ -549,7 +534,7 @@ int ensure_split(rt_ctx *c, size_t seed_bytes, size_t col_bytes)
    seconds, profiles/r05bc; 77 ms with the cap, r05bf); full_grid 0: unbounded. */
 int split_box_blocks(const rt_ctx *c, uint32_t width, int full_grid)
 {
-    const uint32_t per_wave = c->split_gpw ? c->split_gpw : 64u / std::max(1u, width == RT_SEED_COOP4 ? 4u : width);
+    const uint32_t per_wave = 64u / std::max(1u, width == RT_SEED_COOP4 ? 4u : width);
     int n = (int)((c->n_split_box + per_wave * 4u - 1u) / (per_wave * 4u));
     /* subtree-parallel chains (width >= 8) all run at once where they fit: each is the critical path */
     if (full_grid > 0) n = std::min(n, std::max(1, width >= 8 ? full_grid * 3 / 4 : full_grid / RT_BOX_GRID_DIV));
@@ -625,7 +610,8 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
    at the camera ray. */
 bool hit_depth_on(const rt_ctx *c, const RtTriLaunch &t)
 {
-    return c->hit_depth && t.split_coop >= 8 && !t.split_restart && t.split_chunk == 1u && t.max_depth < 255u;
+    (void)c;
+    return t.split_coop >= 8 && !t.split_restart && t.split_chunk == 1u && t.max_depth < 255u;
 }
 
 /* A sample-split render: the box pixels' seed pass, their chunks and their in-order sums on
@@ -643,7 +629,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         b.split_counter = a.split_counter + 32;
         b.work_counter = a.work_counter + kWorkBox;
         b.spill = a.spill + (size_t)std::max<int>(blocks, (int)a.split_seed_blocks) * RT_BLOCK * a.spill_cap;
-        b.split_gpw = c->split_gpw;
+        b.split_gpw = 0;
         b.split_seed_blocks = (uint32_t)std::max(1, c->split_box_grid);
         b.split_chunk = a.split_fine; /* the long chains' chunks: one stored seed each */
         b.split_chunks = (a.sample_rate * a.sample_rate + b.split_chunk - 1u) / b.split_chunk;
@@ -712,7 +698,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.split_n_dev = reinterpret_cast<const uint32_t *>(a.counters + RT_CNT_REPAIR);
         r.split_counter = a.split_counter + 48;
         r.work_counter = a.work_counter + kWorkRepair;
-        r.split_gpw = c->split_gpw;
+        r.split_gpw = 0;
         r.split_seed_blocks = 16u * RT_REPAIR_WIDTH / 16u; /* RT_REPAIR_WIDTH blocks of 4 waves, one chain per wave
                                                                 at width 64: up to 256 chains at once */
         r.split_chunk = a.split_fine;
@@ -722,7 +708,7 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         r.finish_part = RT_FIN_LIST;
         /* the runs form also where the long chains take the cooperative pass (the 4-way tile: the
            repair 2.7 -> 2.1 ms at the end of the mesh pixels' stream, the tile 28.83 -> 28.39 ms, profiles/r05bg, r05bh) */
-        if (a.split_coop >= 8 || c->repair_wide) {
+        {
             const uint32_t spp = a.sample_rate * a.sample_rate;
             r.split_coop = RT_REPAIR_WIDTH; /* runs of width - 1 hit samples (k_chain_seeds<width, true>) */
             RtTriLaunch s = r;
@@ -842,8 +828,9 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     /* speculated mesh pixels: the silhouettes' neighbours run as long chains (RT_SPLIT_SPEC=2: every
        probe-hit pixel speculated — a test knob that makes repairs happen) */
     const uint32_t spec_row = split && c->split_spec == 1 ? W : 0u;
-    /* RT_LONG_STEPS (A/B knob): the probe steps per ray above which a mesh pixel runs as a long chain (96; 0: none) */
-    const uint32_t long_steps = env_u32("RT_LONG_STEPS", 96);
+    /* the probe steps per ray above which a mesh pixel runs as a long chain (none / 200 measured slower,
+       profiles/r05ak) */
+    const uint32_t long_steps = 96;
     e = rt_sched_box_scan(c->sched, c->d_flags, (uint32_t)npx, pn2, split ? long_steps * pn2 : 0u, spec_row, st);
     if (e) return hip_fail(c, (hipError_t)e, "box-pixel scan");
     uint32_t n_box = 0;
@@ -930,18 +917,13 @@ try {
     if (const char *v = getenv("RT_SPLIT_MB")) c->split_mb = (size_t)std::max(0L, atol(v));
     if (const char *v = getenv("RT_SPLIT")) c->split = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_SPLIT_SPEC")) c->split_spec = atoi(v);
-    if (const char *v = getenv("RT_MEASURED_LPT")) c->measured_lpt = atoi(v); /* 0 off, 1 whole pixels, 2 + split */
-    if (const char *v = getenv("RT_REPAIR_WIDE")) c->repair_wide = atoi(v) != 0; /* A/B knob */
-    if (const char *v = getenv("RT_SPLIT_NCH")) c->split_nch = (uint32_t)std::min(64, std::max(1, atoi(v))); /* A/B knob */
-    if (const char *v = getenv("RT_SPLIT_GPW")) c->split_gpw = (uint32_t)std::max(0, atoi(v)); /* A/B knob */
-    if (const char *v = getenv("RT_SEED_WIDTH")) { /* A/B knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
+    if (const char *v = getenv("RT_SEED_WIDTH")) { /* test knob: 0 automatic, 1 one lane, 3 cooperative, 8-64 (a power of two) */
         const int w = atoi(v);
         if (w == 0 || w == 1 || w == 3 || (w >= 8 && w <= 64 && (w & (w - 1)) == 0)) c->seed_width = (uint32_t)w;
         else fprintf(stderr, "[rtmi] RT_SEED_WIDTH=%s ignored (0, 1, 3 or a power of two from 8 to 64)\n", v);
     }
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     c->repair_slots = std::max(1u, env_u32("RT_REPAIR_SLOTS", RT_REPAIR_SLOTS)); /* test knob: the path beyond them */
-    c->hit_depth = env_u32("RT_HIT_DEPTH", RT_HIT_DEPTH) != 0;
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -956,10 +938,10 @@ try {
     }
     memset(c->h_counters, 0, kCounterBytes + sizeof(unsigned long long)); /* no stale guard before any render */
     c->d_work = reinterpret_cast<uint32_t *>(c->d_counters + RT_COUNTER_WORDS);
-    /* the pinned copy's device address: a render hands its counters back with k_counters_out
-       (RT_COUNTERS_KERNEL=0: the copy-engine transfer instead) */
+    /* the pinned copy's device address: a render hands its counters back with k_counters_out (a copy-engine
+       transfer where the mapping is unavailable) */
     void *hd = nullptr;
-    if (env_u32("RT_COUNTERS_KERNEL", 1) && hipHostGetDevicePointer(&hd, c->h_counters, 0) == hipSuccess)
+    if (hipHostGetDevicePointer(&hd, c->h_counters, 0) == hipSuccess)
         c->h_counters_dev = static_cast<unsigned long long *>(hd);
     *out = c;
     return RT_OK;
@@ -1572,8 +1554,9 @@ try {
            dragon frame at 1024 blocks 96.7 -> 101.2 ms: profiles/r04l, r04m) */
         const bool short_frame =
             (uint64_t)W * hl * c->sample_rate * c->sample_rate < kShortFrameSamplesPerLane * (uint64_t)blocks * RT_BLOCK;
-        if (short_frame) /* RT_SHORT_BLOCKS (A/B knob): blocks per CU of a short frame */
-            blocks = std::max(1, blocks * (int)env_u32("RT_SHORT_BLOCKS", kShortFrameBlocksPerCU) / RT_TRIS_WAVES);
+        if (short_frame) blocks = std::max(1, blocks * (int)kShortFrameBlocksPerCU / RT_TRIS_WAVES);
+        /* scheduling knobs (read every render; test_stepping_knobs_change_no_bits): a smaller grid, the
+           stepping round's exit rule */
         if (const uint32_t gb = env_u32("RTMI_GRID_BLOCKS", 0)) blocks = std::min(blocks, (int)gb);
         if (trav == RT_TRAV_BVH4Q) {
             r = grid_blocks(c, trav, c->counting, RT_FORM_SPLIT, &blocks_split);
@@ -1589,10 +1572,8 @@ try {
             if (rs != RT_OK) return rs;
         }
         a.spill = c->d_spill;
-        a.fetch_k = env_u32("RTMI_FETCH_K", kFetchK); /* tuning knobs (profiles/bunny_sweep.py) */
-        a.fetch_k_box = env_u32("RTMI_FETCH_K_BOX", a.fetch_k);
+        a.fetch_k = env_u32("RTMI_FETCH_K", kFetchK);
         a.fetch_frac = env_u32("RTMI_FETCH_FRAC", kFetchFrac);
-        a.box_exit = env_u32("RTMI_BOX_EXIT", 0);
         a.probe_n = probe_n(c->sample_rate);
         a.diag_pixel = 0xffffffffu;
 #if RT_DIAG_ONE_PIXEL
@@ -1669,38 +1650,33 @@ try {
             }
         }
         /* whole pixels of many samples (long tasks, a few dequeues per microsecond): queue takes of
-           exactly the items the idle lanes need, so no wave holds the queue's last tiles back
-           (RT_TAKE_EXACT=0/1: an A/B knob) */
+           exactly the items the idle lanes need, so no wave holds the queue's last tiles back */
         a.take_exact = !a.split_chunks && c->sample_rate * c->sample_rate >= 16u ? 1u : 0u;
-        if (const char *v = getenv("RT_TAKE_EXACT")) a.take_exact = atoi(v) != 0 && !a.split_chunks ? 1u : 0u;
         /* short frames: box-path queries whose segment misses the mesh's padded bounds are answered
            without a traversal (bunny class 0.469 -> 0.457 ms; the dragon frame measured 87.1 -> 88.4
-           ms with it, profiles/r05ah: off there). RT_MESH_BOUNDS=0/1 forces it off / on */
+           ms with it, profiles/r05ah; the 2-way tile within noise, r05bj: off there) */
         a.mesh_bounds = c->mesh_bounds_ok && short_frame ? 1u : 0u;
-        if (const char *v = getenv("RT_MESH_BOUNDS")) a.mesh_bounds = c->mesh_bounds_ok && atoi(v) != 0 ? 1u : 0u;
         for (int k = 0; k < 3; ++k) {
             a.mesh_lo[k] = c->mesh_lo[k];
             a.mesh_hi[k] = c->mesh_hi[k];
         }
         /* short whole-pixel frames take from the multi-head queue (mq_take) in batches of
            RT_QUEUE_BATCH items (0: one head; bunny class 0.519 -> 0.473 ms, profiles/r05ac) */
-        a.queue_batch = a.take_exact || a.split_chunks ? 0u : std::min(64u, env_u32("RT_QUEUE_BATCH", RT_QUEUE_BATCH));
+        a.queue_batch = a.take_exact || a.split_chunks ? 0u : RT_QUEUE_BATCH;
         /* long tasks take exactly from the multi-head queue too: each head's tiles go to the waves
            of one XCD's blocks, so a tile's pixels share that XCD's L2 (dragon frame 87.4 -> 86.5 ms,
-           profiles/r05ar; RT_EXACT_HEADS=0: one head) */
-        if (a.take_exact && env_u32("RT_EXACT_HEADS", 1)) a.queue_batch = 64u;
-        /* a split tile's mesh chunk tasks from the heads too, in batches of RT_SPLIT_HEADS (64; 0: one
-           head), a tile's chunk layers on one head (8-way tile 15.95 -> 15.71 ms, profiles/r05au) */
-        if (a.split_chunks && env_u32("RT_SPLIT_HEADS", 64))
-            a.queue_batch = std::min(64u, env_u32("RT_SPLIT_HEADS", 64));
+           profiles/r05ar) */
+        if (a.take_exact) a.queue_batch = 64u;
+        /* a split tile's mesh chunk tasks from the heads too, in batches of 64, a tile's chunk layers on
+           one head (8-way tile 15.95 -> 15.71 ms, profiles/r05au) */
+        if (a.split_chunks) a.queue_batch = 64u;
         /* a frame under the probe's order records its pixels' costs for the next frame (a sample-split
            frame: its mesh pixels' chunk tasks; the long chains' entries stay 0) */
         a.pixel_iter = nullptr;
         bool record_iter = false;
         /* (frames of >= 16 samples per pixel: a 1-spp pixel's cost is one random path, and the bunny
            class measured 0.436 -> 0.459 ms re-sorted by it, profiles/r05aj) */
-        if (a.tile_order && c->measured_lpt && !c->order_measured && c->sample_rate * c->sample_rate >= 16u &&
-            (!a.split_chunks || c->measured_lpt > 1)) {
+        if (a.tile_order && !c->order_measured && c->sample_rate * c->sample_rate >= 16u) {
             const uint32_t nch = a.split_chunks ? a.split_chunks : 1u;
             const size_t n_i = (size_t)W * hl * nch;
             if (c->pixel_iter_px < n_i) {

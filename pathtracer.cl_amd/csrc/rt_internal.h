@@ -51,9 +51,6 @@ int rt_exception_status(std::string *err) noexcept;
 #ifndef RT_TRIS_WAVES
 #define RT_TRIS_WAVES 5
 #endif
-#ifndef RT_SHADOW_REDO
-#define RT_SHADOW_REDO 1 /* k_tris: shadow rays answered without traversal are consumed in the same D pass (-3.9 %) */
-#endif
 #define RT_LEAF_MAX 8
 /* device counters: rays_closest, rays_shadow, nodes, tris, leaves, lane slots,
    traversal-loop clocks, kernel clocks (the last two: per lane, summed), shadow rays
@@ -160,10 +157,8 @@ struct RtTriLaunch {
     const uint32_t *pixel_flags; /* cost probe per pixel: mesh hits of its probe rays << RT_PROBE_HIT_SHIFT |
                                     their steps (NULL: no probe) */
     uint32_t probe_n;            /* probe rays per pixel: probe_n x probe_n (<= 5) */
-    uint32_t fetch_k_box;       /* fetch_k of waves holding box pixels (pixel_flags 0) */
     uint32_t fetch_frac;        /* stepping-round exit at ceil(live lanes x fetch_frac / 64) completed
                                    queries when that is below fetch_k (0: fetch_k only) */
-    uint32_t box_exit;          /* a box pixel's completed query ends the stepping round */
     uint32_t diag_pixel;        /* RT_DIAG_ONE_PIXEL builds: yl * W + x of the target pixel, and how many */
     uint32_t diag_k;            /* pixels of its 8 x 8 tile are rendered (from it on, in-tile order) */
     uint32_t *pixel_stats;      /* diagnostics (counting launches, RT_PIXEL_STATS): per pixel 4 x u32 =

@@ -775,9 +775,6 @@ __device__ __forceinline__ void coop_begin(CoopQuery &q, V3 o, V3 d, float tmax)
     q.sp = 0;
 }
 
-#ifndef RT_SEED_EXISTS
-#define RT_SEED_EXISTS 1 /* seed-pass queries end at the first accepted triangle */
-#endif
 
 /* Cooperative closest-hit query, one stack ITEM per lane: each round the 4 lanes of a group take
    the top entries of the group's stack — a node (one lane: its 4 child boxes) or the triangles of
@@ -909,9 +906,6 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
     return q.sp == 0;
 }
 
-#ifndef RT_SEED_ROOT
-#define RT_SEED_ROOT 1 /* cooperative seed-pass queries start from the root's child boxes, tested in registers */
-#endif
 #ifndef RT_SEED_STATS
 #define RT_SEED_STATS 0 /* diagnostics builds: per-pixel query / immediate-answer / iteration counts (RT_PIXEL_STATS) */
 #endif
@@ -927,11 +921,6 @@ __device__ __forceinline__ bool coop_round(const float4 *__restrict__ nodes, con
 __device__ __forceinline__ bool coop_root(uint4 r0, uint4 r1, uint4 r2, uint4 r3, CoopQuery &q, const CoopStack &gst, V3 d,
                                           bool writer)
 {
-    if (!RT_SEED_ROOT) {
-        if (writer) gst[0] = 0;
-        q.sp = 1;
-        return true;
-    }
     float t[4];
     int c[4];
     const int nh = node_children(r0, r1, r2, r3, q.inv, q.oi, d, q.best_t, false, false, t, c);
@@ -1059,7 +1048,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
         /* The path advance, over as many segments and samples as it takes before the next stepping
            round: a new sample's camera ray, and every query answered without a round — an empty
            candidate list, a box bounce whose ray misses the root's child boxes (tested from
-           registers: RT_SEED_ROOT) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly
+           registers) — advances at once, up to RT_SEED_IMM passes.  Box paths mostly
            leave the mesh's box alone, so a long chain's samples are mostly resolved here, without a
            memory round trip. */
         const unsigned long long t_adv0 = RT_SEED_STATS ? wave_clock() : 0ull;
@@ -1128,7 +1117,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                                 running = false;
                                 fin = true;
                             }
-                        } else if (RT_SEED_ROOT && !lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
+                        } else if (!lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
                             running = false;
                             fin = true;
                         }
@@ -1177,7 +1166,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                                 }
                             } else {
                                 trav_begin(ts, stk, qo, qd, kInf);
-                                if (RT_SEED_ROOT && !lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
+                                if (!lane_root(rq0, rq1, rq2, rq3, ts, stk, qd)) {
                                     running = false;
                                     fin = true;
                                 }
@@ -1219,7 +1208,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 /* The seed needs only WHETHER a segment hits the mesh (a hit ends the sample
                    after the light samples' draws, wherever it is): the query ends at its first
                    accepted triangle (the closest-hit rule's acceptance, t >= tmin) */
-                const bool exists = RT_SEED_EXISTS && (COOP ? cq.best : ts.best) >= 0;
+                const bool exists = (COOP ? cq.best : ts.best) >= 0; /* the query ends at its first accepted triangle */
                 /* a query never takes 2^14 rounds (a ray meets far fewer nodes than that):
                    a bound every wave reaches, whatever a defect would do to a stack (reported) */
                 if (q_steps > (1u << 14)) atomicOr(guard, (unsigned long long)RT_GUARD_ROUNDS);
@@ -1290,9 +1279,6 @@ __device__ __forceinline__ uint32_t mwc_jump(uint32_t x, uint32_t k, uint32_t mu
    shared stack or an item assignment (coop_round's cost: DESIGN.md §4.5). */
 #ifndef RT_CHAIN_IMM
 #define RT_CHAIN_IMM 2 /* path-advance passes per iteration */
-#endif
-#ifndef RT_REPAIR_RUNS
-#define RT_REPAIR_RUNS 1 /* the repair pass takes its chains' hit samples in runs of G - 1 */
 #endif
 #ifndef RT_CHAIN_UNROLL
 #define RT_CHAIN_UNROLL 3 /* traversal steps per iteration (1 / 2 / 3 / 4: 8-way tile 16.8 / 16.4 / 16.3 / 16.4 ms, r04h2) */
@@ -1611,7 +1597,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_chain_seeds(RtTriLa
                 }
             }
             bool run_on = false;
-            if (RT_REPAIR_RUNS && RUNS && next && a.split_restart && sample < spp && lpack != RT_LPACK_NONE &&
+            if (RUNS && next && a.split_restart && sample < spp && lpack != RT_LPACK_NONE &&
                 lpack != RT_LPACK_EMPTY) {
                 /* the repair pass (a speculated pixel's chain): a run of up to G - 1 samples at once,
                    one per lane, each from the seed it has if every earlier sample of the run hit the
@@ -1771,17 +1757,9 @@ enum : int { M_IDLE = 0, M_NEWSAMPLE = 1, M_CLOSEST = 2, M_SHADOW = 3, M_DONE = 
         the iteration (the reference loop, wave-uniform).
    SPLIT: a queue item is one chunk of a pixel's samples, started from the seed the seed pass
    (k_split_seeds) stored for it; each sample's radiance is stored for k_split_finish. */
-#ifndef RT_LPT_STEPS
-#define RT_LPT_STEPS 1 /* pixel_iter records a pixel's traversal steps (0: its wave iterations in flight) */
-#endif
-#ifndef RT_LPT_QW
-#define RT_LPT_QW 0 /* A/B: the recorded cost's weight of a completed query, in steps */
-#endif
-#ifndef RT_OFF_MESH_REDO
-#define RT_OFF_MESH_REDO 1 /* path-advance passes that may answer an off-mesh box-path query in place (0 / 1 / all:
-                              bunny class 0.484 / 0.457 / 0.594 ms, profiles/r05ag-r05ah); later ones at the
-                              stepping round's start, without a step */
-#endif
+/* path-advance passes that may answer an off-mesh box-path query in place (0 / 1 / all: bunny class
+   0.484 / 0.457 / 0.594 ms, profiles/r05ag-r05ah); later ones at the stepping round's start, without a step */
+constexpr int kOffMeshRedo = 1;
 template <int TRAV, bool COUNT, bool SPLIT = false, bool MQ = false> /* MQ: the multi-head queue (mq_take) */
 __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
 {
@@ -1841,7 +1819,6 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const float mix_t = uniform_f(a.progressive > 0 ? 1.0f / (float)a.progressive : 0.0f);
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
     const int fetch_k_all = (int)a.fetch_k;
-    const int fetch_k_box = (int)a.fetch_k_box;
 
     int mode = M_IDLE;
     uint32_t x = 0, yl = 0; /* pixel column and local row (global row / seed slot derived) */
@@ -1882,19 +1859,14 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
     const bool multi_q = MQ; /* multi-head queue: short frames' batched takes, long tasks' exact takes (batch 0)
                                 and a split tile's mesh chunk tasks; never for RT_SPLIT_BOX launches */
     uint32_t qs = (blockIdx.x % RT_QHEADS) << 4;
-    /* the wave's loop iterations (wave-uniform): a whole pixel's take and finish iterations go to
-       pixel_iter, the measured cost the view's next schedule sorts by (rt_sched_order_measured) */
-    uint32_t it_wave = 0;
 
     for (;;) {
-        ++it_wave;
         const unsigned long long t_d0 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
         /* ---- D: advance the path (trace_path_tri, rtcommon.h:378-468) ---- */
         for (int redo_pass = 0;; ++redo_pass) {
         if (fin) {
             fin = false;
             bool want_shadow = false, seg_done = false, sample_done = false;
-            if (RT_LPT_STEPS && RT_LPT_QW) pix_steps += RT_LPT_QW;
             if (mode == M_CLOSEST) {
                 ++cnt[0];
                 if (COUNT || RT_PLAIN_PIXEL_STATS) ++pix_q;
@@ -2034,7 +2006,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 mode = (sample >= spp || sample % a.split_chunk == 0u) ? M_IDLE : M_NEWSAMPLE;
                 if (a.pixel_iter && mode == M_IDLE) /* the chunk task's finish */
                     a.pixel_iter[(size_t)a.W * a.Hl * a.split_chunks + (size_t)(yl * a.W + x) * a.split_chunks +
-                                 (sample - 1u) / a.split_chunk] = RT_LPT_STEPS ? (uint32_t)pix_steps : it_wave;
+                                 (sample - 1u) / a.split_chunk] = (uint32_t)pix_steps;
                 if (sample >= spp && !a.split_seed_slot) /* the pixel's final seed, from its last chunk's own draws
                                                             (a slotted long chain's: from its seed pass) */
                     reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * a.split_nseed + a.split_nseed - 1u] =
@@ -2072,7 +2044,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                     a.seeds[slot] = seed.x;
                     a.seeds[plane + slot] = seed.y;
-                    if (a.pixel_iter) a.pixel_iter[a.W * a.Hl + yl * a.W + x] = RT_LPT_STEPS ? (uint32_t)pix_steps : it_wave;
+                    if (a.pixel_iter) a.pixel_iter[a.W * a.Hl + yl * a.W + x] = (uint32_t)pix_steps;
                     mode = M_IDLE;
                     pclass = -1;
                     if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats) { /* diagnostics (RT_PIXEL_STATS) */
@@ -2095,10 +2067,9 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 }
             }
         }
-        /* RT_SHADOW_REDO: a shadow ray just issued whose answer is known without a traversal
-           (the C-phase rule below: tmax <= tmin, or cos(wi) <= 0) is answered here and the
-           path advanced again in this pass, instead of after a whole stepping round */
-        if (!RT_SHADOW_REDO) break;
+        /* a shadow ray just issued whose answer is known without a traversal (the C-phase rule
+           below: tmax <= tmin, or cos(wi) <= 0) is answered here and the path advanced again in
+           this pass, instead of after a whole stepping round (-3.9 %, profiles/r01n) */
         const float cw_q = qd.x * hn.x + qd.y * hn.y + qd.z * hn.z;
         const bool issued = mode == M_SHADOW && !fin && !running;
         const bool need_trav = stmax > RT_SMALL_F && cw_q > 0;
@@ -2107,7 +2078,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
         /* and a box-path query (a bounce off the box, or a shadow ray leaving it) whose segment misses
            the mesh's padded bounds: no triangle accepted, whatever the traversal would visit */
         bool off_mesh = false;
-        if (!SPLIT && redo_pass < RT_OFF_MESH_REDO && a.mesh_bounds && !tri_hit && !fin && !running &&
+        if (!SPLIT && redo_pass < kOffMeshRedo && a.mesh_bounds && !tri_hit && !fin && !running &&
             ((mode == M_SHADOW && need_trav) || (mode == M_CLOSEST && depth > 0)))
             off_mesh = segment_misses_box(qo, qd, RT_SMALL_F, mode == M_SHADOW ? stmax : kInf, a.mesh_lo, a.mesh_hi);
         const bool redo = (issued && !need_trav) || known_miss || off_mesh;
@@ -2192,22 +2163,22 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     }
                     if (SPLIT && take) {
                         if (a.pixel_iter) /* a mesh pixel's chunk task: its take (pixel_iter, whole pixels: below) */
-                            a.pixel_iter[(size_t)(yl * a.W + x) * a.split_chunks + chunk] = RT_LPT_STEPS ? 0u : it_wave;
+                            a.pixel_iter[(size_t)(yl * a.W + x) * a.split_chunks + chunk] = 0u;
                         sample = chunk * a.split_chunk;
                         if (a.split_hit_depth) hit_depth = a.split_hit_depth[(size_t)sbase * spp + sample];
                         pclass = a.pixel_class ? a.pixel_class[(size_t)yl * a.W + x] : -1;
                         mode = M_NEWSAMPLE;
-                        if (COUNT || RT_LPT_STEPS) pix_q = pix_steps = 0;
+                        pix_q = pix_steps = 0;
                     } else if (take) {
                         const uint32_t slot = global_row(a, yl) * a.Wpad + x;
                         /* raytracer.cl:207-209: unshifted seed slot */
                         seed.x = a.seeds[slot];
                         seed.y = a.seeds[plane + slot];
-                        if (a.pixel_iter) a.pixel_iter[yl * a.W + x] = RT_LPT_STEPS ? 0u : it_wave;
+                        if (a.pixel_iter) a.pixel_iter[yl * a.W + x] = 0u;
                         if ((COUNT || RT_PLAIN_PIXEL_STATS) && a.pixel_stats)
                             pix_rt0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         if (COUNT) pix_t0 = wave_clock();
-                        if (COUNT || RT_PLAIN_PIXEL_STATS || RT_LPT_STEPS) pix_q = pix_steps = pix_d = pix_ab = pix_c = pix_it = 0;
+                        pix_q = pix_steps = pix_d = pix_ab = pix_c = pix_it = 0;
                         ACC_SET(0, 0.0f);
                         ACC_SET(1, 0.0f);
                         ACC_SET(2, 0.0f);
@@ -2302,15 +2273,11 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
             }
             const unsigned long long t_c0 = (COUNT || RT_PLAIN_PIXEL_STATS) ? wave_clock() : 0ull;
             if (COUNT || RT_PLAIN_PIXEL_STATS) pix_ab += t_c0 - t_d1;
-            /* a wave holding box pixels (the long serial chains that set the frame time)
-               leaves the stepping rounds after fewer completed queries: less idling on the
-               critical path, at the price of more (less full) shading passes */
             /* The exit threshold follows the wave's live queries: with few lanes left (the
                frame's tail, or a small tile) a fixed fetch_k is never reached, and every lane
                would wait for the wave's longest query before its path moves on — the long
                serial chains then run at the pace of their slowest neighbours. */
-            const unsigned long long costly_lanes = __ballot(pclass != -1);
-            int fetch_k = costly_lanes ? fetch_k_box : fetch_k_all;
+            int fetch_k = fetch_k_all;
             if (a.fetch_frac) {
                 const int live = __popcll(__ballot(running || fin));
                 const int k_live = (live * (int)a.fetch_frac + 63) >> 6;
@@ -2343,8 +2310,8 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                             cnt[3] += tc.tests;
                             cnt[4] += tc.leaves;
                             pix_steps += tc.nodes + tc.leaves;
-                        } else if (RT_PLAIN_PIXEL_STATS || RT_LPT_STEPS) {
-                            ++pix_steps; /* (plain stats builds, RT_LPT_STEPS: trav_step calls) */
+                        } else {
+                            ++pix_steps; /* (the measured cost, pixel_iter: trav_step calls) */
                         }
                     }
                     if (COUNT) ++cnt[5];
@@ -2352,8 +2319,6 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                 if (!__any(running)) break;
                 const unsigned long long fin_lanes = __ballot(fin);
                 if (__popcll(fin_lanes) >= fetch_k) break;
-                /* a box pixel's query completed: its chain (the frame's critical path) moves on */
-                if (a.box_exit && (fin_lanes & costly_lanes)) break;
             }
             if (COUNT || RT_PLAIN_PIXEL_STATS) {
                 const unsigned long long dc = wave_clock() - t_c0;

@@ -250,9 +250,8 @@ int rt_sched_order_measured(RtSchedScratch &s, const uint32_t *iters, uint32_t W
     if (!n_t) return 0;
     int r = reserve(s, n_t, W * hl);
     if (r) return r;
-    /* the tile key's weight of its costliest pixel (RT_LPT_MAX: an A/B knob, default the probe key's) */
-    float wmax = (float)kLptMax;
-    if (const char *v = getenv("RT_LPT_MAX")) wmax = (float)atof(v);
+    /* the tile key's weight of its costliest pixel: the probe key's */
+    const float wmax = (float)kLptMax;
     hipLaunchKernelGGL(k_tile_cost_measured, dim3((n_t + 255u) / 256u), dim3(256), 0, st, iters, W, hl, nch, wmax,
                        s.keys, s.idx);
     hipError_t e = hipGetLastError();

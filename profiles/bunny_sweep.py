@@ -1,10 +1,9 @@
 """Sweep k_tris's stepping knobs on one context (GPU box): for each setting the frame's kernel
-time (median of --reps renders) with RTMI_FETCH_K / RTMI_FETCH_FRAC / RTMI_GRID_BLOCKS /
-RTMI_BOX_EXIT / RTMI_FETCH_K_BOX set
+time (median of --reps renders) with RTMI_FETCH_K / RTMI_FETCH_FRAC / RTMI_GRID_BLOCKS set
 (rt_host.cpp reads them at every render).  Settings alternate round after round.
 
     python profiles/bunny_sweep.py [--config bunny] [--reps 5] [--rounds 3] [--lib build.so] 24:24:0 16:24:0 ...
-    (K:FRAC:GRID[:BOXEXIT[:KBOX]]; GRID 0 = the host's grid, KBOX 0 = K)
+    (K:FRAC:GRID; GRID 0 = the host's grid)
 """
 from __future__ import annotations
 
@@ -48,12 +47,10 @@ def main():
     wall = {s: [] for s in args.settings}
     for r in range(args.rounds):
         for s in args.settings:
-            k, f, g, bx, kb = (s.split(":") + ["0"] * 4)[:5]
+            k, f, g = (s.split(":") + ["0"] * 2)[:3]
             os.environ["RTMI_FETCH_K"] = k
             os.environ["RTMI_FETCH_FRAC"] = f
             os.environ["RTMI_GRID_BLOCKS"] = g
-            os.environ["RTMI_BOX_EXIT"] = bx
-            os.environ["RTMI_FETCH_K_BOX"] = kb if kb != "0" else k
             rt.rayTrace(out, W, H, 0, kernel=pt.RayTracer.KERNEL_TRIS)  # settle
             for _ in range(args.reps):
                 t0 = time.perf_counter()

@@ -1,6 +1,5 @@
 """Seed-pass width A/B on the 8-way (or N-way) row-stripe tiles of a bench configuration: for each
-RT_SEED_WIDTH (lanes per long chain: 8-64 subtree-parallel k_chain_seeds, 3 coop_round; "W/C": C
-chains per wave, RT_SPLIT_GPW) a fresh
+RT_SEED_WIDTH (lanes per long chain: 8-64 subtree-parallel k_chain_seeds, 3 coop_round) a fresh
 context renders every rank's tile (best of --reps) and the slowest rank is reported, with the
 tile's frame bits checked equal across widths.
 
@@ -35,10 +34,7 @@ def main():
     ref = {}
     res = {}
     for spec in args.widths.replace(":", ",").split(","):
-        # "W" or "W/C": RT_SEED_WIDTH W with RT_SPLIT_GPW C chains per wave
-        wd, _, gpw = spec.partition("/")
-        os.environ["RT_SEED_WIDTH"] = wd
-        os.environ["RT_SPLIT_GPW"] = gpw or "0"
+        os.environ["RT_SEED_WIDTH"] = spec
         wd = spec
         rt = pt.RayTracer(0)
         rt.setSpheres(sc.ply_scene())

@@ -1537,12 +1537,48 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
         np.testing.assert_array_equal(s, frames[0][1])
 
 
+def test_tree_cull_knobs_change_no_bits(tracer, pt, monkeypatch):
+    """The host build's two culls are traversal savings only: a tree without the determinant cull's
+    normal boxes (RT_DET_CULL=0) and one that keeps the triangles no unit ray can hit
+    (RT_CULL_UNHITTABLE=0) render a frame of the dragon-class mesh (871,414 triangles, 66,533 of
+    them under the |det| >= 1e-4 rule for every unit ray, geometryFuncs.h:167) to the same bits and
+    seeds as the default tree, at sampleRate 4 with the candidate lists."""
+    sc = pt.scenes
+    W, H, sr = 160, 120, 4
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
+    seeds = sc.default_seeds(Wp, Hp, skip=5)
+    frames = []
+    for env in ({}, {"RT_DET_CULL": "0"}, {"RT_CULL_UNHITTABLE": "0"}, {"RT_DET_CULL": "0", "RT_CULL_UNHITTABLE": "0"}):
+        for k in ("RT_DET_CULL", "RT_CULL_UNHITTABLE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        c = sc.PLY_CAMERA
+        rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)  # the knobs are read by the build
+        info = rt.meshInfo()
+        rt.setSeeds(Wp, Hp, seeds)
+        out = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        frames.append((bits(out).copy(), rt.getSeeds().copy(), info["n_tris_tree"]))
+        rt.close()
+    assert frames[0][2] < len(idx) and frames[2][2] == len(idx), [f[2] for f in frames]
+    for f, s_, _ in frames[1:]:
+        np.testing.assert_array_equal(f, frames[0][0])
+        np.testing.assert_array_equal(s_, frames[0][1])
+
+
 def test_stepping_knobs_change_no_bits(tracer, pt, monkeypatch):
     """k_tris's stepping-round exit rule and its grid are scheduling only: a short frame (1 spp,
     so the short-frame grid of 3 blocks per CU) renders to the same bits and seeds with a grid of
     7 blocks, with the round ending at every completed query, with it ending only when 64 have
-    completed (no live-lane rule), and with box-pixel waves leaving at their first completion
-    (RTMI_* knobs, read at every render)."""
+    completed (no live-lane rule), and with the live-lane rule alone (RTMI_* knobs, read at every
+    render)."""
     sc = pt.scenes
     W, H, sr = 256, 192, 1
     Wp, Hp = sc.padded_dims(W, H)
@@ -1555,10 +1591,10 @@ def test_stepping_knobs_change_no_bits(tracer, pt, monkeypatch):
     rt.setSampleRate(sr)
     rt.setMaxPathDepth(6)
     rt.setMesh(verts, idx)
-    knobs = ("RTMI_GRID_BLOCKS", "RTMI_FETCH_K", "RTMI_FETCH_FRAC", "RTMI_BOX_EXIT", "RTMI_FETCH_K_BOX")
+    knobs = ("RTMI_GRID_BLOCKS", "RTMI_FETCH_K", "RTMI_FETCH_FRAC")
     frames = []
     for env in ({}, {"RTMI_GRID_BLOCKS": "7"}, {"RTMI_FETCH_K": "1"}, {"RTMI_FETCH_K": "64", "RTMI_FETCH_FRAC": "0"},
-                {"RTMI_BOX_EXIT": "1", "RTMI_FETCH_K_BOX": "3"}):
+                {"RTMI_FETCH_K": "64", "RTMI_FETCH_FRAC": "16"}):
         for k in knobs:
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():

@@ -248,7 +248,9 @@ typedef struct rt_render_info {
     uint32_t split_hit_depth;  /* 1: the long chains' chunk tasks answered their box segments' closest-hit
                                   queries from the seed pass's per-sample mesh-hit depths (no traversal) */
     uint32_t schedule_measured; /* 1: the queue's tiles were ordered by the view's previous frame's measured
-                                   per-pixel costs (its wave iterations), not by the cost probe */
+                                   per-pixel costs (its traversal steps), not by the cost probe */
+    uint32_t schedule_pilot;    /* 1: a view's first frame, ordered by the per-pixel costs of a pilot render of
+                                   a few samples per pixel (scratch seeds and framebuffer), not by the probe */
 } rt_render_info;
 int rt_last_render_info(rt_ctx *ctx, rt_render_info *out);
 /* The long chains of the last sample-split render (pixels_long of them: tile-local y * W + x, the

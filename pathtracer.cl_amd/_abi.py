@@ -145,6 +145,7 @@ class RtRenderInfo(ctypes.Structure):
         ("split_repaired", ctypes.c_uint32),
         ("split_hit_depth", ctypes.c_uint32),
         ("schedule_measured", ctypes.c_uint32),
+        ("schedule_pilot", ctypes.c_uint32),
     ]
 
 

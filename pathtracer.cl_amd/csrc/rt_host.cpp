@@ -221,6 +221,13 @@ struct rt_ctx {
     uint32_t *d_stripe_map = nullptr;
     size_t stripe_map_cap = 0;
     uint32_t stripe_map_serial = 0;
+    /* the pilot render of a view's first frame (pilot_order): its seeds, framebuffer and counters +
+       queue cursors, apart from the frame's */
+    int pilot_sr = 2; /* RT_PILOT (test knob): the pilot's sampleRate, 0 = no pilot (the probe's order) */
+    uint32_t *d_pilot_seeds = nullptr;
+    float *d_pilot_out = nullptr;
+    unsigned long long *d_pilot_cnt = nullptr;
+    size_t pilot_seed_words = 0, pilot_out_floats = 0;
     /* rt_partition_stripes: the last map and what it was computed for */
     std::vector<uint32_t> part_key, part_owner;
     uint32_t *d_part_probe = nullptr;
@@ -820,9 +827,14 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     const bool split = split_wanted(c, npx, (uint64_t)blocks * RT_BLOCK);
     RtTriLaunch pa = a;
     pa.probe_n = split && c->sample_rate >= 4 ? c->split_probe : probe_n(c->sample_rate);
+    /* a whole-pixel frame that a pilot render will order (pilot_order): the probe only classes the
+       pixels (box pixels: the issue priority), one ray each */
+    const bool pilot_next = !split && c->pilot_sr > 0 && c->sample_rate * c->sample_rate >= 16u && !c->counting;
+    if (pilot_next) pa.probe_n = 1;
     const uint32_t pn2 = pa.probe_n * pa.probe_n;
     int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
     if (e) return hip_fail(c, (hipError_t)e, "probe launch");
+    /* (the probe's order even then: the frame falls back to it should the pilot not run) */
     e = rt_sched_order(c->sched, c->d_flags, W, hl, pn2, (uint32_t)c->lights.size(), c->max_depth, c->d_order, st);
     if (e) return hip_fail(c, (hipError_t)e, "tile order");
     /* speculated mesh pixels: the silhouettes' neighbours run as long chains (RT_SPLIT_SPEC=2: every
@@ -850,6 +862,52 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     c->n_split_box = n_box;
     c->order_key = key;
     c->schedule_rebuilt = true;
+    return RT_OK;
+}
+
+/* The first frame of a view, whole pixels of many samples: its queue order from a pilot render
+   instead of the cost probe.  The probe's few rays per pixel aim their shadow rays at the light
+   centres and miss where the samples' rays graze the mesh; the view's next frames are ordered by
+   the measured per-pixel costs of the frame before, and the first frame had only
+   the probe.  The pilot is the same kernel on the same pixels at pilot_sr^2 samples per pixel,
+   with candidate lists built, from a copy of the seeds into a scratch framebuffer and its own
+   counters and queue cursors, recording each pixel's traversal steps; the tiles are then sorted
+   by them exactly as a measured frame's (rt_sched_order_measured).  Scheduling only: the frame's
+   seeds, output and counters are not touched. */
+int pilot_order(rt_ctx *c, const RtTriLaunch &a, int trav, int blocks, hipStream_t st)
+{
+    const size_t seed_words = 2ull * c->wpad * c->hpad, out_floats = (size_t)a.W * a.Hl * 4;
+    if (c->pilot_seed_words < seed_words) {
+        free_dev(c->d_pilot_seeds);
+        c->d_pilot_seeds = nullptr;
+        c->pilot_seed_words = 0;
+        HIPCHK(c, hipMalloc(&c->d_pilot_seeds, seed_words * sizeof(uint32_t)));
+        c->pilot_seed_words = seed_words;
+    }
+    if (c->pilot_out_floats < out_floats) {
+        free_dev(c->d_pilot_out);
+        c->d_pilot_out = nullptr;
+        c->pilot_out_floats = 0;
+        HIPCHK(c, hipMalloc(&c->d_pilot_out, out_floats * sizeof(float)));
+        c->pilot_out_floats = out_floats;
+    }
+    if (!c->d_pilot_cnt) HIPCHK(c, hipMalloc(&c->d_pilot_cnt, kCounterBytes + kWorkWords * sizeof(uint32_t)));
+    HIPCHK(c, hipMemcpyAsync(c->d_pilot_seeds, c->d_seeds, seed_words * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, hipMemsetAsync(c->d_pilot_cnt, 0, kCounterBytes + kWorkWords * sizeof(uint32_t), st));
+    RtTriLaunch p = a;
+    p.seeds = c->d_pilot_seeds;
+    p.out = c->d_pilot_out;
+    p.progressive = 0;
+    p.sample_rate = (uint32_t)c->pilot_sr;
+    p.counters = c->d_pilot_cnt;
+    p.work_counter = reinterpret_cast<uint32_t *>(c->d_pilot_cnt + RT_COUNTER_WORDS);
+    p.take_exact = 0; /* a short-task launch: batched takes from the multi-head queue */
+    p.queue_batch = RT_QUEUE_BATCH;
+    p.pixel_stats = nullptr;
+    p.pixel_iter = c->d_pixel_iter;
+    int e = rt_launch_tris(p, trav, false, blocks, st);
+    if (!e) e = rt_sched_order_measured(c->sched, c->d_pixel_iter, a.W, a.Hl, 1u, c->d_order, st);
+    if (e) return hip_fail(c, (hipError_t)e, "pilot render");
     return RT_OK;
 }
 
@@ -923,6 +981,7 @@ try {
         else fprintf(stderr, "[rtmi] RT_SEED_WIDTH=%s ignored (0, 1, 3 or a power of two from 8 to 64)\n", v);
     }
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
+    if (const char *v = getenv("RT_PILOT")) c->pilot_sr = std::max(0, std::min(8, atoi(v))); /* test knob */
     c->repair_slots = std::max(1u, env_u32("RT_REPAIR_SLOTS", RT_REPAIR_SLOTS)); /* test knob: the path beyond them */
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -987,6 +1046,9 @@ try {
     free_dev(c->d_counters); /* d_work lives in it */
     free_dev(c->d_totals);
     free_dev(c->d_stripe_map);
+    free_dev(c->d_pilot_seeds);
+    free_dev(c->d_pilot_out);
+    free_dev(c->d_pilot_cnt);
     free_dev(c->d_part_probe);
     free_dev(c->d_part_cost);
     if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -1792,6 +1854,12 @@ try {
                                                 c->d_list_code, c->d_list_tile, st)
                         : 0;
         if (e) c->list_key.clear();
+        /* a view's first frame of whole pixels: its order from a pilot render (pilot_order) */
+        const bool pilot = !e && record_iter && !a.split_chunks && c->schedule_rebuilt && c->pilot_sr > 0 && !c->counting;
+        if (pilot) {
+            const int rp = pilot_order(c, a, trav, blocks, st);
+            if (rp != RT_OK) return rp;
+        }
         HIPCHK(c, hipEventRecord(c->evm, st));
         if (!e && lists && getenv("RT_LIST_STATS")) { /* diagnostics: candidate list lengths */
             std::vector<uint16_t> h((size_t)npx);
@@ -1833,6 +1901,7 @@ try {
         c->info.schedule_measured = a.tile_order && c->order_measured ? 1u : 0u;
         c->info.schedule_rebuilt = c->schedule_rebuilt ? 1u : 0u;
         c->info.schedule_host_ms = sched_ms;
+        c->info.schedule_pilot = pilot ? 1u : 0u;
         c->info_list_pending = lists;
         if (d_stats) {
             std::vector<uint32_t> h((size_t)W * hl * 8);

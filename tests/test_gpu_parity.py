@@ -1506,17 +1506,19 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     seeds with the queue row-major (RT_SCHEDULE=0), with the default schedule (a sample-split
     render: few pixels per lane), with whole-pixel tasks (RT_SPLIT=0), with the split forced
     on, with split buffers too small for the frame (RT_SPLIT_MB=1: whole pixels again), with
-    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0), and
-    with a list area too small for every pixel (RT_LIST_MB=2)."""
+    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0), with
+    a list area too small for every pixel (RT_LIST_MB=2), and — whole pixels — with the first
+    frame's order from the probe instead of a pilot render (RT_PILOT=0) or from a 9-spp pilot."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
     verts, idx = sc.make_mesh(20_000)
     seeds = sc.default_seeds(Wp, Hp, skip=7)
     frames = []
-    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_SPLIT": "0"}, {"RT_SPLIT": "1"}, {"RT_SPLIT": "1", "RT_SPLIT_MB": "1"},
+    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_SPLIT": "0"}, {"RT_SPLIT": "0", "RT_PILOT": "0"},
+                {"RT_SPLIT": "0", "RT_PILOT": "3"}, {"RT_SPLIT": "1"}, {"RT_SPLIT": "1", "RT_SPLIT_MB": "1"},
                 {"RT_PIXEL_LISTS": "0"}, {"RT_LIST_MB": "2"}):
-        for k in ("RT_SCHEDULE", "RT_SPLIT", "RT_SPLIT_MB", "RT_PIXEL_LISTS", "RT_LIST_MB"):
+        for k in ("RT_SCHEDULE", "RT_SPLIT", "RT_SPLIT_MB", "RT_PIXEL_LISTS", "RT_LIST_MB", "RT_PILOT"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -1530,6 +1532,9 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
         rt.setSeeds(Wp, Hp, seeds)
         out = np.zeros(W * H * 4, np.float32)
         rt.rayTrace(out, W, H, 0, kernel=2)
+        info = rt.renderInfo()
+        if env.get("RT_SPLIT") == "0":
+            assert info["schedule_pilot"] == (0 if env.get("RT_PILOT") == "0" else 1), (env, info)
         frames.append((bits(out).copy(), rt.getSeeds().copy()))
         rt.close()
     for f, s in frames[1:]:

@@ -702,6 +702,10 @@ def roofline_block(pt, kernel, cnt, traversal, pix, k_ms, workload, n_ranks, cha
     alg_gbps = alg_bytes / sec / 1e9
     out = {"bound": "hbm", "achieved": round(alg_gbps, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(alg_gbps / HBM_PEAK_GBS, 4),
+           # the same algorithmic bytes over the committed steady-state profile's kernel time
+           # (profiles/<run>/pmc_summary.json: rocprofv3 over the steady-state frames only)
+           "frac_profiled": (round(pm["algorithmic_frac_of_hbm_peak"], 4)
+                             if pm and pm.get("algorithmic_frac_of_hbm_peak") else None),
            "traffic": pm["hbm_bytes_per_launch"] if pm else None,
            "traffic_unit": "HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE, PMC)" if pm else None,
            "traffic_source": pm["source"] if pm else None,

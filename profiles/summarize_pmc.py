@@ -14,7 +14,10 @@ config), with the gfx950 rules of MI355X_MICROARCH.md §HBM:
   - vector-memory address path: TA_BUSY_avr / kernel cycles;
   - L2 hit rate, wave-cycle breakdown, effective clock.
 
-    python profiles/summarize_pmc.py <tag> [gpurun_out/prof_<tag>] [workload] [kernel]
+    python profiles/summarize_pmc.py <tag> [gpurun_out/prof_<tag>] [workload] [kernel] [--last N]
+
+--last N: only the kernel's last N full-size dispatches of every pass (the steady-state frames of
+profiles/steady_state.py, whose earlier dispatches are a view's pilot and first frames).
 """
 from __future__ import annotations
 
@@ -29,9 +32,10 @@ ROOT = Path(__file__).resolve().parent.parent
 N_CU, N_SIMD, N_XCD = 256, 1024, 8
 
 
-def counters(paths, kernel):
+def counters(paths, kernel, last=0):
     """mean over the kernel's full-size dispatches (the largest grid: bench.py also launches the
-    kernel on 1-row tiles for its critical-path figure), per counter, over the collection files"""
+    kernel on 1-row tiles for its critical-path figure) — the last `last` of them if > 0 — per
+    counter, over the collection files"""
     tot = defaultdict(list)
     for path in paths:
         per = defaultdict(lambda: defaultdict(float))
@@ -41,32 +45,41 @@ def counters(paths, kernel):
                 per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
                 grid[r["Dispatch_Id"]] = int(r["Grid_Size"])
         gmax = max(grid.values()) if grid else 0
-        for did, d in per.items():
-            if grid[did] != gmax:
-                continue
-            for k, v in d.items():
+        ids = sorted((did for did in per if grid[did] == gmax), key=int)
+        for did in ids[-last:] if last else ids:
+            for k, v in per[did].items():
                 tot[k].append(v)
     return {k: sum(v) / len(v) for k, v in tot.items()}
 
 
-def kernel_ns(src, kernel):
-    """mean duration and count of the kernel's full-size dispatches in the kernel trace"""
+def kernel_ns(src, kernel, last=0):
+    """mean duration and count of the kernel's full-size dispatches in the kernel trace (the last
+    `last` of them if > 0, in start order)"""
     rows = [r for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")) if kernel in r["Kernel_Name"]]
     size = lambda r: int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
     gmax = max(size(r) for r in rows)
-    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if size(r) == gmax]
+    full = sorted((r for r in rows if size(r) == gmax), key=lambda r: int(r["Start_Timestamp"]))
+    if last:
+        full = full[-last:]
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in full]
     return sum(d) / len(d), len(d)
 
 
 def main():
-    tag = sys.argv[1]
-    src = Path(sys.argv[2]) if len(sys.argv) > 2 else ROOT / "gpurun_out" / f"prof_{tag}"
-    workload = sys.argv[3] if len(sys.argv) > 3 else None
-    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_tris<4, false, false, true>"
+    argv = list(sys.argv[1:])
+    last = 0
+    if "--last" in argv:
+        i = argv.index("--last")
+        last = int(argv[i + 1])
+        del argv[i:i + 2]
+    tag = argv[0]
+    src = Path(argv[1]) if len(argv) > 1 else ROOT / "gpurun_out" / f"prof_{tag}"
+    workload = argv[2] if len(argv) > 2 else None
+    kernel = argv[3] if len(argv) > 3 else "k_tris<4, false, false, true>"
     files = sorted(glob.glob(f"{src}/pmc_*/run_counter_collection.csv")) + sorted(
         glob.glob(f"{src}/pmcx_*/run_counter_collection.csv"))
-    c = counters(files, kernel)
-    avg_ns, n_disp = kernel_ns(src, kernel)
+    c = counters(files, kernel, last)
+    avg_ns, n_disp = kernel_ns(src, kernel, last)
     cyc = c["GRBM_GUI_ACTIVE"] / N_XCD if c.get("GRBM_GUI_ACTIVE") else None
     fetch_b = 2 * c["FETCH_SIZE"] * 1024 if c.get("FETCH_SIZE") else None
     write_b = c["WRITE_SIZE"] * 1024 if c.get("WRITE_SIZE") else None
@@ -78,6 +91,7 @@ def main():
         "kernel": kernel,
         "avg_kernel_ms_rocprof": avg_ns / 1e6,
         "dispatches": n_disp,
+        "dispatch_selection": f"the last {last} full-grid dispatches (steady state)" if last else "every full-grid dispatch",
         "fetch_size_kb": c.get("FETCH_SIZE"),
         "write_size_kb": c.get("WRITE_SIZE"),
         "hbm_read_bytes_corrected": fetch_b,
@@ -99,6 +113,13 @@ def main():
         "sq_active_inst_frac": frac(c.get("SQ_ACTIVE_INST_ANY"), c.get("SQ_WAVE_CYCLES")),
         "counters": c,
     }
+    drv = src / "driver.json"  # profiles/steady_state.py's line: the counting launch's algorithmic bytes
+    if drv.exists() and drv.read_text().strip():
+        d = json.loads(drv.read_text().strip().splitlines()[-1])
+        summ["algorithmic_bytes_per_launch"] = d["algorithmic_bytes_per_launch"]
+        summ["algorithmic_gbps"] = d["algorithmic_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9
+        summ["algorithmic_frac_of_hbm_peak"] = summ["algorithmic_gbps"] / 8000.0
+        summ["driver"] = d
     out = ROOT / "profiles" / tag
     out.mkdir(parents=True, exist_ok=True)
     (out / "pmc_summary.json").write_text(json.dumps(summ, indent=1) + "\n")
@@ -108,7 +129,10 @@ def main():
         allw[workload] = {key: summ[key] for key in (
             "kernel", "avg_kernel_ms_rocprof", "hbm_bytes_per_launch", "effective_clock_ghz", "sq_insts_valu",
             "sq_insts_salu", "ta_busy_avr", "kernel_cycles_per_xcd", "valu_issue_frac", "salu_issue_frac",
-            "ta_busy_frac", "l2_hit_rate")}
+            "ta_busy_frac", "l2_hit_rate", "dispatches", "dispatch_selection")}
+        for key in ("algorithmic_bytes_per_launch", "algorithmic_frac_of_hbm_peak"):
+            if key in summ:
+                allw[workload][key] = summ[key]
         allw[workload]["source"] = f"profiles/{tag}/pmc_summary.json"
         p.write_text(json.dumps(allw, indent=1) + "\n")
     print(json.dumps({k: v for k, v in summ.items() if k != "counters"}, indent=1))

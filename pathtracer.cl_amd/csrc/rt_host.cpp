@@ -106,6 +106,10 @@ constexpr uint32_t kWorkBox = RT_QSTRIDE * RT_QHEADS, kWorkRepair = RT_QSTRIDE *
 constexpr uint32_t kFetchK = RT_FETCH_K;
 constexpr uint64_t kShortFrameSamplesPerLane = 8; /* below: a short frame (fewer blocks per CU) */
 constexpr int kShortFrameBlocksPerCU = 3;
+/* the pilot render (pilot_order) only for frames of at least this many samples per pixel: its 4 spp
+   are 1.6 % of a 256-spp frame, but a quarter of the Lucy class's 16-spp frame (133 against 506 ms,
+   profiles/r06f), which keeps the probe's order */
+constexpr uint32_t kPilotMinSpp = 64;
 /* an unsigned environment knob (tuning sweeps), `def` when unset or unparsable */
 uint32_t env_u32(const char *name, uint32_t def)
 {
@@ -829,7 +833,7 @@ int tile_order(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
     pa.probe_n = split && c->sample_rate >= 4 ? c->split_probe : probe_n(c->sample_rate);
     /* a whole-pixel frame that a pilot render will order (pilot_order): the probe only classes the
        pixels (box pixels: the issue priority), one ray each */
-    const bool pilot_next = !split && c->pilot_sr > 0 && c->sample_rate * c->sample_rate >= 16u && !c->counting;
+    const bool pilot_next = !split && c->pilot_sr > 0 && c->sample_rate * c->sample_rate >= kPilotMinSpp && !c->counting;
     if (pilot_next) pa.probe_n = 1;
     const uint32_t pn2 = pa.probe_n * pa.probe_n;
     int e = rt_launch_probe_cost(pa, blocks, c->d_flags, st);
@@ -1855,7 +1859,8 @@ try {
                         : 0;
         if (e) c->list_key.clear();
         /* a view's first frame of whole pixels: its order from a pilot render (pilot_order) */
-        const bool pilot = !e && record_iter && !a.split_chunks && c->schedule_rebuilt && c->pilot_sr > 0 && !c->counting;
+        const bool pilot = !e && record_iter && !a.split_chunks && c->schedule_rebuilt && c->pilot_sr > 0 && !c->counting &&
+                           c->sample_rate * c->sample_rate >= kPilotMinSpp;
         if (pilot) {
             const int rp = pilot_order(c, a, trav, blocks, st);
             if (rp != RT_OK) return rp;

@@ -156,9 +156,8 @@ def test_bunny_config_whole_frame_vs_bvh_oracle(tracer, pt, oracle):
 def test_dragon_whole_frame_sr4_vs_bvh_oracle(tracer, pt, dragon, dragon_sr4):
     """BASELINE configs[3]'s frame (dragon class, 871,414 triangles, 1920x1080, maxDepth 6) at
     sampleRate 4: all 2,073,600 pixels, both seed planes and the ray counts equal to the oracle's —
-    rendered under the order of a pilot render (scratch seeds and framebuffer: the frame's own must
-    be untouched by it), then again from the same seeds under the order re-sorted by the first
-    render's measured per-pixel costs (16 spp, whole pixels: DESIGN §4.4)."""
+    rendered under the probe's order, then again from the same seeds under the order re-sorted by
+    the first render's measured per-pixel costs (16 spp, whole pixels: DESIGN §4.4)."""
     d = dragon
     exp, sd, c_or = dragon_sr4
     rt = _tracer(pt, d, 4)
@@ -169,7 +168,7 @@ def test_dragon_whole_frame_sr4_vs_bvh_oracle(tracer, pt, dragon, dragon_sr4):
         rt.rayTrace(got, d["W"], d["H"], 0, kernel=2)
         info = rt.renderInfo()
         assert info["lists"] == 1 and info["split_chunks"] == 0 and info["schedule_measured"] == k, info
-        assert info["schedule_pilot"] == 1 - k, info  # the view's first frame: ordered by a pilot render
+        assert info["schedule_pilot"] == 0, info  # (16 spp: no pilot render, test_pilot_order_changes_no_bits)
         np.testing.assert_array_equal(bits(got), bits(exp), err_msg=f"render {k}")
         np.testing.assert_array_equal(rt.getSeeds(), sd, err_msg=f"render {k}")
         cnt = rt.counters()

@@ -1506,19 +1506,17 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
     seeds with the queue row-major (RT_SCHEDULE=0), with the default schedule (a sample-split
     render: few pixels per lane), with whole-pixel tasks (RT_SPLIT=0), with the split forced
     on, with split buffers too small for the frame (RT_SPLIT_MB=1: whole pixels again), with
-    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0), with
-    a list area too small for every pixel (RT_LIST_MB=2), and — whole pixels — with the first
-    frame's order from the probe instead of a pilot render (RT_PILOT=0) or from a 9-spp pilot."""
+    camera rays traversing the tree instead of their candidate lists (RT_PIXEL_LISTS=0), and
+    with a list area too small for every pixel (RT_LIST_MB=2)."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
     verts, idx = sc.make_mesh(20_000)
     seeds = sc.default_seeds(Wp, Hp, skip=7)
     frames = []
-    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_SPLIT": "0"}, {"RT_SPLIT": "0", "RT_PILOT": "0"},
-                {"RT_SPLIT": "0", "RT_PILOT": "3"}, {"RT_SPLIT": "1"}, {"RT_SPLIT": "1", "RT_SPLIT_MB": "1"},
+    for env in ({"RT_SCHEDULE": "0"}, {}, {"RT_SPLIT": "0"}, {"RT_SPLIT": "1"}, {"RT_SPLIT": "1", "RT_SPLIT_MB": "1"},
                 {"RT_PIXEL_LISTS": "0"}, {"RT_LIST_MB": "2"}):
-        for k in ("RT_SCHEDULE", "RT_SPLIT", "RT_SPLIT_MB", "RT_PIXEL_LISTS", "RT_LIST_MB", "RT_PILOT"):
+        for k in ("RT_SCHEDULE", "RT_SPLIT", "RT_SPLIT_MB", "RT_PIXEL_LISTS", "RT_LIST_MB"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -1532,14 +1530,63 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
         rt.setSeeds(Wp, Hp, seeds)
         out = np.zeros(W * H * 4, np.float32)
         rt.rayTrace(out, W, H, 0, kernel=2)
-        info = rt.renderInfo()
-        if env.get("RT_SPLIT") == "0":
-            assert info["schedule_pilot"] == (0 if env.get("RT_PILOT") == "0" else 1), (env, info)
         frames.append((bits(out).copy(), rt.getSeeds().copy()))
         rt.close()
     for f, s in frames[1:]:
         np.testing.assert_array_equal(f, frames[0][0])
         np.testing.assert_array_equal(s, frames[0][1])
+
+
+def test_pilot_order_changes_no_bits(tracer, pt, oracle, monkeypatch):
+    """The first frame of a view of >= 64 samples per pixel is ordered by a pilot render (DESIGN
+    §4.4: the same kernel at 2x2 samples per pixel from a copy of the seeds, into a scratch
+    framebuffer, with its own counters and queue cursors).  Nothing of it may reach the frame: at
+    sampleRate 8 (64 spp, whole pixels) the frame, both seed planes and the ray counts are the same
+    with the pilot (default), with a 3x3 pilot and without one (RT_PILOT=0: the probe's order), and
+    equal to the oracle's; the view's next frame is ordered by the first frame's measured costs."""
+    sc = pt.scenes
+    W, H, sr = 96, 72, 8
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    seeds = sc.default_seeds(Wp, Hp, skip=9)
+    frames = []
+    for pilot in (None, "3", "0"):
+        monkeypatch.delenv("RT_PILOT", raising=False)
+        monkeypatch.setenv("RT_SPLIT", "0")  # whole pixels (a 96x72 frame would render sample-split)
+        if pilot is not None:
+            monkeypatch.setenv("RT_PILOT", pilot)
+        rt = pt.RayTracer(0)  # the knobs are read when the context is created
+        rt.setSpheres(sc.ply_scene())
+        c = sc.PLY_CAMERA
+        rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        out = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        info = rt.renderInfo()
+        assert info["split_chunks"] == 0 and info["schedule_pilot"] == (0 if pilot == "0" else 1), (pilot, info)
+        cnt = rt.counters()
+        frames.append((bits(out).copy(), rt.getSeeds().copy(), (cnt["rays_closest"], cnt["rays_shadow"])))
+        rt.setSeeds(Wp, Hp, seeds)
+        rt.rayTrace(out, W, H, 0, kernel=2)
+        info = rt.renderInfo()
+        assert info["schedule_pilot"] == 0 and info["schedule_measured"] == 1, (pilot, info)
+        np.testing.assert_array_equal(bits(out), frames[-1][0])
+        rt.close()
+    for f, s_, c_ in frames[1:]:
+        np.testing.assert_array_equal(f, frames[0][0])
+        np.testing.assert_array_equal(s_, frames[0][1])
+        assert c_ == frames[0][2]
+    exp = np.zeros(W * H * 4, np.float32)
+    sd = seeds.copy()
+    cam = sc.camera_spherical(W, **sc.PLY_CAMERA)
+    c_or = oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, sr, 6, 0, sd, verts, idx,
+                              bvh=oracle.build_bvh(verts, idx))
+    np.testing.assert_array_equal(frames[0][0], bits(exp))
+    np.testing.assert_array_equal(frames[0][1], sd)
+    assert frames[0][2] == tuple(c_or)
 
 
 def test_tree_cull_knobs_change_no_bits(tracer, pt, monkeypatch):

@@ -267,8 +267,10 @@ struct rt_ctx {
     bool counters_zeroed = false;                 /* the last render ended with k_counters_out: no fill needed */
     unsigned long long *d_totals = nullptr;     /* running totals over renders (k_counters_out; rt_counter_totals) */
     hipStream_t sync_stream = nullptr;          /* the stream of the last render (rt_synchronize waits on it) */
-    hipEvent_t ev_done = nullptr;               /* recorded after the last render's counter hand-back: a render on
-                                                   another stream waits for it (its counters and queue cursors) */
+    hipEvent_t ev_done = nullptr;               /* the end of the last render's counter hand-back: a render on another
+                                                   stream waits for it (the counters, the queue cursors).  Recorded at
+                                                   the render's end on a caller's stream (which may be gone later), and
+                                                   only when needed on the context's own (no per-frame record there) */
     float *d_stage = nullptr;
     size_t stage_bytes = 0;
     rt_counters last = {};
@@ -1390,7 +1392,10 @@ try {
     }
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    if (c->sync_stream && c->sync_stream != st) HIPCHK(c, hipStreamWaitEvent(st, c->ev_done, 0));
+    if (c->sync_stream && c->sync_stream != st) {
+        if (c->sync_stream == c->stream) HIPCHK(c, hipEventRecord(c->ev_done, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_done, 0));
+    }
     const size_t npx = (size_t)W * H;
     if (c->part_probe_px < npx) {
         HIPCHK(c, hipStreamSynchronize(st));
@@ -1561,7 +1566,10 @@ try {
     }
     /* a render on another stream than the last one's: ordered after that render's counter hand-back
        (which reads and zeroes the counters and queue cursors this render uses) */
-    if (c->sync_stream && st != c->sync_stream) HIPCHK(c, hipStreamWaitEvent(st, c->ev_done, 0));
+    if (c->sync_stream && st != c->sync_stream) {
+        if (c->sync_stream == c->stream) HIPCHK(c, hipEventRecord(c->ev_done, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(st, c->ev_done, 0));
+    }
     /* the counters, the guard word and the queue cursors: one memset (none when the last render's
        k_counters_out left them zeroed) */
     if (!c->counters_zeroed)
@@ -1963,7 +1971,7 @@ try {
     if (c->info.lists_rebuilt)
         HIPCHK(c, hipMemcpyAsync(c->h_counters + RT_COUNTER_WORDS, c->d_list_alloc, sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, st));
-    HIPCHK(c, hipEventRecord(c->ev_done, st));
+    if (st != c->stream) HIPCHK(c, hipEventRecord(c->ev_done, st));
     c->sync_stream = st;
     c->have_timing = true;
     c->last_out = dout;
@@ -2220,7 +2228,9 @@ try {
                 }
             }
         c->counters_zeroed = false; /* this trace leaves its counts there */
-        if (c->sync_stream && c->sync_stream != c->stream) e = hipStreamWaitEvent(c->stream, c->ev_done, 0);
+        if (c->sync_stream && c->sync_stream != c->stream) {
+            e = hipStreamWaitEvent(c->stream, c->ev_done, 0); /* (recorded on the caller's stream) */
+        }
         if (e == hipSuccess && c->counting) e = hipMemsetAsync(c->d_counters, 0, RT_COUNTER_WORDS * sizeof(unsigned long long), c->stream);
         if (e == hipSuccess) {
             const int le = rt_launch_trace_rays(trav_nodes(c), c->d_tris, c->n_tris, d_rays, n, any_hit, kind, c->d_spill,

@@ -1537,6 +1537,57 @@ def test_schedule_changes_no_bits(tracer, pt, monkeypatch):
         np.testing.assert_array_equal(s, frames[0][1])
 
 
+def test_renders_on_alternating_streams(tracer, pt):
+    """rt_render_async on a different stream from the previous render's: the new render
+    is ordered after the previous one's counter hand-back (which reads and zeroes the counters and
+    queue cursors it uses) and so after its seed and framebuffer writes.  Progressive frames enqueued
+    without a host wait, alternately on the context's stream and on two torch streams, end in the same
+    framebuffer, seeds and per-frame ray counts as the same frames rendered one by one, and the
+    device-side counter totals (rt_counter_totals) add up every frame's counts."""
+    import torch
+
+    sc = pt.scenes
+    W, H, sr = 128, 96, 2
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    seeds = sc.default_seeds(Wp, Hp, skip=13)
+
+    def make():
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        c = sc.PLY_CAMERA
+        rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
+        rt.setSampleRate(sr)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        return rt
+
+    ref = make()
+    exp = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
+    rays = 0
+    for p in range(6):
+        ref.rayTrace(exp, W, H, p, kernel=2)
+        c = ref.counters()
+        rays += c["rays_closest"] + c["rays_shadow"]
+    exp_seeds = ref.getSeeds()
+    ref.close()
+    rt = make()
+    got = torch.zeros_like(exp)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    rt.rayTrace(got, W, H, 0, kernel=2)  # the schedule and lists (host work) before the async frames
+    rt.setSeeds(Wp, Hp, seeds)
+    rt.counterTotals(reset=True)
+    for p, st in enumerate([None, s1.cuda_stream, s2.cuda_stream, None, s2.cuda_stream, s1.cuda_stream]):
+        rt.rayTrace(got, W, H, p, kernel=2, stream=st, sync=False)
+    tot = rt.counterTotals(reset=True)
+    torch.cuda.synchronize()
+    assert tot["renders"] == 6 and tot["rays_closest"] + tot["rays_shadow"] == rays, tot
+    assert torch.equal(got.view(torch.int32), exp.view(torch.int32))
+    np.testing.assert_array_equal(rt.getSeeds(), exp_seeds)
+    rt.close()
+
+
 def test_pilot_order_changes_no_bits(tracer, pt, oracle, monkeypatch):
     """The first frame of a view of >= 64 samples per pixel is ordered by a pilot render (DESIGN
     §4.4: the same kernel at 2x2 samples per pixel from a copy of the seeds, into a scratch

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--config", default="dragon")
     ap.add_argument("--tile", default=None)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--balanced", action="store_true", help="the tile under rt_partition_stripes' owner map")
     ap.add_argument("--lib", default=None, help="another build of librtmi.so (A/B)")
     ap.add_argument("--env", action="append", default=[], help="NAME=VALUE set before the context is created")
     args = ap.parse_args()
@@ -37,6 +38,8 @@ def main():
     rt.setMaxPathDepth(6)
     rt.setMesh(*sc.make_mesh(sc.MESH_CONFIGS[args.config]))
     tile = tuple(int(v) for v in args.tile.replace(":", ",").split(",")) if args.tile else None
+    if tile and args.balanced:
+        tile = tile + (rt.partitionStripes(W, H, tile[0], tile[1]),)
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
     for _ in range(args.reps):
         rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)

@@ -4,7 +4,8 @@
 Workload (BASELINE.json configs[3], the metric's config): 871,414-triangle
 synthetic mesh (dragon class), 1920x1080, sampleRate 16 (256 spp, one launch,
 progression 0), maxDepth 6, plymain.cpp lights and camera, BVH traversal.
-One step = one full frame: every rank renders its interleaved row stripes (rt_tile) and,
+One step = one full frame: every rank renders its row stripes (rt_tile; dealt by their probed
+cost, rt_partition_stripes, unless --partition interleaved) and,
 for N > 1, the frame is gathered to rank 0 over RCCL — by librtmi's own communicator
 (rt_comm_render: seed-row halo, grouped ncclSend/ncclRecv, device-side assembly; the
 default, `--comm native`) or by torch.distributed (`--comm torch`, also the gloo rehearsal).

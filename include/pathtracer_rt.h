@@ -347,8 +347,8 @@ int rt_comm_render(rt_comm *comm, rt_ctx *ctx, float *frame_dev, uint32_t width,
 int rt_comm_reset_halo(rt_comm *comm);
 /* Partition of rt_comm_render's frames: RT_PARTITION_INTERLEAVED (stripe s to rank
    s % n_ranks) or RT_PARTITION_BALANCED (the default: raytrace_tris frames by
-   rt_partition_stripes, computed by every rank for each new view and checked against the
-   root's with one broadcast; sphere frames stay interleaved).  A change of owner moves the
+   rt_partition_stripes, computed by every rank for each new view, every rank then taking the
+   root's map from one broadcast; sphere frames stay interleaved).  A change of owner moves the
    stripe's seed rows through the halo (rt_seed_halo_plan).  rt_comm_last_partition copies
    the last frame's owner map (cap entries; *n = its stripes). */
 enum { RT_PARTITION_INTERLEAVED = 0, RT_PARTITION_BALANCED = 1 };

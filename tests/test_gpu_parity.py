@@ -401,14 +401,15 @@ def test_tiles_assemble_to_full_frame(kernel, prog, tracer, pt, oracle):
         np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full))
 
 
-@pytest.mark.parametrize("n_ranks,stripe,H", [(2, 8, 53), (3, 4, 45)])
-def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt, oracle):
+@pytest.mark.parametrize("n_ranks,stripe,H,owned", [(2, 8, 53, False), (3, 4, 45, False), (3, 4, 45, True)])
+def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, owned, tracer, pt, oracle):
     """raytrace (row-shifted seeds) on row-stripe tiles over progressive frames, with the
     seed-row halo moved between contexts through device buffers (rt_pack/unpack_seed_rows,
     the path dist.exchange_seed_rows drives over RCCL): every frame reassembles bit-exactly
     to the single-device frame (itself equal to the oracle's frames and seeds), and every
     seed row equals the single-device seeds on its last writer.  Includes a restart
-    (progression back to 0)."""
+    (progression back to 0) and, with `owned`, owner-map partitions that change between frames
+    (rt_tile.stripe_owner; the halo moves the rows of the stripes that changed owner too)."""
     import torch
     from importlib import import_module
 
@@ -432,13 +433,25 @@ def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt,
     ranks = [make() for _ in range(n_ranks)]
     halo = dist.SeedHalo(H, Hp, stripe, n_ranks)
     full = np.zeros(W * H * 4, np.float32)
+    ns = (H + stripe - 1) // stripe
+    maps = [None, dist.lpt_owner(np.arange(ns)[::-1] + 1, n_ranks), np.array([(3 * s_) % n_ranks for s_ in range(ns)])]
+    owner = None
     rows = [dist.tile_rows(H, stripe, n_ranks, r) for r in range(n_ranks)]
-    tiles = [torch.zeros(len(rows[r]) * W * 4, dtype=torch.float32, device="cuda:0") for r in range(n_ranks)]
+    tiles = [torch.zeros(H * W * 4, dtype=torch.float32, device="cuda:0") for r in range(n_ranks)]
     moved = 0
     exp = np.zeros_like(full)
     sd = seeds.copy()
     try:
-        for p in [0, 1, 2, 3, 4, 0, 1, 2]:
+        for f, p in enumerate([0, 1, 2, 3, 4, 0, 1, 2]):
+            if owned:  # the partition changes between frames; a tile keeps what it holds for progression
+                new_owner = maps[f % 3]
+                if f > 0 and p > 0:  # progression mixes into the tile's previous pixels: carry them over
+                    prev = dist.assemble([t.cpu().numpy().reshape(-1, W, 4) for t in tiles], H, W, stripe, owner)
+                    for r in range(n_ranks):
+                        rr = dist.tile_rows(H, stripe, n_ranks, r, new_owner)
+                        tiles[r][: len(rr) * W * 4] = torch.from_numpy(np.ascontiguousarray(prev[rr]).reshape(-1)).cuda()
+                owner = new_owner
+                halo.set_owner(owner)
             ref.rayTrace(full, W, H, p, kernel=0)
             # raytrace's row-shifted seeds (raytracer.cl:20-30) over the same progression
             oracle.render_spheres(exp, cam, sc.main_scene(), W, H, Wp, Hp, sr, 6, p, sd)
@@ -449,9 +462,9 @@ def test_progressive_sphere_tiles_with_seed_halo(n_ranks, stripe, H, tracer, pt,
                 ranks[dst].unpackSeedRows(rws, buf)
                 moved += len(rws)
             for r in range(n_ranks):
-                ranks[r].rayTrace(tiles[r], W, H, p, kernel=0, tile=(stripe, n_ranks, r), halo=True)
+                ranks[r].rayTrace(tiles[r], W, H, p, kernel=0, tile=(stripe, n_ranks, r, owner), halo=True)
             halo.commit(p)
-            frame = dist.assemble([t.cpu().numpy().reshape(-1, W, 4) for t in tiles], H, W, stripe)
+            frame = dist.assemble([t.cpu().numpy().reshape(-1, W, 4) for t in tiles], H, W, stripe, owner)
             np.testing.assert_array_equal(bits(frame.reshape(-1)), bits(full), err_msg=f"progression {p}")
         ref_seeds = ref.getSeeds().reshape(2, Hp, Wp)
         np.testing.assert_array_equal(ref_seeds.reshape(-1), sd)

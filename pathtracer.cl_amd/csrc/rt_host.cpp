@@ -228,7 +228,6 @@ struct rt_ctx {
     /* the pilot render of a view's first frame (pilot_order): its seeds, framebuffer and counters +
        queue cursors, apart from the frame's */
     int pilot_sr = 2; /* RT_PILOT (test knob): the pilot's sampleRate, 0 = no pilot (the probe's order) */
-    int pilot_conc = 0; /* RT_PILOT_CONC (A/B): the pilot beside the list pre-pass on stream2, without lists */
     uint32_t *d_pilot_seeds = nullptr;
     float *d_pilot_out = nullptr;
     unsigned long long *d_pilot_cnt = nullptr;
@@ -989,7 +988,6 @@ try {
     }
     if (const char *v = getenv("RT_PIXEL_LISTS")) c->pixel_lists = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("RT_PILOT")) c->pilot_sr = std::max(0, std::min(8, atoi(v))); /* test knob */
-    if (const char *v = getenv("RT_PILOT_CONC")) c->pilot_conc = atoi(v);
     c->repair_slots = std::max(1u, env_u32("RT_REPAIR_SLOTS", RT_REPAIR_SLOTS)); /* test knob: the path beyond them */
     if (const char *v = getenv("RT_LIST_MB")) c->list_mb = (size_t)std::max(0L, atol(v));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1867,26 +1865,14 @@ try {
         /* a view's first frame of whole pixels: its order from a pilot render (pilot_order) */
         const bool pilot = record_iter && !a.split_chunks && c->schedule_rebuilt && c->pilot_sr > 0 && !c->counting &&
                            c->sample_rate * c->sample_rate >= kPilotMinSpp;
-        const bool pilot_beside = pilot && build_lists && c->pilot_conc;
-        if (pilot_beside) { /* on stream2, beside the list pre-pass, its camera rays through the tree */
-            if (!c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-            if (!c->ev_split0) HIPCHK(c, hipEventCreateWithFlags(&c->ev_split0, hipEventDisableTiming));
-            if (!c->ev_box) HIPCHK(c, hipEventCreateWithFlags(&c->ev_box, hipEventDisableTiming));
-            HIPCHK(c, hipEventRecord(c->ev_split0, st));
-            HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split0, 0));
-            RtTriLaunch pa = a;
-            pa.list_code = nullptr;
-            pa.list_tile = nullptr;
-            const int rp = pilot_order(c, pa, trav, blocks, c->stream2);
-            if (rp != RT_OK) return rp;
-            HIPCHK(c, hipEventRecord(c->ev_box, c->stream2));
-        }
         e = build_lists ? rt_launch_pixel_lists(a, c->d_nodes4, trav == RT_TRAV_BVH4Q ? c->d_nodes4q : nullptr,
                                                 c->d_list_code, c->d_list_tile, st)
                         : 0;
         if (e) c->list_key.clear();
-        if (pilot_beside) HIPCHK(c, hipStreamWaitEvent(st, c->ev_box, 0));
-        if (pilot && !pilot_beside && !e) {
+        /* (after the lists: the pilot's camera rays take them, as the frame's do; beside the list
+           pre-pass on a second stream, through the tree, it ordered the frame worse: 94.96 against
+           98.89 ms, profiles/r06m) */
+        if (pilot && !e) {
             const int rp = pilot_order(c, a, trav, blocks, st);
             if (rp != RT_OK) return rp;
         }

@@ -32,12 +32,10 @@ def main():
     mesh = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
     c = sc.PLY_CAMERA
     out = torch.zeros(W * H * 4, dtype=torch.float32, device="cuda:0")
-    # "N": RT_PILOT=N; "Nc": the same pilot beside the list pre-pass (RT_PILOT_CONC=1)
-    pilots = [v for v in args.pilots.replace(":", ",").split(",")]
+    pilots = [v for v in args.pilots.replace(":", ",").split(",")]  # RT_PILOT values
     tracers = {}
     for p in pilots:
-        os.environ["RT_PILOT"] = p.rstrip("c")
-        os.environ["RT_PILOT_CONC"] = "1" if p.endswith("c") else "0"
+        os.environ["RT_PILOT"] = p
         rt = pt.RayTracer(0)
         rt.setSpheres(sc.ply_scene())
         rt.setCameraSpherical(c["target"], c["elevation"], c["azimuth"], c["distance"])
@@ -49,7 +47,6 @@ def main():
             rt.rayTrace(out, W, H, 0, kernel=2)
         tracers[p] = rt
     os.environ.pop("RT_PILOT", None)
-    os.environ.pop("RT_PILOT_CONC", None)
     res = {p: {"cold_ms": [], "cold_pre_ms": [], "cold_main_ms": [], "next_ms": [], "pilot": []} for p in pilots}
     for r in range(args.rounds):
         for p in pilots:

@@ -144,9 +144,11 @@ public:
         dirty_ = true;
     }
 
-    /* ---- mesh for raytrace_tris (raytracer.cl:184-188); builds the BVH ---- */
+    /* ---- mesh for raytrace_tris (raytracer.cl:184-188); builds the BVH, its cost area leaning
+       toward the lights of the spheres added so far (uploaded first; culling only) ---- */
     void setMesh(const float *verts_xyz, unsigned n_verts, const int *idx, unsigned n_tris)
     {
+        flushScene();
         check(rt_set_mesh(ctx_, verts_xyz, n_verts, idx, n_tris), "setMesh");
     }
     void setTraversal(int traversal) { check(rt_set_traversal(ctx_, traversal), "setTraversal"); }

@@ -110,7 +110,9 @@ const char *rt_status_string(int status);
 int rt_set_spheres(rt_ctx *ctx, const rt_sphere *spheres, uint32_t n);
 
 /* ---- mesh: the tri_verts / tri_vert_idx / n_tris kernel arguments of
-   raytrace_tris (raytracer.cl:184-188); the context builds the BVH. ---- */
+   raytrace_tris (raytracer.cl:184-188); the context builds the BVH (the host build's cost area
+   leans toward the emissive spheres of the last rt_set_spheres; a later rt_set_spheres keeps the
+   tree: culling only, no result depends on it). ---- */
 int rt_set_mesh(rt_ctx *ctx, const float *verts_xyz, uint32_t n_verts, const int32_t *idx, uint32_t n_tris);
 /* BVH statistics of the current mesh. */
 typedef struct rt_mesh_stats {

@@ -1164,6 +1164,14 @@ try {
     RtBvh b;
     if (const char *v = getenv("RT_CULL_UNHITTABLE")) b.cull_unhittable = atoi(v) != 0; /* A/B knob */
     if (const char *v = getenv("RT_DET_CULL")) b.det_cull = atoi(v) != 0; /* A/B knob */
+    /* the tree leans toward the lights set when the mesh is (rt_bvh.cpp Builder::area; a later
+       setSpheres keeps the tree: culling only) */
+    for (const rt_sphere &L : c->lights) {
+        b.light_centres.push_back(L.center.x);
+        b.light_centres.push_back(L.center.y);
+        b.light_centres.push_back(L.center.z);
+    }
+    if (const char *v = getenv("RT_BVH_LIGHT_W")) b.light_cost_weight = (float)atof(v); /* A/B knob (0: surface area) */
     if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
     c->mesh_builder = RT_BUILD_HOST;

@@ -103,6 +103,8 @@ struct RtBvh {
     double build_seconds = 0.0;
     bool cull_unhittable = true; /* in: leave triangles no ray can hit out of the tree (rt_bvh.cpp never_hit) */
     bool det_cull = true;        /* in: normal boxes in the compressed nodes (rt_quant.h determinant cull) */
+    std::vector<float> light_centres; /* in: the scene's lights (3 floats each): the cost area leans toward them */
+    float light_cost_weight = 0.6f;   /* in: their share of the cost area (rt_bvh.cpp Builder::area) */
     uint32_t n_hit = 0;          /* out: triangles in the tree (slots [0, n_hit)) */
 };
 

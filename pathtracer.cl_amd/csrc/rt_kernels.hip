@@ -25,6 +25,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef RT_DIAG_RAYSPLIT
+#define RT_DIAG_RAYSPLIT 0 /* diagnostics build: counting launches sum the stepping loop's steps of shadow rays
+                              from mesh hits / shadow rays from the box / camera rays into counters 10 / 11 / 12 */
+#endif
 #ifndef RT_DIAG_MIX
 #define RT_DIAG_MIX 0 /* diagnostics build (profiles/step_mix.py): counting launches report the stepping
                          rounds' wave-step mix in the per-pixel-maximum counters */
@@ -670,7 +674,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long *dst, const un
     }
     if (with_trav) /* per-pixel maxima (RT_DIAG_MIX builds: the wave-step mix, summed) */
         for (int i = RT_N_SUM_COUNTERS; i < RT_N_COUNTERS; ++i) {
-            if (RT_DIAG_MIX) atomicAdd(&dst[i], v[i]);
+            if (RT_DIAG_MIX || RT_DIAG_RAYSPLIT) atomicAdd(&dst[i], v[i]);
             else atomicMax(&dst[i], v[i]);
         }
 }
@@ -2058,7 +2062,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                         ps[6] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)(pix_c >> 6) : 0u;
                         ps[7] = (COUNT || RT_PLAIN_PIXEL_STATS) ? (uint32_t)pix_it : 0u;
                     }
-                    if (COUNT && !RT_DIAG_MIX) {
+                    if (COUNT && !RT_DIAG_MIX && !RT_DIAG_RAYSPLIT) {
                         const unsigned long long dt = wave_clock() - pix_t0;
                         cnt[10] = dt > cnt[10] ? dt : cnt[10];
                         cnt[11] = pix_q > cnt[11] ? pix_q : cnt[11];
@@ -2310,6 +2314,10 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                             cnt[3] += tc.tests;
                             cnt[4] += tc.leaves;
                             pix_steps += tc.nodes + tc.leaves;
+                            if (RT_DIAG_RAYSPLIT) {
+                                const int k = shadow ? (tri_hit ? 10 : 11) : (depth == 0 ? 12 : -1);
+                                if (k >= 0) cnt[k] += tc.nodes + tc.leaves;
+                            }
                         } else {
                             ++pix_steps; /* (the measured cost, pixel_iter: trav_step calls) */
                         }

@@ -142,7 +142,9 @@ class RayTracer:
         self.addSphere(spheres)
 
     def setMesh(self, verts, idx) -> None:
-        """Triangle mesh for the raytrace_tris kernel; the BVH is built on the host."""
+        """Triangle mesh for the raytrace_tris kernel; the BVH is built on the host, its cost area
+        leaning toward the lights of the spheres added so far (uploaded first; culling only)."""
+        self._sync_scene()
         v = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
         i = np.ascontiguousarray(idx, np.int32).reshape(-1, 3)
         self._check(self._lib.rt_set_mesh(self._h, _abi.ptr(v), v.shape[0], _abi.ptr(i), i.shape[0]), "rt_set_mesh")

@@ -3,7 +3,7 @@ RT_SEED_WIDTH (lanes per long chain: 8-64 subtree-parallel k_chain_seeds, 3 coop
 context renders every rank's tile (best of --reps) and the slowest rank is reported, with the
 tile's frame bits checked equal across widths.
 
-    python profiles/seed_width_ab.py [--config dragon] [--n 8] [--widths 16,4,8,32] [--reps 2]
+    python profiles/seed_width_ab.py [--config dragon] [--n 8] [--widths 16,4,8,32] [--reps 2] [--balanced]
 """
 import argparse
 import json
@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--widths", default="16,4,8,32")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--balanced", action="store_true", help="the tiles under rt_partition_stripes' owner map")
     args = ap.parse_args()
     import torch
     import ptload
@@ -44,8 +45,9 @@ def main():
         rt.setMaxPathDepth(6)
         rt.setMesh(*mesh)
         times, same = [], True
+        owner = rt.partitionStripes(W, H, args.stripe, args.n) if args.balanced else None
         for r in range(args.n):
-            tile = (args.stripe, args.n, r)
+            tile = (args.stripe, args.n, r) + ((owner,) if owner is not None else ())
             best = 1e9
             for _ in range(args.reps):
                 rt.rayTrace(out, W, H, 0, kernel=2, tile=tile)

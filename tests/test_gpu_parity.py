@@ -1654,19 +1654,21 @@ def test_pilot_order_changes_no_bits(tracer, pt, oracle, monkeypatch):
 
 
 def test_tree_cull_knobs_change_no_bits(tracer, pt, monkeypatch):
-    """The host build's two culls are traversal savings only: a tree without the determinant cull's
-    normal boxes (RT_DET_CULL=0) and one that keeps the triangles no unit ray can hit
-    (RT_CULL_UNHITTABLE=0) render a frame of the dragon-class mesh (871,414 triangles, 66,533 of
-    them under the |det| >= 1e-4 rule for every unit ray, geometryFuncs.h:167) to the same bits and
-    seeds as the default tree, at sampleRate 4 with the candidate lists."""
+    """The host build's two culls and its cost area are traversal savings only: a tree without the
+    determinant cull's normal boxes (RT_DET_CULL=0), one that keeps the triangles no unit ray can hit
+    (RT_CULL_UNHITTABLE=0), and trees split by the surface area alone (RT_BVH_LIGHT_W=0) or by the
+    lights' projected area alone (1) render a frame of the dragon-class mesh (871,414 triangles,
+    66,533 of them under the |det| >= 1e-4 rule for every unit ray, geometryFuncs.h:167) to the same
+    bits and seeds as the default tree, at sampleRate 4 with the candidate lists."""
     sc = pt.scenes
     W, H, sr = 160, 120, 4
     Wp, Hp = sc.padded_dims(W, H)
     verts, idx = sc.make_mesh(sc.MESH_CONFIGS["dragon"])
     seeds = sc.default_seeds(Wp, Hp, skip=5)
     frames = []
-    for env in ({}, {"RT_DET_CULL": "0"}, {"RT_CULL_UNHITTABLE": "0"}, {"RT_DET_CULL": "0", "RT_CULL_UNHITTABLE": "0"}):
-        for k in ("RT_DET_CULL", "RT_CULL_UNHITTABLE"):
+    for env in ({}, {"RT_DET_CULL": "0"}, {"RT_CULL_UNHITTABLE": "0"}, {"RT_DET_CULL": "0", "RT_CULL_UNHITTABLE": "0"},
+                {"RT_BVH_LIGHT_W": "0"}, {"RT_BVH_LIGHT_W": "1"}):
+        for k in ("RT_DET_CULL", "RT_CULL_UNHITTABLE", "RT_BVH_LIGHT_W"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -1683,7 +1685,7 @@ def test_tree_cull_knobs_change_no_bits(tracer, pt, monkeypatch):
         rt.rayTrace(out, W, H, 0, kernel=2)
         frames.append((bits(out).copy(), rt.getSeeds().copy(), info["n_tris_tree"]))
         rt.close()
-    assert frames[0][2] < len(idx) and frames[2][2] == len(idx), [f[2] for f in frames]
+    assert frames[0][2] < len(idx) and frames[2][2] == len(idx) and frames[4][2] == frames[0][2], [f[2] for f in frames]
     for f, s_, _ in frames[1:]:
         np.testing.assert_array_equal(f, frames[0][0])
         np.testing.assert_array_equal(s_, frames[0][1])

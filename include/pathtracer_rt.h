@@ -124,6 +124,8 @@ typedef struct rt_mesh_stats {
     uint32_t builder; /* RT_BUILD_HOST or RT_BUILD_GPU */
     uint32_t n_tris_tree; /* triangles in the tree: the host build leaves out those no ray can
                              hit (|det| < 1e-4 for every unit direction, geometryFuncs.h:167) */
+    uint32_t n_nodes4_shadow; /* the shadow queries' 4-wide tree (host build with lights: its cost
+                                 area leans toward them); 0: they walk the closest-hit tree */
 } rt_mesh_stats;
 /* BVH builder used by the next rt_set_mesh: the host binned-SAH build (default: the best
    trees) or the GPU build (LBVH over Morton codes, collapsed on the device: seconds-to-

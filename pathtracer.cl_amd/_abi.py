@@ -103,7 +103,8 @@ def tile_struct(tile):
 class RtMeshStats(ctypes.Structure):
     _fields_ = [("n_tris", ctypes.c_uint32), ("n_nodes2", ctypes.c_uint32), ("depth2", ctypes.c_uint32),
                 ("n_nodes4", ctypes.c_uint32), ("depth4", ctypes.c_uint32), ("stack4", ctypes.c_uint32),
-                ("build_seconds", ctypes.c_double), ("builder", ctypes.c_uint32), ("n_tris_tree", ctypes.c_uint32)]
+                ("build_seconds", ctypes.c_double), ("builder", ctypes.c_uint32), ("n_tris_tree", ctypes.c_uint32),
+                ("n_nodes4_shadow", ctypes.c_uint32)]
 
 
 class RtCounters(ctypes.Structure):

@@ -19,11 +19,13 @@
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pathtracer_rt.h"
 #include "rt_internal.h"
 #include "rt_math.h"
+#include "rt_quant.h"
 
 namespace {
 
@@ -141,6 +143,9 @@ struct rt_ctx {
     uint32_t *d_nodes4q = nullptr; /* 4-wide tree, compressed nodes */
     float *d_tris = nullptr;
     size_t tris_cap = 0;       /* triangle records d_tris holds (mesh + camera-ray candidate lists) */
+    size_t tree_recs = 0;      /* of them the trees' triangle records: n_tris, or 2 n_tris with the shadow tree */
+    uint32_t shadow_root = 0;  /* the shadow queries' tree: its root node in d_nodes4q (0: the closest-hit tree) */
+    uint32_t n_nodes4_shadow = 0, stack4_all = 0;
     uint16_t *d_list_code = nullptr;  /* per pixel: offset in its tile's block << 5 | count - 1 (k_pixel_lists) */
     uint32_t *d_list_tile = nullptr;  /* per 8x8 tile: first slot of its block of lists */
     uint32_t *d_list_alloc = nullptr; /* the list area's allocator */
@@ -435,7 +440,7 @@ uint32_t spill_cap(const rt_ctx *c)
 {
     /* worst-case stack: the 4-wide tree's stack4 */
     const int k = trav_kind(c);
-    const uint32_t need = (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) ? c->bvh.stack4 : 0u;
+    const uint32_t need = (k == RT_TRAV_BVH4 || k == RT_TRAV_BVH4Q) ? std::max(c->bvh.stack4, c->stack4_all) : 0u;
     return need > RT_STACK_DEPTH ? need - RT_STACK_DEPTH : 0;
 }
 
@@ -1157,23 +1162,79 @@ try {
         c->bvh.stack4 = g.stack4;
         c->bvh.build_seconds = g.build_seconds;
         c->bvh.n_hit = n_tris; /* the GPU build keeps every triangle */
+        c->tree_recs = n_tris; /* one tree for every query */
+        c->shadow_root = 0;
+        c->n_nodes4_shadow = 0;
+        c->stack4_all = g.stack4;
         c->mesh_builder = RT_BUILD_GPU;
         c->mesh_bounds_ok = mesh_bounds(verts, idx, n_tris, c->mesh_lo, c->mesh_hi);
         return RT_OK;
     }
+    /* Two host trees over the same triangles: the closest-hit queries (camera rays, bounces, the
+       seed passes) walk one split by surface area, the shadow queries one whose cost area leans
+       toward the scene's lights (rt_bvh.cpp Builder::area) — three quarters of the dragon frame's
+       steps are shadow rays from mesh hits, and the lights' tree cuts them 10 %, while the long
+       chains' subtree-parallel seed pass (closest hits of box paths over a cut of the tree's top
+       levels) ran 1.3 ms slower on it (profiles/r06za).  Built side by side on two host threads;
+       the shadow tree's nodes and triangle records follow the first tree's in d_nodes4q / d_tris
+       (links offset), so a shadow query only starts at another root.  Culling only: any tree gives
+       the same hits. */
     RtBvh b;
     if (const char *v = getenv("RT_CULL_UNHITTABLE")) b.cull_unhittable = atoi(v) != 0; /* A/B knob */
     if (const char *v = getenv("RT_DET_CULL")) b.det_cull = atoi(v) != 0; /* A/B knob */
-    /* the tree leans toward the lights set when the mesh is (rt_bvh.cpp Builder::area; a later
-       setSpheres keeps the tree: culling only) */
+    RtBvh sb;
+    sb.cull_unhittable = b.cull_unhittable;
+    sb.det_cull = b.det_cull;
     for (const rt_sphere &L : c->lights) {
-        b.light_centres.push_back(L.center.x);
-        b.light_centres.push_back(L.center.y);
-        b.light_centres.push_back(L.center.z);
+        sb.light_centres.push_back(L.center.x);
+        sb.light_centres.push_back(L.center.y);
+        sb.light_centres.push_back(L.center.z);
     }
-    if (const char *v = getenv("RT_BVH_LIGHT_W")) b.light_cost_weight = (float)atof(v); /* A/B knob (0: surface area) */
-    if (!rt_build_bvh(verts, n_verts, idx, n_tris, b, err))
+    if (const char *v = getenv("RT_BVH_LIGHT_W")) sb.light_cost_weight = (float)atof(v); /* A/B knob (0: one tree) */
+    b.light_cost_weight = 0.0f;
+    bool two = !sb.light_centres.empty() && sb.light_cost_weight > 0.0f && 2ull * n_tris < (1ull << 28);
+    bool ok2 = false;
+    std::string err2;
+    std::thread th;
+    if (two)
+        th = std::thread([&]() {
+            try {
+                ok2 = rt_build_bvh(verts, n_verts, idx, n_tris, sb, err2);
+            } catch (...) {
+                ok2 = false;
+            }
+        });
+    bool ok = false;
+    try {
+        ok = rt_build_bvh(verts, n_verts, idx, n_tris, b, err);
+    } catch (...) {
+        if (th.joinable()) th.join();
+        throw;
+    }
+    if (th.joinable()) th.join();
+    if (!ok)
         return fail(c, err.find("deeper") != std::string::npos ? RT_ERR_LIMIT : RT_ERR_ARG, err);
+    two = two && ok2 && !b.nodes4q.empty() && !sb.nodes4q.empty();
+    std::vector<uint32_t> q4 = std::move(b.nodes4q);
+    std::vector<float> tr = std::move(b.tris);
+    const uint32_t n_a = b.n_nodes4;
+    if (two) {
+        q4.insert(q4.end(), sb.nodes4q.begin(), sb.nodes4q.end());
+        for (size_t i = n_a; i < (size_t)n_a + sb.n_nodes4; ++i)
+            for (int k = 0; k < 4; ++k) {
+                uint32_t &w = q4[i * RT_QNODE_DWORDS + 12 + k]; /* the explicit child links (rt_quant.h) */
+                int32_t code = (int32_t)w;
+                if (code == RT_EMPTY_CHILD) continue;
+                if (code >= 0) {
+                    code += (int32_t)n_a;
+                } else {
+                    const uint32_t enc = (uint32_t)(~code);
+                    code = ~(int32_t)((((enc >> 3) + n_tris) << 3) | (enc & 7u));
+                }
+                w = (uint32_t)code;
+            }
+        tr.insert(tr.end(), sb.tris.begin(), sb.tris.end());
+    }
     c->mesh_builder = RT_BUILD_HOST;
     free_dev(c->d_nodes4);
     free_dev(c->d_nodes4q);
@@ -1182,14 +1243,17 @@ try {
     c->d_nodes4q = nullptr;
     c->n_tris = 0;
     HIPCHK(c, hipMalloc(&c->d_nodes4, b.nodes4.size() * sizeof(float)));
-    if (!b.nodes4q.empty()) HIPCHK(c, hipMalloc(&c->d_nodes4q, b.nodes4q.size() * sizeof(uint32_t)));
-    HIPCHK(c, hipMalloc(&c->d_tris, b.tris.size() * sizeof(float)));
-    c->tris_cap = b.tris.size() / 12;
+    if (!q4.empty()) HIPCHK(c, hipMalloc(&c->d_nodes4q, q4.size() * sizeof(uint32_t)));
+    HIPCHK(c, hipMalloc(&c->d_tris, tr.size() * sizeof(float)));
+    c->tris_cap = tr.size() / 12;
     HIPCHK(c, hipMemcpy(c->d_nodes4, b.nodes4.data(), b.nodes4.size() * sizeof(float), hipMemcpyHostToDevice));
-    if (!b.nodes4q.empty())
-        HIPCHK(c, hipMemcpy(c->d_nodes4q, b.nodes4q.data(), b.nodes4q.size() * sizeof(uint32_t),
-                            hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->d_tris, b.tris.data(), b.tris.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (!q4.empty())
+        HIPCHK(c, hipMemcpy(c->d_nodes4q, q4.data(), q4.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_tris, tr.data(), tr.size() * sizeof(float), hipMemcpyHostToDevice));
+    c->tree_recs = tr.size() / 12;
+    c->shadow_root = two ? n_a : 0u;
+    c->n_nodes4_shadow = two ? sb.n_nodes4 : 0u;
+    c->stack4_all = two ? std::max(b.stack4, sb.stack4) : b.stack4;
     c->n_tris = n_tris;
     c->mesh_serial++;
     c->bvh.n_nodes = b.n_nodes;
@@ -1211,6 +1275,7 @@ try {
     out->n_tris = c->n_tris;
     out->n_nodes2 = c->bvh.n_nodes;
     out->depth2 = c->bvh.depth;
+    out->n_nodes4_shadow = c->n_nodes4_shadow;
     out->n_nodes4 = c->bvh.n_nodes4;
     out->depth4 = c->bvh.depth4;
     out->stack4 = c->bvh.stack4;
@@ -1600,6 +1665,7 @@ try {
         a.out = dout;
         a.seeds = c->d_seeds;
         a.nodes = trav_nodes(c);
+        a.shadow_root = trav_kind(c) == RT_TRAV_BVH4Q ? c->shadow_root : 0u; /* the shadow tree: compressed nodes only */
         a.tris = c->d_tris;
         a.n_tris = c->n_tris;
         a.lights = c->d_lights;
@@ -1797,7 +1863,7 @@ try {
         a.list_code = nullptr;
         a.list_tile = nullptr;
         const bool bvh4 = c->d_nodes4 && (trav == RT_TRAV_BVH4Q || trav == RT_TRAV_BVH4);
-        const uint64_t kept = (c->n_tris + 7ull) & ~7ull; /* the list area starts on a 128-B line */
+        const uint64_t kept = (c->tree_recs + 7ull) & ~7ull; /* the list area starts on a 128-B line, after the trees' records */
         const uint64_t npx = (uint64_t)W * hl;
         uint64_t list_cap = std::min<uint64_t>(npx * RT_LIST_MAX, ((uint64_t)c->list_mb << 20) / 48);
         list_cap = std::min<uint64_t>(list_cap, kept < (1ull << 28) ? (1ull << 28) - 8 - kept : 0);
@@ -1831,7 +1897,7 @@ try {
            (bunny class 1024^2 at 1 spp: a 2.4-ms pre-pass against a 1.0-ms frame) */
         bool lists = (c->pixel_lists == 1 || (c->pixel_lists < 0 && (c->sample_rate >= 4 || same_view))) && bvh4 &&
                      list_cap > 0;
-        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), c->n_tris, st, list_shrink) != RT_OK) {
+        if (lists && ensure_tris_capacity(c, (size_t)(kept + list_cap), c->tree_recs, st, list_shrink) != RT_OK) {
             (void)hipGetLastError(); /* out of device memory: no lists this render */
             lists = false;
         }

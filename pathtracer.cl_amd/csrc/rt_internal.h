@@ -139,6 +139,7 @@ struct RtTriLaunch {
     float *out;
     uint32_t *seeds;
     const float *nodes;
+    uint32_t shadow_root; /* the shadow queries' root node (BVH4Q: the lights' tree after the closest-hit tree's nodes; 0: one tree) */
     const float *tris;
     uint32_t n_tris;
     const rt_sphere *lights; /* emissive spheres only, scene order */

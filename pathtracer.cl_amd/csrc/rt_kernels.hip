@@ -2257,6 +2257,7 @@ __global__ __launch_bounds__(RT_BLOCK, RT_TRIS_WAVES) void k_tris(RtTriLaunch a)
                     ++cnt[RT_CNT_SKIPPED];
                 } else {
                     trav_begin(ts, stk, qo, qd, qt);
+                    if (shadow) ts.node = (int)a.shadow_root; /* the shadow queries' tree */
                     running = true;
                     if (!shadow && depth == 0) { /* a camera ray: the pixel's candidate list */
                         const uint32_t lpack = s_list[threadIdx.x];

@@ -59,6 +59,7 @@ def main():
         steps, box = st[m, 2], st[m, 3]
         order = np.argsort(-dur)[:12]
         res[name] = {"pixels": int(m.sum()), "end_ms_max": round(float(end.max()), 2),
+                     "end_ms": {q: round(float(np.quantile(end, q / 100)), 2) for q in (50, 70, 80, 90, 95, 99, 100)},
                      "dur_ms": {q: round(float(np.quantile(dur, q / 100)), 2) for q in (50, 90, 99, 100)},
                      "steps": {q: int(np.quantile(steps, q / 100)) for q in (50, 90, 99, 100)},
                      "missed_camera_rays": {q: int(np.quantile(box, q / 100)) for q in (50, 90, 99, 100)},

@@ -1656,8 +1656,8 @@ def test_pilot_order_changes_no_bits(tracer, pt, oracle, monkeypatch):
 def test_tree_cull_knobs_change_no_bits(tracer, pt, monkeypatch):
     """The host build's two culls and its cost area are traversal savings only: a tree without the
     determinant cull's normal boxes (RT_DET_CULL=0), one that keeps the triangles no unit ray can hit
-    (RT_CULL_UNHITTABLE=0), and trees split by the surface area alone (RT_BVH_LIGHT_W=0) or by the
-    lights' projected area alone (1) render a frame of the dragon-class mesh (871,414 triangles,
+    (RT_CULL_UNHITTABLE=0), and shadow rays on the closest-hit tree (RT_BVH_LIGHT_W=0: one tree)
+    or on a tree split by the lights' projected area alone (1) render a frame of the dragon-class mesh (871,414 triangles,
     66,533 of them under the |det| >= 1e-4 rule for every unit ray, geometryFuncs.h:167) to the same
     bits and seeds as the default tree, at sampleRate 4 with the candidate lists."""
     sc = pt.scenes
@@ -1683,10 +1683,11 @@ def test_tree_cull_knobs_change_no_bits(tracer, pt, monkeypatch):
         rt.setSeeds(Wp, Hp, seeds)
         out = np.zeros(W * H * 4, np.float32)
         rt.rayTrace(out, W, H, 0, kernel=2)
-        frames.append((bits(out).copy(), rt.getSeeds().copy(), info["n_tris_tree"]))
+        frames.append((bits(out).copy(), rt.getSeeds().copy(), info["n_tris_tree"], info["n_nodes4_shadow"]))
         rt.close()
     assert frames[0][2] < len(idx) and frames[2][2] == len(idx) and frames[4][2] == frames[0][2], [f[2] for f in frames]
-    for f, s_, _ in frames[1:]:
+    assert frames[0][3] > 0 and frames[4][3] == 0 and frames[5][3] > 0, [f[3] for f in frames]  # the shadow tree built
+    for f, s_, _, _ in frames[1:]:
         np.testing.assert_array_equal(f, frames[0][0])
         np.testing.assert_array_equal(s_, frames[0][1])
 

@@ -3041,8 +3041,25 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                 const double le1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
                 const double le2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
                 const double terr = sqrt(tf2) * (2e-6 * le1 * le2 * l1 / 1e-4 + 1e-6) * l1 + 1e-5;
+                /* the float t estimates the exact ray parameter of the triangle's plane, q / (N . d)
+                   with q = N . (v0 - o): over the direction box N . d lies in [mlo, mhi], so where
+                   that keeps one sign with q, t >= q / mhi (q, mlo > 0) or q / mlo (q, mhi < 0) —
+                   for a triangle facing the pixel far later than its box's entry */
+                double tpl = -1e300;
+                {
+                    double mlo = 0.0, mhi = 0.0, q = 0.0;
+                    for (int k = 0; k < 3; ++k) {
+                        const double a0 = nv[k] * dlo[k], a1 = nv[k] * dhi[k];
+                        mlo += fmin(a0, a1);
+                        mhi += fmax(a0, a1);
+                        q += nv[k] * ((double)(k == 0 ? r0.x : k == 1 ? r0.y : r0.z) - olo[k]);
+                    }
+                    const double qe = 1e-12 * (fabs(nv[0]) + fabs(nv[1]) + fabs(nv[2])) * (1.0 + sqrt(tf2));
+                    if (mlo > 0.0 && q - qe > 0.0) tpl = (q - qe) / (mhi * (1.0 + 1e-12));
+                    else if (mhi < 0.0 && q + qe < 0.0) tpl = (q + qe) / (mlo * (1.0 + 1e-12));
+                }
                 slots[n] = s;
-                keys[n] = __double2float_rd(tin - terr);
+                keys[n] = __double2float_rd(fmax(tin, tpl) - terr);
                 ++n;
             }
         }

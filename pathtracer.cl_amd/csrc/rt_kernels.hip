@@ -2775,7 +2775,92 @@ struct Frustum {
     double dlo[3], dhi[3]; /* their directions (component-wise interval) */
     double ilo[3], ihi[3]; /* 1 / dlo, 1 / dhi */
     double l1;             /* max |d|_1 */
+    /* the pixel in the camera's own coordinates: P - o = s0 view + s1 right + s2 up (minv: that
+       basis inverted), a ray of the pixel through P has a = s1 / s0 in [a0, a1], b = s2 / s0 in
+       [b0, b1] (pixel_square); proj false: no such test */
+    double minv[9];
+    double a0, a1, b0, b1;
+    bool proj;
 };
+
+/* The pixel's square in the camera's (a, b) coordinates, padded for the float evaluation of
+   camera_dir: its rays are o + t (view + right a + up b) exactly for a in [ax, ax + 1], b in
+   [by, by + 1] (the strat_rand offsets, raytracer.cl:216-224; the subtraction of W / 2 is exact),
+   and the float direction strays from that ray by a few ulp of |view| + |right a| + |up b|,
+   which moves (a, b) by that over |right| or |up| plus (|a| + |b|) times it over |view|: the pad
+   covers it 20 times over. */
+__device__ __forceinline__ void pixel_square(Frustum &f, const rt_camera &cam, float ax, float by)
+{
+    const double c[3][3] = {{cam.view.x, cam.right.x, cam.up.x}, {cam.view.y, cam.right.y, cam.up.y},
+                            {cam.view.z, cam.right.z, cam.up.z}};
+    const double det = c[0][0] * (c[1][1] * c[2][2] - c[1][2] * c[2][1]) - c[0][1] * (c[1][0] * c[2][2] - c[1][2] * c[2][0]) +
+                       c[0][2] * (c[1][0] * c[2][1] - c[1][1] * c[2][0]);
+    const double nv = sqrt(c[0][0] * c[0][0] + c[1][0] * c[1][0] + c[2][0] * c[2][0]);
+    const double nr = sqrt(c[0][1] * c[0][1] + c[1][1] * c[1][1] + c[2][1] * c[2][1]);
+    const double nu = sqrt(c[0][2] * c[0][2] + c[1][2] * c[1][2] + c[2][2] * c[2][2]);
+    f.proj = fabs(det) > 1e-6 * nv * nr * nu && fmin(nr, nu) > 0.0 &&
+             (double)cam.view.w == 0.0 && (double)cam.right.w == 0.0 && (double)cam.up.w == 0.0;
+    if (!f.proj) return;
+    const double id = 1.0 / det;
+    f.minv[0] = (c[1][1] * c[2][2] - c[1][2] * c[2][1]) * id;
+    f.minv[1] = (c[0][2] * c[2][1] - c[0][1] * c[2][2]) * id;
+    f.minv[2] = (c[0][1] * c[1][2] - c[0][2] * c[1][1]) * id;
+    f.minv[3] = (c[1][2] * c[2][0] - c[1][0] * c[2][2]) * id;
+    f.minv[4] = (c[0][0] * c[2][2] - c[0][2] * c[2][0]) * id;
+    f.minv[5] = (c[0][2] * c[1][0] - c[0][0] * c[1][2]) * id;
+    f.minv[6] = (c[1][0] * c[2][1] - c[1][1] * c[2][0]) * id;
+    f.minv[7] = (c[0][1] * c[2][0] - c[0][0] * c[2][1]) * id;
+    f.minv[8] = (c[0][0] * c[1][1] - c[0][1] * c[1][0]) * id;
+    const double mag = nv + nr * (fabs((double)ax) + 1.0) + nu * (fabs((double)by) + 1.0);
+    const double pad = 0.01 + 64.0 * 0x1p-24 * mag * (1.0 / fmin(nr, nu) + (fabs((double)ax) + fabs((double)by) + 2.0) / nv);
+    f.a0 = (double)ax - pad;
+    f.a1 = (double)ax + 1.0 + pad;
+    f.b0 = (double)by - pad;
+    f.b1 = (double)by + 1.0 + pad;
+}
+
+/* Can a camera ray of the pixel meet the triangle v0 + u e1 + v e2 (the record's float values, as
+   mt_test reads them) where the float test could accept?  The triangle is widened to u, v >= -eps,
+   u + v <= 1 + 2 eps, eps bounding the float test's barycentric error (a few ulp of |e| |o - v0|
+   and |e1| |e2| over |det| >= 1e-4, 7x margin), projected through the camera onto the pixel's
+   (a, b) plane, and tested against the padded square by separating axes (the square's two and the
+   triangle's three edge normals).  A vertex at or behind the camera's plane keeps the triangle.
+   Culling only; false means no ray of the pixel can accept it. */
+__device__ __forceinline__ bool tri_meets_pixel(const Frustum &f, float4 r0, float4 r1, float4 r2, double dist)
+{
+    if (!f.proj) return true;
+    const double e1[3] = {r1.x, r1.y, r1.z}, e2[3] = {r2.x, r2.y, r2.z};
+    const double n1 = fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2]), n2 = fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2]);
+    const double eps = 8.0 * 16.0 * 0x1p-24 * ((n1 + n2) * dist + n1 * n2) / 1e-4 + 1e-6;
+    const double uv[3][2] = {{-eps, -eps}, {1.0 + 3.0 * eps, -eps}, {-eps, 1.0 + 3.0 * eps}};
+    double pa[3], pb[3];
+    for (int i = 0; i < 3; ++i) {
+        double q[3];
+        for (int k = 0; k < 3; ++k)
+            q[k] = ((double)(k == 0 ? r0.x : k == 1 ? r0.y : r0.z) + uv[i][0] * e1[k] + uv[i][1] * e2[k]) - f.o[k];
+        const double s0 = f.minv[0] * q[0] + f.minv[1] * q[1] + f.minv[2] * q[2];
+        const double s1 = f.minv[3] * q[0] + f.minv[4] * q[1] + f.minv[5] * q[2];
+        const double s2 = f.minv[6] * q[0] + f.minv[7] * q[1] + f.minv[8] * q[2];
+        if (!(s0 > 1e-9 * (fabs(s1) + fabs(s2) + fabs(s0)))) return true; /* at or behind the camera's plane */
+        pa[i] = s1 / s0;
+        pb[i] = s2 / s0;
+    }
+    if (fmax(pa[0], fmax(pa[1], pa[2])) < f.a0 || fmin(pa[0], fmin(pa[1], pa[2])) > f.a1) return false;
+    if (fmax(pb[0], fmax(pb[1], pb[2])) < f.b0 || fmin(pb[0], fmin(pb[1], pb[2])) > f.b1) return false;
+    const double cx[4] = {f.a0, f.a1, f.a0, f.a1}, cy[4] = {f.b0, f.b0, f.b1, f.b1};
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        double nx = -(pb[j] - pb[i]), ny = pa[j] - pa[i];
+        if (nx * (pa[k] - pa[i]) + ny * (pb[k] - pb[i]) < 0.0) {
+            nx = -nx;
+            ny = -ny;
+        }
+        bool out = true;
+        for (int q = 0; q < 4 && out; ++q) out = nx * (cx[q] - pa[i]) + ny * (cy[q] - pb[i]) < 0.0;
+        if (out) return false;
+    }
+    return true;
+}
 
 __device__ __forceinline__ void frustum_init(Frustum &f)
 {
@@ -2926,6 +3011,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_pixel_lists(RtTriLaunch a, const f
         const float ax = (float)x - ((float)a.W) / 2.0f, by = (float)y - ((float)a.H) / 2.0f;
         Frustum f;
         pixel_dir_box(a.cam, ax, by, f.dlo, f.dhi);
+        pixel_square(f, a.cam, ax, by);
         for (int k = 0; k < 3; ++k) f.o[k] = k == 0 ? a.cam.position.x : k == 1 ? a.cam.position.y : a.cam.position.z;
         frustum_init(f);
         ok = frustum_list(nodes4, q4, tris, f, slot, key, RT_LIST_MAX, n, (lds_int *)(s_fstack + threadIdx.x));
@@ -3026,6 +3112,12 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                                       e2[0] * e1[1] - e2[1] * e1[0]};
                 const double el = (fabs(e1[0]) + fabs(e1[1]) + fabs(e1[2])) * (fabs(e2[0]) + fabs(e2[1]) + fabs(e2[2]));
                 if (frustum_det(dlo, dhi, nv, nv) * (1.0 + 1e-6) + 8.0 * 0x1p-24 * l1 * el < 1e-4) continue;
+                double tf2 = 0.0;
+                for (int k = 0; k < 3; ++k) {
+                    const double u = fmax(fabs(lo[k] - olo[k]), fabs(hi[k] - olo[k]));
+                    tf2 += u * u;
+                }
+                if (!tri_meets_pixel(fr, r0, r1, r2, sqrt(tf2))) continue;
                 if (n >= cap) {
                     ok = false;
                     break;
@@ -3033,11 +3125,6 @@ __device__ bool frustum_list(const float *__restrict__ nodes4, const uint32_t *_
                 /* the earliest t any ray could accept this triangle at: the box entry less the
                    error of the float t (relative ~gamma |e1| |e2| |d| / |det|, |det| >= 1e-4;
                    30x margin), at the farthest t the box allows; kept in the spare r1.w */
-                double tf2 = 0.0;
-                for (int k = 0; k < 3; ++k) {
-                    const double u = fmax(fabs(lo[k] - olo[k]), fabs(hi[k] - olo[k]));
-                    tf2 += u * u;
-                }
                 const double le1 = sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
                 const double le2 = sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
                 const double terr = sqrt(tf2) * (2e-6 * le1 * le2 * l1 / 1e-4 + 1e-6) * l1 + 1e-5;

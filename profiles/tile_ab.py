@@ -42,9 +42,10 @@ def child(args):
     ptdist = ptload.submodule("dist")
     times, h = [], hashlib.sha1()
     ranks = range(args.n) if args.n > 1 else [0]
+    owner = rt.partitionStripes(W, H, 8, args.n) if args.balanced and args.n > 1 else None
     for r in ranks:
-        tile = (8, args.n, r) if args.n > 1 else None
-        rows = len(ptdist.tile_rows(H, 8, args.n, r)) if args.n > 1 else H
+        tile = ((8, args.n, r) + ((owner,) if owner is not None else ())) if args.n > 1 else None
+        rows = len(ptdist.tile_rows(H, 8, args.n, r, owner)) if args.n > 1 else H
         out = torch.zeros(rows * W * 4, dtype=torch.float32, device="cuda:0")
         best = 1e9
         for _ in range(args.reps):
@@ -72,6 +73,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--frame", action="store_true", help="also time the whole frame (best of --reps)")
+    ap.add_argument("--balanced", action="store_true", help="the tiles under rt_partition_stripes' owner map")
     ap.add_argument("--env", action="append", default=[])
     ap.add_argument("--child", action="store_true")
     ap.add_argument("--lib", default="")
@@ -85,7 +87,7 @@ def main():
             label, _, path = spec.partition("=")
             path, _, envs = path.partition("?")  # LABEL=path?K=V+K2=V2: that child's environment too
             cmd = [sys.executable, "-u", __file__, "--child", "--lib", path, "--n", str(args.n), "--reps",
-                   str(args.reps)] + (["--frame"] if args.frame else []) + sum(
+                   str(args.reps)] + (["--frame"] if args.frame else []) + (["--balanced"] if args.balanced else []) + sum(
                        (["--env", e] for e in args.env + [kv for kv in envs.split("+") if kv]), [])
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
             if r.returncode != 0:

@@ -629,7 +629,7 @@ int spec_setup(rt_ctx *c, RtTriLaunch &a, size_t npx, hipStream_t st)
 bool hit_depth_on(const rt_ctx *c, const RtTriLaunch &t)
 {
     (void)c;
-    return t.split_coop >= 8 && !t.split_restart && t.split_chunk == 1u && t.max_depth < 255u;
+    return (t.split_coop >= 8 || t.split_coop == RT_SEED_COOP4) && !t.split_restart && t.split_chunk == 1u && t.max_depth < 255u;
 }
 
 /* A sample-split render: the box pixels' seed pass, their chunks and their in-order sums on
@@ -653,10 +653,11 @@ int split_render(rt_ctx *c, const RtTriLaunch &a, int blocks, hipStream_t st)
         b.split_chunks = (a.sample_rate * a.sample_rate + b.split_chunk - 1u) / b.split_chunk;
         HIPCHK(c, hipEventRecord(c->ev_split0, st));
         HIPCHK(c, hipStreamWaitEvent(c->stream2, c->ev_split0, 0));
-        if (a.split_coop >= 8) {
-            /* the subtree-parallel pass stores a long chain's seed every RT_LONG_FINE samples into
-               a buffer of its own, by slot: their chunk tasks are that short, so the long chains'
-               last chunks (box paths, the costliest samples) do not trail the frame */
+        if (a.split_coop >= 8 || a.split_coop == RT_SEED_COOP4) {
+            /* the long chains' pass (subtree-parallel or cooperative) stores a chain's seed every
+               RT_LONG_FINE samples into a buffer of its own, by slot, and each sample's mesh-hit
+               depth: their chunk tasks are that short, so the long chains' last chunks (box paths,
+               the costliest samples) do not trail the tile */
             const uint32_t spp = a.sample_rate * a.sample_rate;
             b.split_fine = RT_LONG_FINE;
             b.split_chunk = RT_LONG_FINE;

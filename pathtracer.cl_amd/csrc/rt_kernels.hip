@@ -978,6 +978,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
     const float bw = (float)RT_BOX_WIDTH, bh = (float)RT_BOX_HEIGHT;
     bool have = false, next = false, running = false, fin = false, drained = false;
     uint32_t x = 0, yl = 0, sample = 0, depth = 0;
+    uint32_t pslot = 0; /* the chain's seeds: its pixel, or its slot (split_seed_slot) */
     uint32_t lpack = RT_LPACK_NONE; /* the pixel's candidate list (list_pack) */
     uint32_t bnext = 0, bend = 0; /* the wave's batch of queue items (batch_take) */
     Seed seed = {0u, 0u};
@@ -1015,6 +1016,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         const uint32_t p = a.split_box[a.split_item_base + item];
                         x = p % a.W;
                         yl = p / a.W;
+                        pslot = a.split_seed_slot ? item : p;
                         take = true;
                     } else {
                         uint32_t tile = item >> 6;
@@ -1024,6 +1026,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                         yl = (tile / tiles_x) * 8u + (in >> 3);
                         take = x < a.W && yl < a.Hl;
                         if (take && a.split_which == RT_SPLIT_MESH) take = a.pixel_class[(size_t)yl * a.W + x] == -1;
+                        pslot = yl * a.W + x;
                     }
                     if (take) {
                         const uint32_t slot = global_row(a, yl) * a.Wpad + x;
@@ -1062,7 +1065,7 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 next = false;
                 if ((sample == spp || sample % fine == 0u) && lane == gbase) {
                     const uint32_t c = sample == spp ? nseed - 1u : sample / fine;
-                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)(yl * a.W + x) * nseed + c] = make_uint2(seed.x, seed.y);
+                    reinterpret_cast<uint2 *>(a.split_seed)[(size_t)pslot * nseed + c] = make_uint2(seed.x, seed.y);
                 }
                 if (sample == spp) {
                     have = false;
@@ -1133,7 +1136,8 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                 fin = false;
                 if (RT_SEED_STATS && q_steps == 0) ++st_imm; /* answered without a round */
                 bool sample_done = true;
-                if ((COOP ? cq.best : ts.best) >= 0) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
+                const bool mesh_hit = (COOP ? cq.best : ts.best) >= 0;
+                if (mesh_hit) { /* mesh hit: the light samples' draws, no bounce (rtcommon.h:411-421) */
                     for (uint32_t l = 0; l < nl; ++l) {
                         (void)frand(seed);
                         (void)frand(seed);
@@ -1179,6 +1183,9 @@ __device__ __forceinline__ void seed_pass(const RtTriLaunch &a, int *s_stack)
                     }
                 }
                 if (sample_done) {
+                    /* the sample's mesh-hit depth (0xff: only the box), as k_chain_seeds stores it */
+                    if (a.split_hit_depth && lane == gbase)
+                        a.split_hit_depth[(size_t)pslot * spp + sample] = mesh_hit ? (uint8_t)depth : (uint8_t)0xffu;
                     ++sample;
                     next = true;
                 }

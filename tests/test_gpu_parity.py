@@ -1212,9 +1212,9 @@ def test_sample_split_vs_oracle(tracer, pt, oracle, monkeypatch, sr, width):
         assert info["split_chunks"] == (spp + csz - 1) // csz
         # the long chains ran on their own stream with `width` lanes per chain
         assert info["pixels_long"] > 0 and info["split_coop"] == width and info["split_guard"] == 0, info
-        # subtree-parallel long chains: their chunk tasks answer the box segments from the seed
-        # pass's per-sample mesh-hit depths (no traversal for them)
-        assert info["split_hit_depth"] == (1 if width >= 8 else 0), info
+        # the long chains' chunk tasks (single samples, either pass form) answer the box segments
+        # from the seed pass's per-sample mesh-hit depths (no traversal for them)
+        assert info["split_hit_depth"] == 1, info
         # the view's second frame: its tiles re-sorted by the first frame's measured chunk costs
         # (frames of >= 16 samples per pixel)
         assert info["schedule_measured"] == (1 if p == 1 and spp >= 16 else 0), info

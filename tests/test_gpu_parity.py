@@ -1101,6 +1101,47 @@ def test_pixel_candidate_lists_small_wide_frames(pt, oracle, monkeypatch):
             assert 0 < info["list_pixels_tree"] and info["list_records"] <= info["list_capacity"], info
 
 
+def test_pixel_candidate_lists_skewed_cameras(pt, oracle, monkeypatch):
+    """The lists' pixel-square culling (k_pixel_lists: a candidate's widened triangle projected
+    through the camera basis onto the pixel's (a, b) square) with camera bases the spherical camera
+    never makes: right skewed toward up, up stretched, view off-axis (a general basis, inverted
+    per pixel), and a basis with nonzero w lanes (camera_dir normalises over four lanes; the
+    projection test is then skipped) — lists forced on, sampleRate 2, equal to the oracle."""
+    sc = pt.scenes
+    W, H = 48, 40
+    Wp, Hp = sc.padded_dims(W, H)
+    verts, idx = sc.make_mesh(20_000)
+    c = dict(sc.PLY_CAMERA)
+    c["distance"] = 3.4
+    base = sc.camera_spherical(W, fov=60.0, **c).reshape(4, 4).astype(np.float32)
+    view, up, right = base[0].copy(), base[1].copy(), base[2].copy()
+    skewed = base.copy()
+    skewed[2] = right + np.float32(0.3) * up          # right leans toward up
+    skewed[1] = up * np.float32(1.7)                   # up stretched
+    skewed[0] = view + np.float32(0.2) * W * right     # the view axis off the frame's centre
+    wlanes = base.copy()
+    wlanes[0, 3], wlanes[1, 3], wlanes[2, 3] = np.float32(0.5), np.float32(0.01), np.float32(-0.02)
+    monkeypatch.setenv("RT_PIXEL_LISTS", "1")
+    for name, cam in (("skewed", skewed), ("w lanes", wlanes)):
+        cam = np.ascontiguousarray(cam.reshape(16), np.float32)
+        seeds = sc.default_seeds(Wp, Hp, skip=7)
+        exp = np.zeros(W * H * 4, np.float32)
+        oracle.render_tris(exp, cam, sc.ply_scene(), W, H, Wp, Hp, 2, 6, 0, seeds.copy(), verts, idx)
+        rt = pt.RayTracer(0)
+        rt.setSpheres(sc.ply_scene())
+        rt.setCamera(cam)
+        rt.setSampleRate(2)
+        rt.setMaxPathDepth(6)
+        rt.setMesh(verts, idx)
+        rt.setSeeds(Wp, Hp, seeds)
+        got = np.zeros(W * H * 4, np.float32)
+        rt.rayTrace(got, W, H, 0, kernel=2)
+        info = rt.renderInfo()
+        rt.close()
+        assert info["lists"] == 1, info
+        np.testing.assert_array_equal(bits(got), bits(exp), err_msg=name)
+
+
 def test_candidate_lists_reused_across_frames(pt, oracle, monkeypatch):
     """The candidate lists depend only on camera, mesh / tree, frame and tile: frames of one
     view reuse them (rt_render_info.lists_rebuilt 0) and a camera move rebuilds them.  Every

@@ -38,7 +38,8 @@ int rt_exception_status(std::string *err) noexcept;
 #define RT_PROBE_HIT_SHIFT 27
 #define RT_PROBE_STEP_MASK ((1u << RT_PROBE_HIT_SHIFT) - 1u)
 #ifndef RT_STEP_UNROLL
-#define RT_STEP_UNROLL 6 /* traversal steps per exit check in k_tris (3 / 4 / 6: 176.3 / 174.0 / 173.4 ms) */
+#define RT_STEP_UNROLL 4 /* traversal steps per exit check in k_tris (round 6, dragon frame: 3 / 4 / 5 / 6 / 8:
+                            76.8 / 76.3-76.5 / 77.2 / 77.6-77.8 / 80.4 ms, profiles/r06zz; r01: 6 best) */
 #endif
 #ifndef RT_DIAG_ONE_PIXEL
 #define RT_DIAG_ONE_PIXEL 0 /* diagnostics build: k_tris renders only the pixel RT_DIAG_PIXEL=x,y names (the
